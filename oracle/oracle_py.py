@@ -1,0 +1,121 @@
+"""ctypes binding of the CPU restatement (libngs_oracle.so). TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libngs_oracle.so")
+_lib = None
+
+
+def build() -> None:
+    subprocess.run(["make", "-s", "-C", HERE, "all"], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        L.ngo_build.restype = C.c_void_p
+        L.ngo_build.argtypes = [C.POINTER(C.c_char_p), C.c_uint64, C.c_uint16, C.POINTER(C.c_float)]
+        L.ngo_free.argtypes = [C.c_void_p]
+        L.ngo_indexed.argtypes = [C.c_void_p]
+        L.ngo_size.restype = C.c_uint64
+        L.ngo_size.argtypes = [C.c_void_p]
+        L.ngo_libsize.restype = C.c_uint64
+        L.ngo_libsize.argtypes = [C.c_void_p]
+        L.ngo_nkeys.restype = C.c_uint32
+        L.ngo_nkeys.argtypes = [C.c_void_p]
+        L.ngo_key.restype = C.POINTER(C.c_char)
+        L.ngo_key.argtypes = [C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32)]
+        L.ngo_set_valid.argtypes = [C.c_void_p, C.c_char_p, C.c_int]
+        L.ngo_search.restype = C.c_uint32
+        L.ngo_search.argtypes = [C.c_void_p, C.c_char_p, C.c_float, C.c_uint32, C.POINTER(C.c_uint32),
+                                 C.POINTER(C.c_float), C.c_uint32]
+        L.ngo_search_batch.argtypes = [C.c_void_p, C.POINTER(C.c_char_p), C.c_uint32, C.c_float, C.c_uint32,
+                                       C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_float),
+                                       C.c_uint32, C.c_int]
+        _lib = L
+    return _lib
+
+
+def _words_array(words):
+    arr = (C.c_char_p * max(1, len(words)))()
+    for i, w in enumerate(words):
+        arr[i] = None if w is None else (w if isinstance(w, bytes) else w.encode("latin-1"))
+    return arr
+
+
+class OracleIndex:
+    """CPU restatement of StringSearch::StringIndex (nGramSearch.h:104)."""
+
+    def __init__(self, words, row_size: int = 1, weights=None):
+        L = lib()
+        self._words = _words_array(words)  # keep alive during build
+        w = None
+        if weights is not None:
+            w = (C.c_float * max(1, len(weights)))(*weights)
+        self.h = L.ngo_build(self._words if words else None, len(words), row_size, w)
+        self._keys: dict[int, bytes] = {}
+
+    def close(self):
+        if self.h:
+            lib().ngo_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def size(self) -> int:
+        return lib().ngo_size(self.h)
+
+    def lib_size(self) -> int:
+        return lib().ngo_libsize(self.h)
+
+    def n_keys(self) -> int:
+        return lib().ngo_nkeys(self.h)
+
+    def key(self, k: int) -> bytes:
+        if k not in self._keys:
+            n = C.c_uint32()
+            p = lib().ngo_key(self.h, k, C.byref(n))
+            self._keys[k] = C.string_at(p, n.value)
+        return self._keys[k]
+
+    def set_valid_char(self, chars) -> None:
+        b = chars if isinstance(chars, bytes) else chars.encode("latin-1")
+        lib().ngo_set_valid(self.h, b, len(b))
+
+    def score_ids(self, query, threshold: float, limit: int):
+        q = query if isinstance(query, bytes) else query.encode("latin-1")
+        cap = max(1, min(limit if limit else 2**31 - 1, self.n_keys()))
+        keys = (C.c_uint32 * cap)()
+        scores = (C.c_float * cap)()
+        n = lib().ngo_search(self.h, q, threshold, limit, keys, scores, cap)
+        return list(keys[:n]), list(scores[:n])
+
+    def score(self, query, threshold: float = 0.0, limit: int = 100):
+        """Like dllmain.cpp:82 score(): list of (key bytes, fp32 score)."""
+        ids, sc = self.score_ids(query, threshold, limit)
+        return [(self.key(k), s) for k, s in zip(ids, sc)]
+
+    def score_batch(self, queries, threshold: float, limit: int, threads: int = 1):
+        """Returns (counts[n], keys[n*cap], scores[n*cap], cap) as ctypes arrays."""
+        n = len(queries)
+        cap = max(1, min(limit if limit else 2**31 - 1, self.n_keys()))
+        qs = (C.c_char_p * max(1, n))(*queries)
+        counts = (C.c_uint32 * max(1, n))()
+        keys = (C.c_uint32 * max(1, n * cap))()
+        scores = (C.c_float * max(1, n * cap))()
+        lib().ngo_search_batch(self.h, qs, n, threshold, limit, counts, keys, scores, cap, threads)
+        return counts, keys, scores, cap

@@ -1,0 +1,226 @@
+"""Generate the golden fixtures in tests/golden/ from the REFERENCE implementation.
+
+Runs in the build container only (needs /root/reference): ``make -C oracle ref`` compiles
+the reference DLL source in place into oracle/_ref/, then this script writes a request file,
+runs oracle/_ref/gen_golden (our driver over the reference C ABI, dllmain.cpp:37-151) and
+stores the answers as JSON fixtures. Each fixture holds the corpus (words, weights,
+rowSize), getSize/getLibSize, and per case the reference answer at the requested limit and
+the full answer at limit=0, which the tie-aware checker needs.
+
+Strings are stored latin-1 decoded (one char per byte); scores as fp32 bit patterns.
+
+    python tests/golden/make_golden.py          # rewrites tests/golden/*.json
+"""
+from __future__ import annotations
+
+import json
+import os
+import struct
+import subprocess
+import sys
+import tempfile
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+from stringsearchlib_amd.synth import SplitMix64, gen_corpus, gen_queries  # noqa: E402
+
+REF_SO = os.path.join(ROOT, "oracle", "_ref", "libStringSearchLib.so")
+GEN = os.path.join(ROOT, "oracle", "_ref", "gen_golden")
+INT_MAX = 2147483647
+
+
+def fbits(x: float) -> int:
+    return struct.unpack("<I", struct.pack("<f", x))[0]
+
+
+def hx(b: bytes | None) -> str:
+    if b is None:
+        return "-"
+    return b.hex() if b else "="
+
+
+def as_bytes(s) -> bytes | None:
+    if s is None:
+        return None
+    return s if isinstance(s, bytes) else s.encode("latin-1")
+
+
+def run_reference(corpora):
+    """corpora: list of dict(name, rowSize, words, weights|None, phases=[(validChar|None, cases)])."""
+    lines = []
+    for c in corpora:
+        lines.append(f"C {c['rowSize']} {len(c['words'])} {1 if c['weights'] is not None else 0}")
+        ws = c["weights"] if c["weights"] is not None else [0.0] * len(c["words"])
+        for w, wt in zip(c["words"], ws):
+            lines.append(f"W {hx(as_bytes(w))} {fbits(wt):08x}")
+        lines.append("I")
+        for valid, cases in c["phases"]:
+            if valid is not None:
+                lines.append(f"V {as_bytes(valid).hex()}")
+            for q, thr, limit in cases:
+                qb = as_bytes(q)
+                lines.append(f"Q {hx(qb) if qb else '='} {fbits(thr):08x} {limit}")
+                if limit != 0:
+                    lines.append(f"Q {hx(qb) if qb else '='} {fbits(thr):08x} 0")
+        lines.append("D")
+    with tempfile.NamedTemporaryFile("w", suffix=".req", delete=False) as f:
+        f.write("\n".join(lines) + "\n")
+        req = f.name
+    try:
+        out = subprocess.run([GEN, REF_SO, req], check=True, capture_output=True, text=True).stdout
+    finally:
+        os.unlink(req)
+    return [json.loads(l) for l in out.splitlines() if l.strip()]
+
+
+def build_fixtures(corpora):
+    answers = iter(run_reference(corpora))
+    fixtures = []
+    for c in corpora:
+        head = next(answers)
+        fx = {
+            "name": c["name"],
+            "rowSize": c["rowSize"],
+            "words": [None if w is None else as_bytes(w).decode("latin-1") for w in c["words"]],
+            "weights": None if c["weights"] is None else [fbits(w) for w in c["weights"]],
+            "size": head["size"],
+            "libSize": head["libSize"],
+            "phases": [],
+        }
+        for valid, cases in c["phases"]:
+            ph = {"validChar": None if valid is None else as_bytes(valid).decode("latin-1"), "cases": []}
+            for q, thr, limit in cases:
+                a = next(answers)
+                full = a if limit == 0 else next(answers)
+                dec = lambda xs: [bytes.fromhex(k).decode("latin-1") for k in xs]  # noqa: E731
+                ph["cases"].append({
+                    "q": as_bytes(q).decode("latin-1"), "thr": fbits(thr), "limit": limit,
+                    "keys": dec(a["keys"]), "scores": a["scores"],
+                    "full_keys": dec(full["keys"]), "full_scores": full["scores"],
+                })
+            fx["phases"].append(ph)
+        fixtures.append(fx)
+    return fixtures
+
+
+# ---------------------------------------------------------------- corpora ---------------
+
+def appendix_a():
+    """Hand corpora of SURVEY.md Appendix A (SearchTest/test.cpp:7-9 and friends)."""
+    out = []
+    out.append(dict(name="searchtest", rowSize=7, weights=None,
+                    words=["LWMS", "LWM", "LWMA", "LWYY", "L", "I", "GHRSDGSDGS Egdsrtg g"],
+                    phases=[(None, [(q, 0.5, INT_MAX) for q in
+                                    ["LWMS", "lwm", "LW", "L", "GHRSDG", "gsdgs egd", "*", "", "zzzz",
+                                     "LWMSX", "  lwms  ", "l-w-m-s", "I", "EGDSRTG G"]])]))
+    out.append(dict(name="corpusB", rowSize=2,
+                    words=["Hello World", "greeting phrase", "hello-world!", "salutation", "HELLO WORLDS",
+                           None, "abc", "xyz12345", "  padded key  ", "unrelated text"],
+                    weights=[0.5, 2, 1, 0, 1.25, 9, -1, 0.75, 1, 1],
+                    phases=[(None, [("hello world", 0.3, 100), ("HELLO WORLD", 0.0, 100), ("greeting", 0.3, 100),
+                                    ("phrase greet", 0.3, 100), ("abc", 0.0, 100), ("ab", 0.0, 100),
+                                    ("*", 0.0, 100), ("", 0.0, 100), ("padded", 0.3, 100), ("salutation", 0.3, 100),
+                                    ("hello world", 0.3, 1), ("###", 0.0, 100), ("xyz", 0.0, 100),
+                                    ("xyz12345", 0.3, 100), ("PADDED KEY", 0.0, 100), ("unrelated", 0.5, 3)])]))
+    out.append(dict(name="ties", rowSize=1, weights=None,
+                    words=["ABCDEF1", "ABCDEF2", "ABCDEF3", "ABCDEF4", "ABCDEFGH", "XABCDEF"],
+                    phases=[(None, [("ABCDEF", 0.0, 0), ("ABCDEF", 0.0, 2), ("ABCDEF", 0.0, 5), ("BCDEF", 0.0, 3),
+                                    ("ABCDEF9", 0.5, 4)])]))
+    out.append(dict(name="repeated", rowSize=1, weights=None,
+                    words=["AAAAAAB", "AAAB XX", "BBBBBBBB"],
+                    phases=[(None, [("AAAAAAAAA", 0.0, 100), ("AAAA", 0.0, 100), ("BBBBBBBBBBBB", 0.0, 100),
+                                    ("AB", 0.0, 100), ("A", 0.0, 100)])]))
+    city = ["NEW YORK CITY", "LOS ANGELES", "BOSTON", "YORK", "NYC", "PARIS", "New Jersey", "ROMA"]
+    out.append(dict(name="corpusC", rowSize=1, weights=None, words=city,
+                    phases=[(None, [("NEW YORK CITY", 0.3, 10), ("new york", 0.3, 10), ("york", 0.0, 10),
+                                    ("yrok", 0.0, 10), ("NY", 0.0, 10), ("BOSTN", 0.5, 10),
+                                    ("angeles los", 0.3, 10), ("PARISX", 0.0, 10), ("N", 0.0, 10),
+                                    ("new jersey", 0.3, 10), ("BOSXXX", 0.25, 10), ("roma", 0.0, 0),
+                                    ("LOS", 0.0, 3), ("YOR", 0.0, 0)]),
+                            ("AB", [("ROMA", 0.0, 10), ("NY", 0.0, 10), ("angeles", 0.0, 10)])]))
+    # a library-wide Levenshtein corpus: short and long terms, aliases, odd bytes
+    out.append(dict(name="mixed", rowSize=3,
+                    words=["Key-1", "k1 alias", "KEY ONE", "k2", None, "second key", "\tTAB key\n", "tab",
+                           "caf\xe9 au lait", "x", "y", "z", "DUP", "dup", "DUP", "dup", "Dup", "d u p"],
+                    weights=[1.5, 0.5, 2.0, 1.0, 5.0, 0.0, 1.0, 3.0, -2.0, 1.0, 1.0, 1.0, 0.25, 4.0, 0.5,
+                             1.0, 1.0, 1.0],
+                    phases=[(None, [(q, t, l) for q in ["key", "KEY 1", "k", "k2", "tab", "TAB KEY", "caf",
+                                                        "cafe au", "au lait", "DUP", "d u", "x", "xyz",
+                                                        "second", "\xe9", "KEY-ONE", "ke y"]
+                                    for t, l in [(0.0, 5), (0.4, 100)]])]))
+    # edge cases: a key whose term normalises to "" (kept by the reference, hpp:136-148),
+    # whitespace-only / empty words, tabs inside keys, validChar changes incl. high bytes
+    out.append(dict(name="edge", rowSize=2,
+                    words=["***", "%%", "   ", "ghost", "", "empty key", "a\tb c", "a b c", "x\xffy", "zz\xff",
+                           "LONGWORD1", "LONGWORD2", "longword1", "  ", "TRAILING   ", "\x80\x81abc"],
+                    weights=[1.0, 2.0, 1.0, 1.0, 1.0, 1.0, 0.5, 0.25, 1.0, 1.0, 1.0, 1.0, 3.0, 1.0, 1.0, 1.0],
+                    phases=[(None, [(q, t, l) for q in ["%", "%%", "***", "a b", "A B C", "x y", "LONGWORD",
+                                                        "longword12", "ongwor", "a", "ab", "trailing", "abc",
+                                                        "\x80\x81ab"]
+                                    for t, l in [(0.0, 0), (0.5, 3)]]),
+                            (".%$ @0123456789abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ\xff\x80\x81",
+                             [("x\xffy", 0.0, 0), ("\xff", 0.0, 5), ("zz\xff", 0.3, 0), ("\x80\x81abc", 0.0, 4)]),
+                            ("ABC", [("abc", 0.0, 0), ("CAB", 0.0, 0), ("LONGWORD", 0.0, 4)])]))
+    return out
+
+
+def synthetic():
+    out = []
+    # S1: bench-shaped (config C1), 1k rows, rowSize 1, no weights
+    words, _, rng = gen_corpus(1000, seed=42)
+    qs = gen_queries(words, 1, 60, rng)
+    cases = [(q, 0.0, 100) for q in qs[:20]] + [(q, 0.3, 100) for q in qs[20:40]] + \
+            [(q, 0.5, 10) for q in qs[40:60]]
+    cases += [(w, 0.3, 100) for w in words[:8]]                       # exact -> promote to 100
+    cases += [(w.lower(), 0.3, 100) for w in words[8:12]]             # lower-case exact
+    cases += [(w[:5], 0.0, 20) for w in words[12:16]]                 # short queries, len 5
+    cases += [(w[:3], 0.2, 20) for w in words[16:18]]                 # full-library scan
+    cases += [(w[2:10], 0.3, 20) for w in words[18:22]]               # len 8: short+long
+    out.append(dict(name="synth_c1", rowSize=1, weights=None, words=words, phases=[(None, cases)]))
+
+    # S2: weighted, 3k rows
+    words, wts, rng = gen_corpus(3000, seed=7)
+    qs = gen_queries(words, 1, 60, rng)
+    cases = [(q, 0.3, 100) for q in qs[:30]] + [(q, 0.0, 25) for q in qs[30:45]] + \
+            [(q, 0.6, 100) for q in qs[45:60]] + [(w, 0.3, 50) for w in words[:6]]
+    out.append(dict(name="synth_weighted", rowSize=1, weights=wts, words=words, phases=[(None, cases)]))
+
+    # S3: rowSize 4 (key + 3 aliases), weights with zeros / negatives, NULL holes
+    words, wts, rng = gen_corpus(400, seed=11, min_len=4, span=10, row_size=4)
+    words = list(words)
+    for i in range(0, len(words), 37):
+        words[i] = None
+    for i in range(3, len(wts), 23):
+        wts[i] = 0.0
+    for i in range(5, len(wts), 41):
+        wts[i] = -1.5
+    qs = gen_queries([w or b"ABCDEFGHIJ" for w in words], 4, 40, rng, qlen=10)
+    cases = [(q, t, l) for q in qs[:20] for t, l in [(0.3, 50)]] + [(q, 0.0, 30) for q in qs[20:30]] + \
+            [(q[:4], 0.25, 40) for q in qs[30:36]] + [(q[:2], 0.5, 40) for q in qs[36:40]]
+    out.append(dict(name="synth_rows4", rowSize=4, weights=wts, words=words, phases=[(None, cases)]))
+
+    # S4: many short terms (len 1..12): Levenshtein over shortLib
+    words, _, rng = gen_corpus(1500, seed=5, min_len=1, span=12)
+    qs = gen_queries(words, 1, 40, rng, qlen=7)
+    cases = [(q, 0.0, 15) for q in qs[:20]] + [(q, 0.5, 100) for q in qs[20:40]]
+    cases += [(w, 0.0, 10) for w in words[:10] if len(w) <= 3]
+    out.append(dict(name="synth_short", rowSize=1, weights=None, words=words, phases=[(None, cases)]))
+    return out
+
+
+def main():
+    if not (os.path.exists(REF_SO) and os.path.exists(GEN)):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "oracle"), "ref"], check=True)
+    fixtures = build_fixtures(appendix_a() + synthetic())
+    for fx in fixtures:
+        path = os.path.join(HERE, f"{fx['name']}.json")
+        with open(path, "w") as f:
+            json.dump(fx, f, separators=(",", ":"))
+        ncase = sum(len(p["cases"]) for p in fx["phases"])
+        print(f"{path}: size={fx['size']} libSize={fx['libSize']} cases={ncase} "
+              f"bytes={os.path.getsize(path)}")
+
+
+if __name__ == "__main__":
+    main()
