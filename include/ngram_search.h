@@ -1,0 +1,128 @@
+/* ngram_search.h — C ABI of libngram_search.so, the MI355X-native n-gram fuzzy search engine.
+ *
+ * Drop-in boundary: the first eight entry points have exactly the signatures, argument
+ * meaning, ownership rules and error behaviour of the reference DLL's exports
+ * (serena-yu17/StringSearchLib, nGramSearch/dllmain.cpp; line numbers below). A host that
+ * binds the reference through its C ABI binds this library unchanged.
+ *
+ * The search path runs on the GPU: queries are normalised, hashed into 3-grams, matched
+ * against gram -> term posting lists kept as CSR in HBM, counted in LDS hash tables,
+ * weighted, merged per key and cut to `limit` by HIP kernels for gfx950. indexN builds
+ * the CSR on the host and uploads it once. There is no CPU search fallback: if no GPU
+ * is usable, indexN prints the HIP error and returns 0.
+ *
+ * Threading: one global reader/writer lock, as the reference (dllmain.cpp:22). indexN and
+ * dispose are exclusive; everything else may run concurrently (each call takes its own
+ * stream and scratch from the handle's pool).
+ */
+#ifndef NGRAM_SEARCH_H
+#define NGRAM_SEARCH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NGS_API __attribute__((visibility("default")))
+
+/* ------------------------------------------------------------------------------------
+ * Reference exports (nGramSearch/dllmain.cpp), identical signatures.
+ * ------------------------------------------------------------------------------------ */
+
+/* dllmain.cpp:37. Index `size` words laid out as rows of `rowSize` (first word of a row =
+ * master key, the rest aliases). `weight` (may be NULL) is indexed by FLAT word index;
+ * weight 0 drops the pair. Returns the smallest free handle >= 1; 0 on failure. A
+ * library with size < 2 or words == NULL yields a handle whose searches return 0. */
+NGS_API uint32_t indexN(char** words, uint64_t size, uint16_t rowSize, float* weight);
+
+/* dllmain.cpp:61. Like score() without the scores array. */
+NGS_API uint32_t search(uint32_t handle, const char* query, char*** results, float threshold,
+                        uint32_t limit);
+
+/* dllmain.cpp:82. Top-`limit` master keys for `query` (limit 0 = unlimited) whose match
+ * ratio passes `threshold`, sorted by score desc then key length asc. *results receives a
+ * new[]'d array of pointers to index-owned key strings (valid until dispose), *scores a
+ * new[]'d float array; free both with release(). Returns the count. Unknown handle or
+ * un-built index: returns 0 and leaves *results / *scores untouched. */
+NGS_API uint32_t score(uint32_t handle, const char* query, char*** results, float** scores,
+                       float threshold, uint32_t limit);
+
+/* dllmain.cpp:98. delete[]s arrays returned by search/score/searchBatch/scoreBatch. */
+NGS_API void release(uint32_t handle, char** results, float* scores);
+
+/* dllmain.cpp:110. Frees the index (host and device). Unknown handles are ignored. */
+NGS_API void dispose(uint32_t handle);
+
+/* dllmain.cpp:120. Number of distinct normalised terms (wordMap.size()). */
+NGS_API uint64_t getSize(uint32_t handle);
+
+/* dllmain.cpp:133. Number of distinct 3-grams over the long terms (ngrams.size()). */
+NGS_API uint64_t getLibSize(uint32_t handle);
+
+/* dllmain.cpp:142. Replaces the set of bytes kept by query normalisation (others become
+ * spaces) for later searches. The index itself keeps the default set it was built with. */
+NGS_API void setValidChar(uint32_t handle, char* characters, int n);
+
+/* ------------------------------------------------------------------------------------
+ * Batch extensions (BASELINE.json north_star: "the batched search() scoring loop").
+ * Same semantics as score()/search() for each query; one GPU pass for the whole batch.
+ * counts[i] = results of query i; *results / *scores are ONE flat new[]'d array each,
+ * query i's results starting at sum(counts[0..i)). Returns the total; free with release().
+ * Unknown handle / un-built index: returns 0, counts zeroed, outputs untouched.
+ * ------------------------------------------------------------------------------------ */
+NGS_API uint32_t scoreBatch(uint32_t handle, const char* const* queries, uint32_t nQueries,
+                            float threshold, uint32_t limit, uint32_t* counts, char*** results,
+                            float** scores);
+NGS_API uint32_t searchBatch(uint32_t handle, const char* const* queries, uint32_t nQueries,
+                             float threshold, uint32_t limit, uint32_t* counts, char*** results);
+
+/* ------------------------------------------------------------------------------------
+ * Device-level extensions: inputs and outputs stay in HBM (bench, multi-GPU sharding,
+ * host frameworks that already hold device buffers). Not in the reference.
+ * ------------------------------------------------------------------------------------ */
+
+/* Selects the HIP device that the calling thread's next indexN builds on (default: the
+ * current HIP device). Returns 0, or a negative HIP error code. */
+NGS_API int ngsSetDevice(int device);
+NGS_API int ngsDeviceCount(void);
+
+/* Number of master keys; key ids used by ngsSearchDevice are 0..n-1. */
+NGS_API uint32_t ngsNumKeys(uint32_t handle);
+/* NUL-terminated, index-owned string of key `keyId` (NULL if out of range). */
+NGS_API const char* ngsKey(uint32_t handle, uint32_t keyId);
+
+/* Scores nQueries queries held on the handle's device: query i is the raw bytes
+ * dQueryBytes[dQueryOffsets[i] .. dQueryOffsets[i+1]) (no NUL needed). Writes, for query i,
+ * dCounts[i] results to dKeys/dScores[i*outStride ...]; outStride must be >=
+ * min(limit ? limit : 2^31-1, ngsNumKeys). `stream` is a hipStream_t (NULL = the handle's
+ * own stream); the call returns when the results are complete on that stream.
+ * Returns 0, or a negative error (-1 bad handle, -2 un-built index, -3 bad argument,
+ * -4 HIP failure). */
+NGS_API int ngsSearchDevice(uint32_t handle, const uint8_t* dQueryBytes, const uint64_t* dQueryOffsets,
+                            uint32_t nQueries, float threshold, uint32_t limit, uint32_t outStride,
+                            uint32_t* dCounts, uint32_t* dKeys, float* dScores, void* stream);
+
+/* Per-call statistics of the last search on `handle` (enable timing first). */
+typedef struct {
+    uint64_t queries;          /* queries in the call */
+    uint64_t fast_queries;     /* handled by the fused LDS kernel */
+    uint64_t general_queries;  /* handled by the dense library-wide kernels */
+    uint64_t postings;         /* sum over fast queries of posting ids read (distinct grams) */
+    uint64_t lists;            /* posting lists opened */
+    uint64_t results;          /* results written */
+    double fast_kernel_ms;     /* fused kernel time from HIP events on the call's stream */
+    double prep_kernel_ms;     /* normalisation kernel time */
+    double general_ms;         /* general path time (all its kernels) */
+} ngs_stats;
+NGS_API int ngsSetTiming(uint32_t handle, int enable);
+NGS_API int ngsLastStats(uint32_t handle, ngs_stats* out);
+
+/* Library build identification (e.g. "gfx950 ngram_search 0.1"). */
+NGS_API const char* ngsVersion(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NGRAM_SEARCH_H */

@@ -1,0 +1,112 @@
+"""ctypes binding of libngram_search.so (include/ngram_search.h).
+
+The library is built in-tree (``make -C stringsearchlib_amd/csrc``) and loaded from
+``stringsearchlib_amd/lib``. There is no pure-Python or CPU fallback: if the library is
+missing or no GPU is usable the calls fail loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+import subprocess
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+LIB_DIR = os.path.join(PKG, "lib")
+LIB_PATH = os.path.join(LIB_DIR, "libngram_search.so")
+SYNTH_PATH = os.path.join(LIB_DIR, "libngs_synth.so")
+HEADER = os.path.join(ROOT, "include", "ngram_search.h")
+CSRC = os.path.join(PKG, "csrc")
+
+
+class NgsStats(C.Structure):
+    _fields_ = [("queries", C.c_uint64), ("fast_queries", C.c_uint64), ("general_queries", C.c_uint64),
+                ("postings", C.c_uint64), ("lists", C.c_uint64), ("results", C.c_uint64),
+                ("fast_kernel_ms", C.c_double), ("prep_kernel_ms", C.c_double), ("general_ms", C.c_double)]
+
+
+def build(jobs: int = 4) -> None:
+    """Compile the HIP library for gfx950 in-tree."""
+    subprocess.run(["make", "-s", f"-j{jobs}", "-C", CSRC], check=True)
+
+
+_lib = None
+_synth = None
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} is missing: build it with `make -C {CSRC}` (HIP, gfx950)")
+    L = C.CDLL(LIB_PATH)
+    u32, u64, f32, cp = C.c_uint32, C.c_uint64, C.c_float, C.c_char_p
+    PP = C.POINTER(C.POINTER(C.c_char))
+    L.indexN.restype = u32
+    L.indexN.argtypes = [C.POINTER(cp), u64, C.c_uint16, C.POINTER(f32)]
+    L.search.restype = u32
+    L.search.argtypes = [u32, cp, C.POINTER(PP), f32, u32]
+    L.score.restype = u32
+    L.score.argtypes = [u32, cp, C.POINTER(PP), C.POINTER(C.POINTER(f32)), f32, u32]
+    L.release.restype = None
+    L.release.argtypes = [u32, PP, C.POINTER(f32)]
+    L.dispose.restype = None
+    L.dispose.argtypes = [u32]
+    L.getSize.restype = u64
+    L.getSize.argtypes = [u32]
+    L.getLibSize.restype = u64
+    L.getLibSize.argtypes = [u32]
+    L.setValidChar.restype = None
+    L.setValidChar.argtypes = [u32, cp, C.c_int]
+    L.scoreBatch.restype = u32
+    L.scoreBatch.argtypes = [u32, C.POINTER(cp), u32, f32, u32, C.POINTER(u32), C.POINTER(PP),
+                             C.POINTER(C.POINTER(f32))]
+    L.searchBatch.restype = u32
+    L.searchBatch.argtypes = [u32, C.POINTER(cp), u32, f32, u32, C.POINTER(u32), C.POINTER(PP)]
+    L.ngsSetDevice.restype = C.c_int
+    L.ngsSetDevice.argtypes = [C.c_int]
+    L.ngsDeviceCount.restype = C.c_int
+    L.ngsDeviceCount.argtypes = []
+    L.ngsNumKeys.restype = u32
+    L.ngsNumKeys.argtypes = [u32]
+    L.ngsKey.restype = C.c_void_p
+    L.ngsKey.argtypes = [u32, u32]
+    L.ngsSearchDevice.restype = C.c_int
+    L.ngsSearchDevice.argtypes = [u32, C.c_void_p, C.c_void_p, u32, f32, u32, u32, C.c_void_p, C.c_void_p,
+                                  C.c_void_p, C.c_void_p]
+    L.ngsSetTiming.restype = C.c_int
+    L.ngsSetTiming.argtypes = [u32, C.c_int]
+    L.ngsLastStats.restype = C.c_int
+    L.ngsLastStats.argtypes = [u32, C.POINTER(NgsStats)]
+    L.ngsVersion.restype = cp
+    L.ngsVersion.argtypes = []
+    _lib = L
+    return L
+
+
+def synth():
+    global _synth
+    if _synth is None:
+        if not os.path.exists(SYNTH_PATH):
+            raise RuntimeError(f"{SYNTH_PATH} is missing: build it with `make -C {CSRC}`")
+        S = C.CDLL(SYNTH_PATH)
+        S.ngs_synth_corpus.restype = C.c_int
+        S.ngs_synth_corpus.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32,
+                                       C.POINTER(C.c_void_p), C.POINTER(C.POINTER(C.c_char_p)),
+                                       C.POINTER(C.POINTER(C.c_float)), C.POINTER(C.c_uint64)]
+        S.ngs_synth_queries.restype = C.c_int
+        S.ngs_synth_queries.argtypes = [C.POINTER(C.c_char_p), C.c_uint64, C.c_uint32, C.c_uint64,
+                                        C.POINTER(C.c_uint64), C.c_uint32, C.POINTER(C.c_void_p),
+                                        C.POINTER(C.POINTER(C.c_uint64))]
+        S.ngs_synth_free.restype = None
+        S.ngs_synth_free.argtypes = [C.c_void_p]
+        _synth = S
+    return _synth
+
+
+def declared_symbols() -> list[str]:
+    """Every function include/ngram_search.h declares with NGS_API."""
+    text = open(HEADER).read()
+    return re.findall(r"NGS_API\s+[\w\s\*]+?\b(\w+)\s*\(", text)

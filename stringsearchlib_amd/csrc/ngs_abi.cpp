@@ -1,0 +1,564 @@
+// ngs_abi.cpp — the C ABI (include/ngram_search.h): handle registry, device residency of the
+// index, per-call search contexts (stream + scratch) and result marshalling.
+//
+// Mirrors nGramSearch/dllmain.cpp (paths under /root/reference): the global shared_mutex
+// (:22), smallest-free-handle allocation (:41-46), shared locks for searches (:63,84,100,122,
+// 135,147) and exclusive locks for indexN/dispose (:39,112).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+#include <memory>
+#include <mutex>
+#include <shared_mutex>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/ngram_search.h"
+#include "ngs_index.h"
+#include "ngs_kernels.h"
+
+namespace ngs {
+namespace {
+
+constexpr char kDefaultValid[] = ".%$ @0123456789abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ";
+constexpr uint32_t kInt32Max = (uint32_t)std::numeric_limits<int32_t>::max();
+constexpr size_t kOutBudget = size_t(1) << 30;       // bytes of (key, score) output per chunk
+constexpr size_t kGeneralBudget = size_t(2) << 30;   // bytes of dense general-path state
+
+bool hip_ok(hipError_t e, const char* what) {
+    if (e == hipSuccess) return true;
+    std::fprintf(stderr, "ngram_search: %s failed: %s\n", what, hipGetErrorString(e));
+    return false;
+}
+#define HIP_CHECK(expr) hip_ok((expr), #expr)
+
+template <class T>
+bool dev_alloc(T** p, size_t n) {
+    *p = nullptr;
+    return HIP_CHECK(hipMalloc((void**)p, std::max<size_t>(n, 1) * sizeof(T)));
+}
+
+template <class T>
+bool dev_upload(T** p, const std::vector<T>& v, std::vector<void*>& owned) {
+    if (!dev_alloc(p, v.size())) return false;
+    owned.push_back(*p);
+    return v.empty() || HIP_CHECK(hipMemcpy(*p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+}
+
+struct Context {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[6] = {};
+    size_t qcap = 0, bcap = 0, ncap = 0, ocap = 0;
+    uint8_t* d_raw = nullptr;
+    uint64_t* d_off = nullptr;
+    uint8_t* d_norm = nullptr;
+    uint32_t* d_qm = nullptr;
+    uint32_t* d_glist = nullptr;
+    uint32_t* d_gcount = nullptr;
+    uint32_t* d_group = nullptr;
+    DevStats* d_stats = nullptr;
+    uint32_t* d_n = nullptr;
+    uint32_t* d_k = nullptr;
+    float* d_s = nullptr;
+    GeneralBuffers gen;
+    std::vector<uint8_t> h_raw;
+    std::vector<uint64_t> h_off;
+
+    ~Context() {
+        hipSetDevice(device);
+        for (void* p : {(void*)d_raw, (void*)d_off, (void*)d_norm, (void*)d_qm, (void*)d_glist, (void*)d_gcount,
+                        (void*)d_group, (void*)d_stats, (void*)d_n, (void*)d_k, (void*)d_s, (void*)gen.cnt,
+                        (void*)gen.kenc, (void*)gen.list, (void*)gen.sorted, (void*)gen.lcount, gen.temp})
+            if (p) hipFree(p);
+        for (hipEvent_t e : ev)
+            if (e) hipEventDestroy(e);
+        if (stream) hipStreamDestroy(stream);
+    }
+};
+
+struct Library {
+    HostIndex host;
+    int device = 0;
+    bool on_device = false;
+    DevIndex dev{};
+    std::vector<void*> owned;
+    std::mutex valid_mu;
+    uint32_t valid[8] = {};
+    std::mutex pool_mu;
+    std::vector<std::unique_ptr<Context>> pool;
+    std::atomic<bool> timing{false};
+    std::mutex stats_mu;
+    ngs_stats last{};
+
+    ~Library() {
+        pool.clear();
+        if (on_device) {
+            hipSetDevice(device);
+            for (void* p : owned) hipFree(p);
+        }
+    }
+
+    std::unique_ptr<Context> acquire() {
+        {
+            std::lock_guard<std::mutex> g(pool_mu);
+            if (!pool.empty()) {
+                auto c = std::move(pool.back());
+                pool.pop_back();
+                return c;
+            }
+        }
+        auto c = std::make_unique<Context>();
+        c->device = device;
+        if (!HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking))) return nullptr;
+        for (hipEvent_t& e : c->ev)
+            if (!HIP_CHECK(hipEventCreate(&e))) return nullptr;
+        if (!dev_alloc(&c->d_gcount, 1) || !dev_alloc(&c->d_group, 64) || !dev_alloc(&c->d_stats, 1)) return nullptr;
+        return c;
+    }
+    void give_back(std::unique_ptr<Context> c) {
+        std::lock_guard<std::mutex> g(pool_mu);
+        pool.push_back(std::move(c));
+    }
+};
+
+std::shared_mutex g_lock;                                        // dllmain.cpp:22
+std::unordered_map<uint32_t, std::unique_ptr<Library>> g_libs;   // dllmain.cpp:24
+thread_local int t_device = -1;
+
+Library* find_lib(uint32_t h) {
+    auto it = g_libs.find(h);
+    return it == g_libs.end() ? nullptr : it->second.get();
+}
+
+bool upload(Library& L) {
+    int dev = t_device;
+    if (dev < 0 && !HIP_CHECK(hipGetDevice(&dev))) return false;
+    if (!HIP_CHECK(hipSetDevice(dev))) return false;
+    L.device = dev;
+    HostIndex& H = L.host;
+    DevIndex& X = L.dev;
+    X.n_terms = H.n_terms;
+    X.n_short = H.n_short;
+    X.n_keys = H.n_keys;
+    std::vector<uint8_t> kb(H.key_bytes.begin(), H.key_bytes.end());
+    uint64_t *gram_off, *term_off, *key_off;
+    uint32_t *post, *tk_off, *wild_key;
+    uint8_t *term_bytes, *key_bytes;
+    uint2* tk;
+    float *wild_w, *wild_score;
+    L.on_device = true;  // from here on the destructor frees what was allocated
+    bool ok = dev_upload(&gram_off, H.gram_off, L.owned) && dev_upload(&post, H.post, L.owned) &&
+              dev_upload(&term_off, H.term_off, L.owned) && dev_upload(&term_bytes, H.term_bytes, L.owned) &&
+              dev_upload(&tk_off, H.tk_off, L.owned) && dev_upload(&tk, H.tk, L.owned) &&
+              dev_upload(&key_off, H.key_off, L.owned) && dev_upload(&key_bytes, kb, L.owned) &&
+              dev_upload(&wild_w, H.wild_w, L.owned);
+    if (!ok) return false;
+    if (!dev_alloc(&wild_key, H.n_keys)) return false;
+    L.owned.push_back(wild_key);
+    if (!dev_alloc(&wild_score, H.n_keys)) return false;
+    L.owned.push_back(wild_score);
+    if (!HIP_CHECK(build_wildcard(wild_w, H.n_keys, wild_key, wild_score, nullptr))) return false;
+    X.gram_off = gram_off;
+    X.post = post;
+    X.term_off = term_off;
+    X.term_bytes = term_bytes;
+    X.tk_off = tk_off;
+    X.tk = tk;
+    X.key_off = key_off;
+    X.key_bytes = key_bytes;
+    X.wild_key = wild_key;
+    X.wild_score = wild_score;
+    // the device copy is authoritative for the search; keep only what marshalling needs
+    std::vector<uint64_t>().swap(H.gram_off);
+    std::vector<uint32_t>().swap(H.post);
+    std::vector<uint64_t>().swap(H.term_off);
+    std::vector<uint8_t>().swap(H.term_bytes);
+    std::vector<uint32_t>().swap(H.tk_off);
+    std::vector<uint2>().swap(H.tk);
+    std::vector<float>().swap(H.wild_w);
+    return true;
+}
+
+bool ensure_queries(Context& c, size_t B, size_t bytes) {
+    if (B > c.bcap) {
+        for (void** p : {(void**)&c.d_off, (void**)&c.d_qm, (void**)&c.d_glist})
+            if (*p) { hipFree(*p); *p = nullptr; }
+        size_t nb = std::max<size_t>(B, 1024);
+        if (!dev_alloc(&c.d_off, nb + 1) || !dev_alloc(&c.d_qm, nb) || !dev_alloc(&c.d_glist, nb)) return false;
+        c.bcap = nb;
+    }
+    if (bytes > c.qcap) {
+        for (void** p : {(void**)&c.d_raw, (void**)&c.d_norm})
+            if (*p) { hipFree(*p); *p = nullptr; }
+        size_t nb = std::max<size_t>(bytes, 1 << 16);
+        if (!dev_alloc(&c.d_raw, nb) || !dev_alloc(&c.d_norm, nb)) return false;
+        c.qcap = nb;
+    }
+    return true;
+}
+
+bool ensure_outputs(Context& c, size_t B, size_t stride) {
+    const size_t need = B * stride;
+    if (!c.d_n || B > c.ncap || need > c.ocap) {
+        for (void** p : {(void**)&c.d_n, (void**)&c.d_k, (void**)&c.d_s})
+            if (*p) { hipFree(*p); *p = nullptr; }
+        if (!dev_alloc(&c.d_n, B) || !dev_alloc(&c.d_k, need) || !dev_alloc(&c.d_s, need)) return false;
+        c.ncap = B;
+        c.ocap = need;
+    }
+    return true;
+}
+
+bool ensure_general(Library& L, Context& c) {
+    if (c.gen.G) return true;
+    const DevIndex& X = L.dev;
+    const uint64_t n_long = X.n_terms - X.n_short;
+    const uint64_t per = n_long * 4 + (uint64_t)X.n_keys * 12 + 64;
+    uint32_t G = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(64, kGeneralBudget / per));
+    if ((uint64_t)G * std::max<uint32_t>(X.n_keys, 1) > (uint64_t)kInt32Max) G = 1;
+    GeneralBuffers& W = c.gen;
+    if (!dev_alloc(&W.cnt, (size_t)G * n_long) || !dev_alloc(&W.kenc, (size_t)G * X.n_keys) ||
+        !dev_alloc(&W.list, (size_t)G * X.n_keys) || !dev_alloc(&W.sorted, X.n_keys) || !dev_alloc(&W.lcount, G))
+        return false;
+    W.temp_bytes = general_sort_temp_bytes(X.n_keys);
+    if (!HIP_CHECK(hipMalloc(&W.temp, std::max<size_t>(W.temp_bytes, 1)))) return false;
+    if (!HIP_CHECK(hipMemset(W.cnt, 0, sizeof(uint32_t) * std::max<size_t>((size_t)G * n_long, 1))) ||
+        !HIP_CHECK(hipMemset(W.kenc, 0, sizeof(uint32_t) * std::max<size_t>((size_t)G * X.n_keys, 1))))
+        return false;
+    W.G = G;
+    return true;
+}
+
+// The search pipeline over B queries already in device memory. Returns 0 or a negative code.
+int device_search(Library& L, Context& c, const uint8_t* d_raw, const uint64_t* d_off, uint32_t B, uint64_t qbytes,
+                  float thr, uint32_t limit, uint32_t stride, uint32_t* d_n, uint32_t* d_k, float* d_s,
+                  hipStream_t s) {
+    if (!B) return 0;
+    SearchParams P{};
+    P.thr = thr;
+    P.limit = limit;
+    P.out_stride = stride;
+    P.n_queries = B;
+    {
+        std::lock_guard<std::mutex> g(L.valid_mu);
+        std::memcpy(P.valid, L.valid, sizeof(P.valid));
+    }
+    if (!ensure_queries(c, B, qbytes)) return -4;
+    const bool timing = L.timing.load();
+    ngs_stats st{};
+    st.queries = B;
+    if (timing) {
+        if (!HIP_CHECK(hipMemsetAsync(c.d_stats, 0, sizeof(DevStats), s))) return -4;
+        HIP_CHECK(hipEventRecord(c.ev[0], s));
+    }
+    if (!HIP_CHECK(launch_prep(d_raw, d_off, B, P, c.d_norm, c.d_qm, s))) return -4;
+    if (timing) HIP_CHECK(hipEventRecord(c.ev[1], s));
+    if (!HIP_CHECK(hipMemsetAsync(c.d_gcount, 0, sizeof(uint32_t), s))) return -4;
+    if (timing) HIP_CHECK(hipEventRecord(c.ev[2], s));
+    if (!HIP_CHECK(launch_fast(L.dev, P, c.d_norm, d_off, c.d_qm, d_n, d_k, d_s, c.d_glist, c.d_gcount,
+                               timing ? c.d_stats : nullptr, s)))
+        return -4;
+    if (timing) HIP_CHECK(hipEventRecord(c.ev[3], s));
+    uint32_t ngen = 0;
+    if (!HIP_CHECK(hipMemcpyAsync(&ngen, c.d_gcount, sizeof(uint32_t), hipMemcpyDeviceToHost, s)) ||
+        !HIP_CHECK(hipStreamSynchronize(s)))
+        return -4;
+    if (ngen) {
+        std::vector<uint32_t> gl(ngen);
+        if (!HIP_CHECK(hipMemcpyAsync(gl.data(), c.d_glist, sizeof(uint32_t) * ngen, hipMemcpyDeviceToHost, s)) ||
+            !HIP_CHECK(hipStreamSynchronize(s)))
+            return -4;
+        std::sort(gl.begin(), gl.end());
+        if (!ensure_general(L, c)) return -4;
+        if (timing) HIP_CHECK(hipEventRecord(c.ev[4], s));
+        for (uint32_t g0 = 0; g0 < ngen; g0 += c.gen.G) {
+            const uint32_t G = std::min(c.gen.G, ngen - g0);
+            if (!HIP_CHECK(hipMemcpyAsync(c.d_group, gl.data() + g0, sizeof(uint32_t) * G, hipMemcpyHostToDevice, s)))
+                return -4;
+            if (!HIP_CHECK(run_general(L.dev, P, c.d_norm, d_off, c.d_qm, c.d_group, gl.data() + g0, G, c.gen, d_n,
+                                       d_k, d_s, s)))
+                return -4;
+        }
+        if (timing) HIP_CHECK(hipEventRecord(c.ev[5], s));
+    }
+    if (!HIP_CHECK(hipStreamSynchronize(s))) return -4;
+    if (timing) {
+        DevStats ds{};
+        HIP_CHECK(hipMemcpy(&ds, c.d_stats, sizeof(ds), hipMemcpyDeviceToHost));
+        float ms = 0;
+        st.fast_queries = ds.fast;
+        st.general_queries = ngen;
+        st.postings = ds.postings;
+        st.lists = ds.lists;
+        st.results = ds.results;
+        if (hipEventElapsedTime(&ms, c.ev[0], c.ev[1]) == hipSuccess) st.prep_kernel_ms = ms;
+        if (hipEventElapsedTime(&ms, c.ev[2], c.ev[3]) == hipSuccess) st.fast_kernel_ms = ms;
+        if (ngen && hipEventElapsedTime(&ms, c.ev[4], c.ev[5]) == hipSuccess) st.general_ms = ms;
+        std::lock_guard<std::mutex> g(L.stats_mu);
+        L.last = st;
+    }
+    return 0;
+}
+
+uint32_t effective_limit(const Library& L, uint32_t limit) {
+    if (limit == 0) limit = kInt32Max;  // nGramSearch.hpp:420-421
+    return std::min<uint32_t>(limit, L.host.n_keys);
+}
+
+// Host entry: scores n queries; fills counts and flat (key, score) vectors.
+bool host_search(Library& L, const char* const* queries, uint32_t nq, float thr, uint32_t limit,
+                 std::vector<uint32_t>& counts, std::vector<uint32_t>& keys, std::vector<float>& scores) {
+    counts.assign(nq, 0);
+    keys.clear();
+    scores.clear();
+    const uint32_t Lm = effective_limit(L, limit);
+    if (Lm == 0 || nq == 0) return true;
+    if (!HIP_CHECK(hipSetDevice(L.device))) return false;
+    std::unique_ptr<Context> c = L.acquire();
+    if (!c) return false;
+    const size_t stride = Lm;
+    const size_t max_chunk = std::max<size_t>(1, std::min<size_t>(1 << 20, kOutBudget / (stride * 8)));
+    std::vector<uint32_t> hk, hn;
+    std::vector<float> hs;
+    bool ok = true;
+    for (uint32_t q0 = 0; q0 < nq && ok; q0 += (uint32_t)max_chunk) {
+        const uint32_t B = (uint32_t)std::min<size_t>(max_chunk, nq - q0);
+        c->h_off.resize(B + 1);
+        c->h_off[0] = 0;
+        for (uint32_t i = 0; i < B; ++i) c->h_off[i + 1] = c->h_off[i] + (queries[q0 + i] ? std::strlen(queries[q0 + i]) : 0);
+        c->h_raw.resize(std::max<uint64_t>(c->h_off[B], 1));
+        for (uint32_t i = 0; i < B; ++i)
+            if (queries[q0 + i]) std::memcpy(c->h_raw.data() + c->h_off[i], queries[q0 + i], c->h_off[i + 1] - c->h_off[i]);
+        ok = ensure_queries(*c, B, c->h_off[B]) && ensure_outputs(*c, B, stride) &&
+             HIP_CHECK(hipMemcpyAsync(c->d_raw, c->h_raw.data(), c->h_off[B], hipMemcpyHostToDevice, c->stream)) &&
+             HIP_CHECK(hipMemcpyAsync(c->d_off, c->h_off.data(), sizeof(uint64_t) * (B + 1), hipMemcpyHostToDevice,
+                                      c->stream));
+        if (!ok) break;
+        ok = device_search(L, *c, c->d_raw, c->d_off, B, c->h_off[B], thr, Lm, (uint32_t)stride, c->d_n, c->d_k,
+                           c->d_s, c->stream) == 0;
+        if (!ok) break;
+        hn.resize(B);
+        hk.resize((size_t)B * stride);
+        hs.resize((size_t)B * stride);
+        ok = HIP_CHECK(hipMemcpyAsync(hn.data(), c->d_n, sizeof(uint32_t) * B, hipMemcpyDeviceToHost, c->stream)) &&
+             HIP_CHECK(hipMemcpyAsync(hk.data(), c->d_k, sizeof(uint32_t) * B * stride, hipMemcpyDeviceToHost, c->stream)) &&
+             HIP_CHECK(hipMemcpyAsync(hs.data(), c->d_s, sizeof(float) * B * stride, hipMemcpyDeviceToHost, c->stream)) &&
+             HIP_CHECK(hipStreamSynchronize(c->stream));
+        if (!ok) break;
+        for (uint32_t i = 0; i < B; ++i) {
+            counts[q0 + i] = hn[i];
+            keys.insert(keys.end(), hk.begin() + (size_t)i * stride, hk.begin() + (size_t)i * stride + hn[i]);
+            scores.insert(scores.end(), hs.begin() + (size_t)i * stride, hs.begin() + (size_t)i * stride + hn[i]);
+        }
+    }
+    L.give_back(std::move(c));
+    return ok;
+}
+
+void set_valid(Library& L, const char* chars, int n) {
+    uint32_t v[8] = {};
+    for (int i = 0; i < n; ++i) {
+        const uint8_t c = (uint8_t)chars[i];
+        v[c >> 5] |= 1u << (c & 31);
+    }
+    std::lock_guard<std::mutex> g(L.valid_mu);
+    std::memcpy(L.valid, v, sizeof(v));
+}
+
+uint32_t marshal(const Library& L, const std::vector<uint32_t>& keys, const std::vector<float>& sc, char*** results,
+                 float** scores) {
+    const size_t n = keys.size();
+    if (scores) *scores = new float[n];
+    *results = new char*[n];
+    for (size_t i = 0; i < n; ++i) {
+        (*results)[i] = const_cast<char*>(L.host.key_bytes.data() + L.host.key_off[keys[i]]);
+        if (scores) (*scores)[i] = sc[i];
+    }
+    return (uint32_t)n;
+}
+
+uint32_t one_query(uint32_t handle, const char* query, char*** results, float** scores, float thr, uint32_t limit) {
+    std::shared_lock<std::shared_mutex> lk(g_lock);
+    Library* L = find_lib(handle);
+    if (!L || !L->host.indexed || !query) return 0;  // dllmain.cpp:69, nGramSearch.hpp:417-418
+    std::vector<uint32_t> counts, keys;
+    std::vector<float> sc;
+    if (!host_search(*L, &query, 1, thr, limit, counts, keys, sc)) return 0;
+    return marshal(*L, keys, sc, results, scores);
+}
+
+uint32_t batch_query(uint32_t handle, const char* const* queries, uint32_t nq, float thr, uint32_t limit,
+                     uint32_t* counts, char*** results, float** scores) {
+    if (counts) std::fill(counts, counts + nq, 0u);
+    std::shared_lock<std::shared_mutex> lk(g_lock);
+    Library* L = find_lib(handle);
+    if (!L || !L->host.indexed || !queries || !counts) return 0;
+    std::vector<uint32_t> cnt, keys;
+    std::vector<float> sc;
+    if (!host_search(*L, queries, nq, thr, limit, cnt, keys, sc)) return 0;
+    std::copy(cnt.begin(), cnt.end(), counts);
+    return marshal(*L, keys, sc, results, scores);
+}
+
+}  // namespace
+}  // namespace ngs
+
+using namespace ngs;
+
+extern "C" {
+
+NGS_API uint32_t indexN(char** words, uint64_t size, uint16_t rowSize, float* weight) {
+    std::unique_lock<std::shared_mutex> lk(g_lock);  // dllmain.cpp:39
+    uint32_t handle = 1;                             // dllmain.cpp:41-46
+    const uint32_t maxVal = std::numeric_limits<uint32_t>::max();
+    while (g_libs.count(handle) && handle < maxVal) ++handle;
+    if (handle == maxVal) return 0;
+    auto L = std::make_unique<Library>();
+    set_valid(*L, kDefaultValid, (int)std::strlen(kDefaultValid));
+    build_index(L->host, words, size, rowSize, weight);
+    if (L->host.indexed && !upload(*L)) {
+        std::fprintf(stderr, "ngram_search: indexN could not place the index on a GPU\n");
+        return 0;
+    }
+    if (!L->host.indexed) {
+        int dev = t_device;
+        if (dev < 0 && hipGetDevice(&dev) != hipSuccess) dev = 0;
+        L->device = dev;
+    }
+    g_libs.emplace(handle, std::move(L));
+    return handle;
+}
+
+NGS_API uint32_t search(uint32_t handle, const char* query, char*** results, float threshold, uint32_t limit) {
+    return one_query(handle, query, results, nullptr, threshold, limit);
+}
+
+NGS_API uint32_t score(uint32_t handle, const char* query, char*** results, float** scores, float threshold,
+                       uint32_t limit) {
+    return one_query(handle, query, results, scores, threshold, limit);
+}
+
+NGS_API void release(uint32_t handle, char** results, float* scores) {
+    std::shared_lock<std::shared_mutex> lk(g_lock);  // dllmain.cpp:100-103
+    if (!find_lib(handle)) return;
+    delete[] results;
+    delete[] scores;
+}
+
+NGS_API void dispose(uint32_t handle) {
+    std::unique_lock<std::shared_mutex> lk(g_lock);  // dllmain.cpp:112-113
+    g_libs.erase(handle);
+}
+
+NGS_API uint64_t getSize(uint32_t handle) {
+    std::shared_lock<std::shared_mutex> lk(g_lock);
+    Library* L = find_lib(handle);
+    return L ? L->host.n_terms : 0;
+}
+
+NGS_API uint64_t getLibSize(uint32_t handle) {
+    std::shared_lock<std::shared_mutex> lk(g_lock);
+    Library* L = find_lib(handle);
+    return L ? L->host.n_grams : 0;
+}
+
+NGS_API void setValidChar(uint32_t handle, char* characters, int n) {
+    std::shared_lock<std::shared_mutex> lk(g_lock);
+    Library* L = find_lib(handle);
+    if (L && (characters || n == 0)) set_valid(*L, characters, n);
+}
+
+NGS_API uint32_t scoreBatch(uint32_t handle, const char* const* queries, uint32_t nQueries, float threshold,
+                            uint32_t limit, uint32_t* counts, char*** results, float** scores) {
+    return batch_query(handle, queries, nQueries, threshold, limit, counts, results, scores);
+}
+
+NGS_API uint32_t searchBatch(uint32_t handle, const char* const* queries, uint32_t nQueries, float threshold,
+                             uint32_t limit, uint32_t* counts, char*** results) {
+    return batch_query(handle, queries, nQueries, threshold, limit, counts, results, nullptr);
+}
+
+NGS_API int ngsSetDevice(int device) {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) return -(int)e;
+    if (device < 0 || device >= n) return -(int)hipErrorInvalidDevice;
+    t_device = device;
+    return 0;
+}
+
+NGS_API int ngsDeviceCount(void) {
+    int n = 0;
+    return hipGetDeviceCount(&n) == hipSuccess ? n : 0;
+}
+
+NGS_API uint32_t ngsNumKeys(uint32_t handle) {
+    std::shared_lock<std::shared_mutex> lk(g_lock);
+    Library* L = find_lib(handle);
+    return L ? L->host.n_keys : 0;
+}
+
+NGS_API const char* ngsKey(uint32_t handle, uint32_t keyId) {
+    std::shared_lock<std::shared_mutex> lk(g_lock);
+    Library* L = find_lib(handle);
+    if (!L || keyId >= L->host.n_keys) return nullptr;
+    return L->host.key_bytes.data() + L->host.key_off[keyId];
+}
+
+NGS_API int ngsSearchDevice(uint32_t handle, const uint8_t* dQueryBytes, const uint64_t* dQueryOffsets,
+                            uint32_t nQueries, float threshold, uint32_t limit, uint32_t outStride, uint32_t* dCounts,
+                            uint32_t* dKeys, float* dScores, void* stream) {
+    std::shared_lock<std::shared_mutex> lk(g_lock);
+    Library* L = find_lib(handle);
+    if (!L) return -1;
+    if (!L->host.indexed) return -2;
+    const uint32_t Lm = effective_limit(*L, limit);
+    if (!dQueryOffsets || !dCounts || (nQueries && Lm && (!dKeys || !dScores || outStride < Lm))) return -3;
+    if (!HIP_CHECK(hipSetDevice(L->device))) return -4;
+    hipStream_t s = (hipStream_t)stream;
+    if (Lm == 0) {
+        return HIP_CHECK(hipMemsetAsync(dCounts, 0, sizeof(uint32_t) * nQueries, s)) &&
+                       HIP_CHECK(hipStreamSynchronize(s))
+                   ? 0
+                   : -4;
+    }
+    std::unique_ptr<Context> c = L->acquire();
+    if (!c) return -4;
+    if (!s) s = c->stream;
+    uint64_t qbytes = 0;
+    int rc = 0;
+    if (nQueries &&
+        (!HIP_CHECK(hipMemcpyAsync(&qbytes, dQueryOffsets + nQueries, sizeof(uint64_t), hipMemcpyDeviceToHost, s)) ||
+         !HIP_CHECK(hipStreamSynchronize(s))))
+        rc = -4;
+    if (!rc) rc = device_search(*L, *c, dQueryBytes, dQueryOffsets, nQueries, qbytes, threshold, Lm, outStride,
+                                dCounts, dKeys, dScores, s);
+    L->give_back(std::move(c));
+    return rc;
+}
+
+NGS_API int ngsSetTiming(uint32_t handle, int enable) {
+    std::shared_lock<std::shared_mutex> lk(g_lock);
+    Library* L = find_lib(handle);
+    if (!L) return -1;
+    L->timing.store(enable != 0);
+    return 0;
+}
+
+NGS_API int ngsLastStats(uint32_t handle, ngs_stats* out) {
+    std::shared_lock<std::shared_mutex> lk(g_lock);
+    Library* L = find_lib(handle);
+    if (!L || !out) return -1;
+    std::lock_guard<std::mutex> g(L->stats_mu);
+    *out = L->last;
+    return 0;
+}
+
+NGS_API const char* ngsVersion(void) { return "ngram_search 0.1 gfx950"; }
+
+}  // extern "C"

@@ -1,0 +1,77 @@
+// ngs_common.h — layout of the device index and the constants of the search path.
+//
+// Shared by the host index builder (ngs_index.cpp), the kernels (ngs_kernels.hip) and the
+// C-ABI layer (ngs_abi.cpp). Reference constants are cited (paths under /root/reference).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace ngs {
+
+// nGramSearch.hpp:82 — terms of length >= 6 go to longLib (gram search), others to shortLib.
+constexpr uint32_t kShortTermLen = 6;
+// nGramSearch.hpp:381 — queries shorter than 9 bytes also run the Levenshtein search.
+constexpr uint32_t kShortQueryLen = 9;
+// nGramSearch.hpp:235,247 — queries of <= 3 bytes Levenshtein-scan the WHOLE library.
+constexpr uint32_t kFullScanQueryLen = 3;
+
+// 3-gram code. The reference hashes c0<<16 | c1<<8 | c2 on signed chars (nGramSearch.h:147-150).
+// Indexed terms only hold validChar bytes (< 0x80), so their grams are exactly the 7-bit
+// triples; a query gram holding a byte >= 0x80 has a negative reference hash and can never
+// match. The 21-bit code (c0<<14 | c1<<7 | c2) is therefore a lossless direct index.
+constexpr uint32_t kGramBits = 21;
+constexpr uint32_t kGramSpace = 1u << kGramBits;
+
+// Score encoding shared by every stage: enc = bits(max(w*s, +0.0f)) + 1 for finite
+// non-negative scores (fp32 bits of non-negative floats order like the floats), 0 = "key
+// absent", kPromoted = exact match promoted to 100 (nGramSearch.hpp:328-335).
+constexpr uint32_t kPromoted = 0xFFFFFFFFu;
+
+// Candidate record = (~enc) << 32 | key: ascending order == reference order
+// (score desc, then key rank asc; key ranks are assigned by (length, first appearance)).
+constexpr uint64_t kNoCand = ~0ull;
+
+// ---- fused kernel geometry (tuned on MI355X) ----
+constexpr int kFastThreads = 512;        // 8 waves
+constexpr int kTableSlots = 8192;        // LDS hash table, u32 slot = (term - lo + 1) << 8 | count
+constexpr int kPartCap = kTableSlots / 2;// <= 50 % load: postings per term-range part
+constexpr int kCandCap = 2048;           // LDS candidate buffer (u64 records)
+constexpr uint32_t kFastMaxLimit = kCandCap / 2;
+constexpr uint32_t kFastMaxGrams = 255;  // u8 counts in the table slot
+constexpr uint32_t kMaxPartSpan = (1u << 24) - 2;  // 24-bit relative term id in the slot
+
+struct DevIndex {  // passed by value to kernels; all pointers are device pointers
+    const uint64_t* gram_off;   // [kGramSpace + 1] -> post
+    const uint32_t* post;       // long-term ids (0-based within longLib), sorted per gram
+    const uint64_t* term_off;   // [n_terms + 1] -> term_bytes (normalised terms)
+    const uint8_t* term_bytes;
+    const uint32_t* tk_off;     // [n_terms + 1] -> tk
+    const uint2* tk;            // {key rank, weight bits} — wordMap + wordWeight (h:290,293)
+    const uint64_t* key_off;    // [n_keys + 1] -> key_bytes (raw trimmed keys, NUL-separated)
+    const uint8_t* key_bytes;
+    const uint32_t* wild_key;   // wildcard answer, pre-sorted (hpp:356-369)
+    const float* wild_score;
+    uint32_t n_terms, n_short, n_keys, pad;
+};
+
+struct SearchParams {
+    float thr;
+    uint32_t limit;      // effective L = min(limit or 2^31-1, n_keys)
+    uint32_t out_stride;
+    uint32_t n_queries;
+    uint32_t valid[8];   // 256-bit validChar mask (h:307-313 / setValidChar)
+};
+
+// per-query normalised length sentinels written by the prep kernel
+constexpr uint32_t kQueryWildcard = 0xFFFFFFFFu;
+
+struct DevStats {  // accumulated by the fused kernel (one atomic per block)
+    unsigned long long postings;
+    unsigned long long lists;
+    unsigned long long results;
+    unsigned long long fast;
+};
+
+}  // namespace ngs

@@ -1,0 +1,43 @@
+// ngs_index.h — host-side index build: normalise the library and lay it out for HBM.
+//
+// Restates the reference's index construction (nGramSearch.hpp:120-172 ctor, :54-108 init,
+// :13-21/:41-46 gram build) as flat arrays instead of hash-of-hash-sets:
+//   terms      normalised strings; shortLib (len < 6) gets ids [0, n_short), longLib the rest
+//   keys       raw trimmed master keys, ranked by (length asc, first appearance asc): the
+//              ScoreComparer's length tie-break (nGramSearch.h:262-269) plus a deterministic
+//              refinement of the reference's unspecified order
+//   tk         term -> (key rank, weight) CSR  (wordMap + wordWeight, nGramSearch.h:290,293)
+//   gram CSR   21-bit gram code -> sorted long-term ids (ngrams, nGramSearch.h:296)
+#pragma once
+
+#include <cstdint>
+#include <mutex>
+#include <vector>
+
+#include "ngs_common.h"
+
+namespace ngs {
+
+struct HostIndex {
+    bool indexed = false;                   // nGramSearch.h:301
+    uint32_t n_terms = 0, n_short = 0, n_keys = 0;
+    uint64_t n_grams = 0;                   // distinct grams -> getLibSize
+    std::vector<uint64_t> gram_off;         // kGramSpace + 1
+    std::vector<uint32_t> post;
+    std::vector<uint64_t> term_off;
+    std::vector<uint8_t> term_bytes;
+    std::vector<uint32_t> tk_off;
+    std::vector<uint2> tk;                  // {key rank, float bits}
+    std::vector<uint64_t> key_off;          // key k = key_bytes[key_off[k] .. key_off[k+1]-1), NUL at end
+    std::vector<char> key_bytes;
+    std::vector<float> wild_w;              // wildcard score per key (max of its pair weights)
+};
+
+// Builds the index; `threads` workers for the gram CSR (0 = hardware concurrency).
+void build_index(HostIndex& ix, char* const* words, uint64_t size, uint16_t rowSize, const float* weight,
+                 unsigned threads = 0);
+
+// Wildcard answer: keys sorted by (wild_w desc, rank asc).
+void wildcard_order(const HostIndex& ix, std::vector<uint32_t>& keys, std::vector<float>& scores);
+
+}  // namespace ngs

@@ -1,0 +1,42 @@
+// ngs_kernels.h — launchers of the gfx950 search kernels (ngs_kernels.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "ngs_common.h"
+
+namespace ngs {
+
+// Normalise every query (escapeBlank -> trim -> toUpper, nGramSearch.hpp:372-376) into
+// qnorm (same offsets as the raw bytes) and its length into qm (kQueryWildcard for ""/"*").
+hipError_t launch_prep(const uint8_t* raw, const uint64_t* off, uint32_t B, const SearchParams& P,
+                       uint8_t* qnorm, uint32_t* qm, hipStream_t s);
+
+// Fused per-query kernel: short Levenshtein scan of shortLib (4 <= m < 9), 3-gram posting
+// count in an LDS hash table per term-id part, threshold, term->key weighting, per-key max
+// merge and top-L in LDS. Queries it cannot take are appended to glist for the general path.
+hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* qnorm, const uint64_t* off,
+                       const uint32_t* qm, uint32_t* out_n, uint32_t* out_k, float* out_s, uint32_t* glist,
+                       uint32_t* gcount, DevStats* stats, hipStream_t s);
+
+// Wildcard answer (nGramSearch.hpp:356-369): keys sorted by (weight desc, rank asc).
+hipError_t build_wildcard(const float* d_w, uint32_t n_keys, uint32_t* d_keys, float* d_scores, hipStream_t s);
+
+// General path: library-wide dense scoring of G queries at once (m <= 3 full-library scans,
+// very long queries, limits above kFastMaxLimit).
+struct GeneralBuffers {
+    uint32_t G = 0;             // queries per group
+    uint32_t* cnt = nullptr;    // [G][n_long] posting counts (self-clearing)
+    uint32_t* kenc = nullptr;   // [G][n_keys] per-key score encoding (self-clearing)
+    uint64_t* list = nullptr;   // [G][n_keys] compacted candidate records
+    uint64_t* sorted = nullptr; // [n_keys] radix-sort output
+    uint32_t* lcount = nullptr; // [G] candidates per query
+    void* temp = nullptr;       // radix-sort scratch
+    size_t temp_bytes = 0;
+};
+size_t general_sort_temp_bytes(uint32_t n_keys);
+hipError_t run_general(const DevIndex& X, const SearchParams& P, const uint8_t* qnorm, const uint64_t* off,
+                       const uint32_t* qm, const uint32_t* d_group, const uint32_t* h_group, uint32_t G,
+                       GeneralBuffers& W, uint32_t* out_n, uint32_t* out_k, float* out_s, hipStream_t s);
+
+}  // namespace ngs

@@ -1,0 +1,691 @@
+// ngs_kernels.hip — gfx950 kernels of the batched search() path.
+//
+// Reference semantics (paths under /root/reference):
+//   query normalisation  nGramSearch.hpp:372-376 (escapeBlank h:93-98, trim h:243-247, toUpper h:72-76)
+//   searchLong           nGramSearch.hpp:278-301   count[t] = #query grams (with multiplicity) in t
+//   searchShort          nGramSearch.hpp:182-270   semi-global edit distance, |q| < 9 (whole lib if |q| <= 3)
+//   calcScore            nGramSearch.hpp:310-341   s >= thr, key score = max(w*s, 0), exact -> 100
+//   top-k                nGramSearch.hpp:397-401   score desc, key length asc (ScoreComparer h:262-269)
+//
+// Numerics (bit-exact with the reference): s = (float)count / (float)n is one correctly rounded
+// fp32 division (built with -fhip-fp32-correctly-rounded-divide-sqrt); w*s one fp32 multiply
+// (-ffp-contract=off); threshold `s < thr` in fp32; promotion test `(double)s > 0.999`.
+#include <hipcub/hipcub.hpp>
+
+#include "ngs_kernels.h"
+
+namespace ngs {
+namespace {
+
+__device__ __forceinline__ uint64_t min64(uint64_t a, uint64_t b) { return a < b ? a : b; }
+__device__ __forceinline__ uint64_t max64(uint64_t a, uint64_t b) { return a > b ? a : b; }
+__device__ __forceinline__ bool dev_space(unsigned c) { return c == 32u || (c >= 9u && c <= 13u); }
+__device__ __forceinline__ unsigned dev_upper(unsigned c) { return (c >= 'a' && c <= 'z') ? c - 32u : c; }
+__device__ __forceinline__ unsigned esc(const uint32_t* valid, unsigned c) {
+    return ((valid[c >> 5] >> (c & 31u)) & 1u) ? c : 32u;  // escapeBlank
+}
+
+// ---------------------------------------------------------------- normalisation ------
+// One wave per query: ballots find the first / last byte that survives escape + trim.
+__global__ __launch_bounds__(64) void k_prep(const uint8_t* __restrict__ raw, const uint64_t* __restrict__ off,
+                                             uint32_t B, SearchParams P, uint8_t* __restrict__ qnorm,
+                                             uint32_t* __restrict__ qm) {
+    const uint32_t q = blockIdx.x;
+    if (q >= B) return;
+    const uint32_t lane = threadIdx.x;
+    const uint64_t b = off[q];
+    const uint64_t n = off[q + 1] - b;
+    if (n == 0 || (n == 1 && raw[b] == '*')) {  // wildcard, nGramSearch.hpp:356
+        if (lane == 0) qm[q] = kQueryWildcard;
+        return;
+    }
+    uint64_t first = n, last = 0;
+    for (uint64_t base = 0; base < n; base += 64) {
+        const uint64_t i = base + lane;
+        const bool keep = i < n && !dev_space(esc(P.valid, raw[b + i]));
+        const unsigned long long bal = __ballot(keep);
+        if (bal) { first = base + __ffsll((long long)bal) - 1; break; }
+    }
+    if (first == n) {  // nothing left after escape + trim, nGramSearch.hpp:374-375
+        if (lane == 0) qm[q] = 0;
+        return;
+    }
+    for (uint64_t base = 0; base < n; base += 64) {
+        const uint64_t i = n - 1 - (base + lane);
+        const bool keep = base + lane < n && !dev_space(esc(P.valid, raw[b + i]));
+        const unsigned long long bal = __ballot(keep);
+        if (bal) { last = n - 1 - (base + __ffsll((long long)bal) - 1); break; }
+    }
+    const uint64_t m = last - first + 1;
+    for (uint64_t i = lane; i < m; i += 64) qnorm[b + i] = (uint8_t)dev_upper(esc(P.valid, raw[b + first + i]));
+    if (lane == 0) qm[q] = (uint32_t)(m > 0xFFFFFFF0ull ? 0xFFFFFFF0ull : m);
+}
+
+// ---------------------------------------------------------------- shared helpers -----
+// libStr = escapeBlank(key); trim; libStr == query (nGramSearch.hpp:330-334: the key is NOT
+// upper-cased, so only keys already in query form promote).
+__device__ bool key_equals_query(const DevIndex& X, uint32_t k, const uint8_t* q, uint32_t m,
+                                 const uint32_t* valid) {
+    uint64_t a = X.key_off[k], e = X.key_off[k + 1] - 1;  // drop the NUL
+    while (a < e && dev_space(esc(valid, X.key_bytes[a]))) ++a;
+    while (e > a && dev_space(esc(valid, X.key_bytes[e - 1]))) --e;
+    if (e - a != m) return false;
+    for (uint32_t i = 0; i < m; ++i)
+        if (esc(valid, X.key_bytes[a + i]) != q[i]) return false;
+    return true;
+}
+
+// calcScore's per-pair value (nGramSearch.hpp:326-335) as an order-preserving encoding.
+__device__ __forceinline__ uint32_t pair_enc(uint2 kw, float s, bool promo_possible, const DevIndex& X,
+                                             const uint8_t* q, uint32_t m, const uint32_t* valid) {
+    const float sc = __uint_as_float(kw.y) * s;
+    uint32_t enc = sc > 0.0f ? __float_as_uint(sc) + 1u : 1u;  // std::max(w*s, 0.0f) (entry default)
+    if (promo_possible && key_equals_query(X, kw.x, q, m, valid)) enc = kPromoted;
+    return enc;
+}
+
+// stringMatch (nGramSearch.hpp:182-222): min over source substrings of the edit distance to
+// q (m <= 8); returns m - distance. Column DP over the query held in registers.
+__device__ __forceinline__ uint32_t string_match(const uint8_t (&qc)[8], uint32_t m, const uint8_t* s,
+                                                 uint32_t L) {
+    uint32_t col[9];
+#pragma unroll
+    for (int i = 0; i <= 8; ++i) col[i] = (uint32_t)i;
+    uint32_t best = m;
+    for (uint32_t j = 0; j < L; ++j) {
+        const uint32_t c = s[j];
+        uint32_t diag = 0, cur = 0;  // D[0][j] = 0: free start in the source
+#pragma unroll
+        for (int i = 1; i <= 8; ++i) {
+            const uint32_t up = col[i];
+            const uint32_t v = min(diag + (qc[i - 1] != c ? 1u : 0u), min(up, cur) + 1u);
+            diag = up;
+            col[i] = v;
+            cur = v;
+            if ((uint32_t)i == m) best = min(best, v);  // free end: min over the last row
+        }
+    }
+    return m - best;
+}
+
+// ---------------------------------------------------------------- fused kernel -------
+struct FastSmem {
+    uint32_t table[kTableSlots];   // (term - lo + 1) << 8 | count
+    uint64_t cand[kCandCap];       // (~enc) << 32 | key
+    uint64_t g_cur[256];           // per distinct gram: next posting to read
+    uint64_t g_end[256];           // end of its list
+    uint64_t g_stop[256];          // end of the current part's segment
+    uint32_t g_mult[256];          // multiplicity of the gram in the query
+    uint32_t g_code[256];
+    uint32_t pre[260];             // segment prefix sums
+    uint8_t q[264];
+    uint64_t tau;                  // records >= tau cannot enter the top-L
+    uint64_t p_left;
+    unsigned long long seg_total;
+    uint32_t ng, cand_n, n_valid, pad0;
+    uint32_t lo, hi, step, pad;
+};
+
+__device__ __forceinline__ uint32_t next_pow2(uint32_t x) { return x <= 1 ? 1u : 1u << (32 - __clz(x - 1)); }
+
+__device__ void bitonic_sort(uint64_t* a, uint32_t n) {
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t k = 2; k <= n; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t p = tid; p < n / 2; p += kFastThreads) {
+                const uint32_t i = (p / j) * 2 * j + (p % j), l = i + j;
+                const uint64_t x = a[i], y = a[l];
+                if ((x > y) == ((i & k) == 0)) { a[i] = y; a[l] = x; }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// Merge the buffer: keep each key's best record, then the best L records in order.
+// The running top-L with max-merge is exact: a record evicted here is beaten by L other keys
+// whose scores can only grow.
+__device__ void flush(FastSmem& S, uint32_t L) {
+    const uint32_t tid = threadIdx.x;
+    __syncthreads();
+    const uint32_t n = min(S.cand_n, (uint32_t)kCandCap);
+    const uint32_t P2 = next_pow2(max(n, 2u));
+    for (uint32_t i = tid; i < P2; i += kFastThreads) {
+        const uint64_t r = i < n ? S.cand[i] : kNoCand;
+        S.cand[i] = i < n ? ((r << 32) | (r >> 32)) : kNoCand;  // key-major for the dedup
+    }
+    if (tid == 0) S.n_valid = 0;
+    __syncthreads();
+    bitonic_sort(S.cand, P2);
+    uint64_t keep[kCandCap / kFastThreads];
+#pragma unroll
+    for (int u = 0; u < kCandCap / kFastThreads; ++u) {
+        const uint32_t i = tid + u * kFastThreads;
+        keep[u] = kNoCand;
+        if (i < P2) {
+            const uint64_t d = S.cand[i];
+            if (d != kNoCand && (i == 0 || (S.cand[i - 1] >> 32) != (d >> 32))) keep[u] = (d << 32) | (d >> 32);
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kCandCap / kFastThreads; ++u) {
+        const uint32_t i = tid + u * kFastThreads;
+        if (i < P2) S.cand[i] = keep[u];
+    }
+    __syncthreads();
+    bitonic_sort(S.cand, P2);
+    for (uint32_t i = tid; i < P2; i += kFastThreads)
+        if (S.cand[i] != kNoCand && (i + 1 == P2 || S.cand[i + 1] == kNoCand)) S.n_valid = i + 1;
+    __syncthreads();
+    if (tid == 0) {
+        const uint32_t nv = S.n_valid;
+        S.cand_n = min(nv, L);
+        S.tau = nv >= L ? S.cand[L - 1] : kNoCand;
+    }
+    __syncthreads();
+}
+
+struct EmitState {
+    uint32_t p, pe;  // pending (key, weight) pairs of the current term
+    float s;
+    bool promo;
+};
+
+// Appends the pending pairs; false = buffer full (the pair is retried after a flush).
+__device__ __forceinline__ bool emit_pending(EmitState& st, FastSmem& S, const DevIndex& X, uint64_t tau,
+                                             uint32_t m, const uint32_t* valid) {
+    while (st.p < st.pe) {
+        const uint2 kw = X.tk[st.p];
+        const uint32_t enc = pair_enc(kw, st.s, st.promo, X, S.q, m, valid);
+        const uint64_t rec = ((uint64_t)(~enc) << 32) | kw.x;
+        if (rec < tau) {
+            const uint32_t idx = atomicAdd(&S.cand_n, 1u);
+            if (idx >= (uint32_t)kCandCap) return false;
+            S.cand[idx] = rec;
+        }
+        ++st.p;
+    }
+    return true;
+}
+
+// Drives a per-thread stream of scored terms through calcScore into the buffer, flushing
+// whenever any thread finds it full. next(st) -> 0 exhausted, 1 term loaded into st, 2 skip.
+template <class Next>
+__device__ void produce(FastSmem& S, const DevIndex& X, const SearchParams& P, uint32_t m, uint32_t L,
+                        Next next) {
+    EmitState st{0, 0, 0.0f, false};
+    bool done = false;
+    for (;;) {
+        bool full = false;
+        const uint64_t tau = S.tau;
+        while (!full) {
+            if (st.p < st.pe && !emit_pending(st, S, X, tau, m, P.valid)) { full = true; break; }
+            if (done) break;
+            const int r = next(st);
+            if (r == 0) done = true;
+        }
+        if (!__syncthreads_or(full)) break;
+        flush(S, L);
+    }
+}
+
+__device__ __forceinline__ void table_insert(uint32_t* T, uint32_t rel, uint32_t mult) {
+    uint32_t h = (rel * 0x9E3779B1u) >> (32 - 13);
+    static_assert(kTableSlots == 1 << 13, "hash width");
+    const uint32_t want = rel << 8;
+    for (;;) {
+        uint32_t cur = T[h];
+        if (cur == 0) {
+            const uint32_t prev = atomicCAS(&T[h], 0u, want | mult);
+            if (prev == 0) return;
+            cur = prev;
+        }
+        if ((cur >> 8) == rel) {
+            atomicAdd(&T[h], mult);
+            return;
+        }
+        h = (h + 1) & (kTableSlots - 1);
+    }
+}
+
+// Sum of one value per thread for threads < 256 (waves 0..3) into *dst (zeroed by caller).
+__device__ __forceinline__ void small_sum(uint64_t v, unsigned long long* dst) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if ((threadIdx.x & 63) == 0 && threadIdx.x < 256 && v) atomicAdd(dst, (unsigned long long)v);
+}
+
+__global__ __launch_bounds__(kFastThreads) void k_fast(DevIndex X, SearchParams P, const uint8_t* __restrict__ qnorm,
+                                                       const uint64_t* __restrict__ qoff,
+                                                       const uint32_t* __restrict__ qm, uint32_t* __restrict__ out_n,
+                                                       uint32_t* __restrict__ out_k, float* __restrict__ out_s,
+                                                       uint32_t* __restrict__ glist, uint32_t* __restrict__ gcount,
+                                                       DevStats* __restrict__ stats) {
+    __shared__ FastSmem S;
+    const uint32_t q = blockIdx.x, tid = threadIdx.x;
+    const uint32_t m = qm[q];
+    const uint32_t L = P.limit;
+    const size_t ob = (size_t)q * P.out_stride;
+
+    if (m == kQueryWildcard) {  // nGramSearch.hpp:356-369, answer precomputed at index time
+        const uint32_t n = min(L, X.n_keys);
+        for (uint32_t i = tid; i < n; i += kFastThreads) {
+            out_k[ob + i] = X.wild_key[i];
+            out_s[ob + i] = X.wild_score[i];
+        }
+        if (tid == 0) out_n[q] = n;
+        return;
+    }
+    if (m == 0) {
+        if (tid == 0) out_n[q] = 0;
+        return;
+    }
+    if (m <= kFullScanQueryLen || m - 2 > kFastMaxGrams || L > kFastMaxLimit) {
+        if (tid == 0) glist[atomicAdd(gcount, 1u)] = q;  // library-wide path
+        return;
+    }
+    const uint32_t n = m - 2;
+    const uint32_t n_long = X.n_terms - X.n_short;
+    const uint8_t* qg = qnorm + qoff[q];
+    for (uint32_t i = tid; i < m; i += kFastThreads) S.q[i] = qg[i];
+    for (uint32_t i = tid; i < (uint32_t)kTableSlots; i += kFastThreads) S.table[i] = 0;
+    if (tid == 0) {
+        S.cand_n = 0;
+        S.tau = kNoCand;
+        S.ng = 0;
+        S.seg_total = 0;
+    }
+    __syncthreads();
+
+    // ---- searchShort over shortLib (nGramSearch.hpp:262-270), 4 <= m < 9 ----
+    if (m < kShortQueryLen && X.n_short) {
+        uint8_t qc[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) qc[i] = (uint32_t)i < m ? S.q[i] : 0;
+        uint32_t t = tid;
+        const float fm = (float)m;
+        produce(S, X, P, m, L, [&](EmitState& st) -> int {
+            if (t >= X.n_short) return 0;
+            const uint64_t a = X.term_off[t], b = X.term_off[t + 1];
+            const uint32_t match = string_match(qc, m, X.term_bytes + a, (uint32_t)(b - a));
+            const float s = (float)match / fm;  // nGramSearch.hpp:244
+            const uint32_t id = t;
+            t += kFastThreads;
+            if (s < P.thr) return 2;  // nGramSearch.hpp:315
+            st.p = X.tk_off[id];
+            st.pe = X.tk_off[id + 1];
+            st.s = s;
+            st.promo = (double)s > 0.999;
+            return 1;
+        });
+    }
+
+    // ---- searchLong (nGramSearch.hpp:278-301) ----
+    // distinct grams with multiplicity
+    if (tid < n) {
+        const uint32_t c0 = S.q[tid], c1 = S.q[tid + 1], c2 = S.q[tid + 2];
+        S.g_code[tid] = ((c0 | c1 | c2) & 0x80u) ? 0xFFFFFFFFu : (c0 << 14) | (c1 << 7) | c2;
+    }
+    __syncthreads();
+    uint64_t my_len = 0;
+    if (tid < n) {
+        const uint32_t g = S.g_code[tid];
+        bool first = true;
+        uint32_t mult = 0;
+        for (uint32_t j = 0; j < n; ++j) {
+            if (S.g_code[j] == g) {
+                first &= j >= tid;
+                ++mult;
+            }
+        }
+        if (first && g != 0xFFFFFFFFu) {
+            const uint64_t a = X.gram_off[g], b = X.gram_off[g + 1];
+            if (b > a) {
+                const uint32_t slot = atomicAdd(&S.ng, 1u);
+                S.g_cur[slot] = a;
+                S.g_end[slot] = b;
+                S.g_mult[slot] = mult;
+                my_len = b - a;
+            }
+        }
+    }
+    small_sum(my_len, &S.seg_total);
+    __syncthreads();
+    const uint32_t ng = S.ng;
+    const uint64_t p_total = S.seg_total;
+    if (tid == 0) {
+        S.p_left = p_total;
+        S.lo = 0;
+        // first guess of a part's term-id span from the average posting density
+        const uint64_t est = p_total ? (uint64_t)n_long * (kPartCap * 3 / 4) / p_total : n_long;
+        S.step = (uint32_t)max64(1, min64(est, kMaxPartSpan));
+    }
+    __syncthreads();
+
+    while (S.p_left) {
+        const uint32_t lo = S.lo;
+        // choose hi so that the part's postings fit the table at <= 50 % load
+        for (;;) {
+            const bool last = S.p_left <= (uint64_t)kPartCap && n_long - lo <= kMaxPartSpan;
+            const uint32_t hi = last ? n_long : (uint32_t)min64(n_long, (uint64_t)lo + S.step);
+            __syncthreads();
+            if (tid == 0) S.seg_total = 0;
+            __syncthreads();
+            uint64_t cnt = 0;
+            if (tid < ng) {
+                uint64_t a = S.g_cur[tid], b = S.g_end[tid];
+                if (!last) {
+                    while (a < b) {  // lower_bound(post[cur..end), hi)
+                        const uint64_t mid = (a + b) >> 1;
+                        if (X.post[mid] < hi) a = mid + 1; else b = mid;
+                    }
+                }
+                S.g_stop[tid] = a;
+                cnt = a - S.g_cur[tid];
+            }
+            small_sum(cnt, &S.seg_total);
+            __syncthreads();
+            const uint64_t seg = S.seg_total;
+            if (seg <= (uint32_t)kPartCap || hi - lo <= 1) {
+                if (tid == 0) {
+                    S.hi = hi;
+                    const uint64_t grow = seg ? (uint64_t)(hi - lo) * (kPartCap * 3 / 4) / seg : (uint64_t)(hi - lo) * 4;
+                    S.step = (uint32_t)max64(1, min64(max64(grow, 1), kMaxPartSpan));
+                }
+                break;
+            }
+            __syncthreads();
+            if (tid == 0) S.step = (uint32_t)max64(1, (uint64_t)(hi - lo) * (kPartCap * 3 / 4) / seg);
+            __syncthreads();
+        }
+        // segment prefix sums (wave 0; ng <= 255 -> 4 entries per lane)
+        if (tid < 64) {
+            uint32_t v[4], sum = 0;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t g = tid * 4 + u;
+                v[u] = g < ng ? (uint32_t)(S.g_stop[g] - S.g_cur[g]) : 0u;
+                sum += v[u];
+            }
+            uint32_t incl = sum;
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(incl, o);
+                if ((int)tid >= o) incl += y;
+            }
+            uint32_t run = incl - sum;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                S.pre[tid * 4 + u] = run;
+                run += v[u];
+            }
+            if (tid == 63) S.pre[256] = incl;
+        }
+        __syncthreads();
+        const uint32_t lo_part = S.lo;
+        const uint32_t total = S.pre[ng];
+        // count: every posting of the part into the LDS table (4 loads in flight per thread)
+        {
+            uint32_t g = 0;
+            for (uint32_t j0 = tid; j0 < total; j0 += 4 * kFastThreads) {
+                uint32_t tt[4], mu[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const uint32_t j = j0 + u * kFastThreads;
+                    mu[u] = 0;
+                    if (j < total) {
+                        while (S.pre[g + 1] <= j) ++g;
+                        tt[u] = X.post[S.g_cur[g] + (j - S.pre[g])];
+                        mu[u] = S.g_mult[g];
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (mu[u]) table_insert(S.table, tt[u] - lo_part + 1u, mu[u]);
+            }
+        }
+        __syncthreads();
+        // extract: s = count / n, threshold, calcScore; the scan also clears the table
+        {
+            uint32_t i = 0;
+            const float fn = (float)n;
+            produce(S, X, P, m, L, [&](EmitState& st) -> int {
+                if (i >= (uint32_t)(kTableSlots / kFastThreads)) return 0;
+                const uint32_t slot = tid + i * kFastThreads;
+                ++i;
+                const uint32_t v = S.table[slot];
+                if (!v) return 2;
+                S.table[slot] = 0;
+                const uint32_t t = X.n_short + lo_part + (v >> 8) - 1u;
+                const float s = (float)(v & 255u) / fn;  // nGramSearch.hpp:300
+                if (s < P.thr) return 2;                 // nGramSearch.hpp:315
+                st.p = X.tk_off[t];
+                st.pe = X.tk_off[t + 1];
+                st.s = s;
+                st.promo = (double)s > 0.999;            // nGramSearch.hpp:328
+                return 1;
+            });
+        }
+        // next part
+        if (tid < ng) S.g_cur[tid] = S.g_stop[tid];
+        __syncthreads();
+        if (tid == 0) {
+            S.p_left -= total;
+            S.lo = S.hi;
+        }
+        __syncthreads();
+    }
+
+    flush(S, L);
+    const uint32_t nres = S.cand_n;
+    for (uint32_t i = tid; i < nres; i += kFastThreads) {
+        const uint64_t r = S.cand[i];
+        const uint32_t enc = ~(uint32_t)(r >> 32);
+        out_k[ob + i] = (uint32_t)r;
+        out_s[ob + i] = enc == kPromoted ? 100.0f : __uint_as_float(enc - 1u);
+    }
+    if (tid == 0) {
+        out_n[q] = nres;
+        if (stats) {
+            atomicAdd(&stats->postings, (unsigned long long)p_total);
+            atomicAdd(&stats->lists, (unsigned long long)ng);
+            atomicAdd(&stats->results, (unsigned long long)nres);
+            atomicAdd(&stats->fast, 1ull);
+        }
+    }
+}
+
+// ---------------------------------------------------------------- general path -------
+__device__ __forceinline__ void emit_global(const DevIndex& X, uint32_t t, float s, const uint8_t* q, uint32_t m,
+                                            const uint32_t* valid, uint32_t* kenc) {
+    const bool promo = (double)s > 0.999;
+    for (uint32_t p = X.tk_off[t]; p < X.tk_off[t + 1]; ++p) {
+        const uint2 kw = X.tk[p];
+        atomicMax(&kenc[kw.x], pair_enc(kw, s, promo, X, q, m, valid));
+    }
+}
+
+__global__ __launch_bounds__(256) void k_gen_long(DevIndex X, SearchParams P, const uint8_t* __restrict__ qnorm,
+                                                  const uint64_t* __restrict__ qoff, const uint32_t* __restrict__ qm,
+                                                  const uint32_t* __restrict__ group, uint32_t* __restrict__ cnt,
+                                                  uint32_t* __restrict__ kenc, int phase) {
+    const uint32_t gi = blockIdx.y, q = group[gi], m = qm[q];
+    if (m == kQueryWildcard || m < 3) return;  // nGramSearch.hpp:281
+    const uint32_t n = m - 2, n_long = X.n_terms - X.n_short;
+    const uint8_t* qs = qnorm + qoff[q];
+    uint32_t* C = cnt + (size_t)gi * n_long;
+    uint32_t* K = kenc + (size_t)gi * X.n_keys;
+    const uint64_t me = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (uint64_t)gridDim.x * blockDim.x;
+    const float fn = (float)n;
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t c0 = qs[i], c1 = qs[i + 1], c2 = qs[i + 2];
+        if ((c0 | c1 | c2) & 0x80u) continue;
+        const uint32_t g = (c0 << 14) | (c1 << 7) | c2;
+        const uint64_t a = X.gram_off[g], b = X.gram_off[g + 1];
+        for (uint64_t p = a + me; p < b; p += stride) {
+            const uint32_t t = X.post[p];
+            if (phase == 0) {
+                atomicAdd(&C[t], 1u);
+            } else {
+                const uint32_t c = atomicExch(&C[t], 0u);  // first visitor owns the term
+                if (c) {
+                    const float s = (float)c / fn;
+                    if (!(s < P.thr)) emit_global(X, X.n_short + t, s, qs, m, P.valid, K);
+                }
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_gen_short(DevIndex X, SearchParams P, const uint8_t* __restrict__ qnorm,
+                                                   const uint64_t* __restrict__ qoff, const uint32_t* __restrict__ qm,
+                                                   const uint32_t* __restrict__ group, uint32_t* __restrict__ kenc) {
+    const uint32_t gi = blockIdx.y, q = group[gi], m = qm[q];
+    if (m == kQueryWildcard || m == 0 || m >= kShortQueryLen) return;
+    const uint32_t end = m <= kFullScanQueryLen ? X.n_terms : X.n_short;  // nGramSearch.hpp:247
+    const uint8_t* qs = qnorm + qoff[q];
+    uint8_t qc[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) qc[i] = (uint32_t)i < m ? qs[i] : 0;
+    uint32_t* K = kenc + (size_t)gi * X.n_keys;
+    const float fm = (float)m;
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < end; t += gridDim.x * blockDim.x) {
+        const uint64_t a = X.term_off[t], b = X.term_off[t + 1];
+        const float s = (float)string_match(qc, m, X.term_bytes + a, (uint32_t)(b - a)) / fm;
+        if (!(s < P.thr)) emit_global(X, t, s, qs, m, P.valid, K);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_gen_compact(uint32_t n_keys, uint32_t* __restrict__ kenc,
+                                                     uint64_t* __restrict__ list, uint32_t* __restrict__ lcount) {
+    const uint32_t gi = blockIdx.y;
+    uint32_t* K = kenc + (size_t)gi * n_keys;
+    uint64_t* Lst = list + (size_t)gi * n_keys;
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n_keys; k += gridDim.x * blockDim.x) {
+        const uint32_t e = K[k];
+        if (e) {
+            K[k] = 0;
+            Lst[atomicAdd(&lcount[gi], 1u)] = ((uint64_t)(~e) << 32) | k;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_gen_write(const uint64_t* __restrict__ sorted, uint32_t n, uint32_t q,
+                                                   SearchParams P, uint32_t* __restrict__ out_n,
+                                                   uint32_t* __restrict__ out_k, float* __restrict__ out_s) {
+    const uint32_t cnt = min(n, P.limit);
+    const size_t ob = (size_t)q * P.out_stride;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += gridDim.x * blockDim.x) {
+        const uint64_t r = sorted[i];
+        const uint32_t enc = ~(uint32_t)(r >> 32);
+        out_k[ob + i] = (uint32_t)r;
+        out_s[ob + i] = enc == kPromoted ? 100.0f : __uint_as_float(enc - 1u);
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) out_n[q] = cnt;
+}
+
+__global__ void k_wild_records(const float* __restrict__ w, uint32_t n, uint64_t* __restrict__ rec) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const uint32_t b = __float_as_uint(w[k]);
+    const uint32_t ord = b ^ ((b >> 31) ? 0xFFFFFFFFu : 0x80000000u);  // ascending with the float
+    rec[k] = ((uint64_t)(~ord) << 32) | k;                               // score desc, rank asc
+}
+
+__global__ void k_wild_split(const uint64_t* __restrict__ rec, const float* __restrict__ w, uint32_t n,
+                             uint32_t* __restrict__ keys, float* __restrict__ scores) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t k = (uint32_t)rec[i];
+    keys[i] = k;
+    scores[i] = w[k];
+}
+
+}  // namespace
+
+hipError_t build_wildcard(const float* d_w, uint32_t n_keys, uint32_t* d_keys, float* d_scores, hipStream_t s) {
+    if (!n_keys) return hipSuccess;
+    uint64_t *a = nullptr, *b = nullptr;
+    void* temp = nullptr;
+    size_t bytes = 0;
+    hipError_t e = hipcub::DeviceRadixSort::SortKeys(nullptr, bytes, a, b, (int)n_keys, 0, 64, s);
+    if (e == hipSuccess) e = hipMalloc(&a, sizeof(uint64_t) * n_keys);
+    if (e == hipSuccess) e = hipMalloc(&b, sizeof(uint64_t) * n_keys);
+    if (e == hipSuccess) e = hipMalloc(&temp, bytes);
+    if (e == hipSuccess) {
+        const uint32_t gx = (n_keys + 255) / 256;
+        hipLaunchKernelGGL(k_wild_records, dim3(gx), dim3(256), 0, s, d_w, n_keys, a);
+        e = hipcub::DeviceRadixSort::SortKeys(temp, bytes, a, b, (int)n_keys, 0, 64, s);
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(k_wild_split, dim3(gx), dim3(256), 0, s, b, d_w, n_keys, d_keys, d_scores);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+    }
+    hipFree(a);
+    hipFree(b);
+    hipFree(temp);
+    return e;
+}
+
+hipError_t launch_prep(const uint8_t* raw, const uint64_t* off, uint32_t B, const SearchParams& P, uint8_t* qnorm,
+                       uint32_t* qm, hipStream_t s) {
+    if (!B) return hipSuccess;
+    hipLaunchKernelGGL(k_prep, dim3(B), dim3(64), 0, s, raw, off, B, P, qnorm, qm);
+    return hipGetLastError();
+}
+
+hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* qnorm, const uint64_t* off,
+                       const uint32_t* qm, uint32_t* out_n, uint32_t* out_k, float* out_s, uint32_t* glist,
+                       uint32_t* gcount, DevStats* stats, hipStream_t s) {
+    if (!P.n_queries) return hipSuccess;
+    hipLaunchKernelGGL(k_fast, dim3(P.n_queries), dim3(kFastThreads), 0, s, X, P, qnorm, off, qm, out_n, out_k,
+                       out_s, glist, gcount, stats);
+    return hipGetLastError();
+}
+
+size_t general_sort_temp_bytes(uint32_t n_keys) {
+    size_t bytes = 0;
+    hipcub::DeviceRadixSort::SortKeys(nullptr, bytes, (const uint64_t*)nullptr, (uint64_t*)nullptr,
+                                      (int)std::max<uint32_t>(n_keys, 1));
+    return bytes;
+}
+
+hipError_t run_general(const DevIndex& X, const SearchParams& P, const uint8_t* qnorm, const uint64_t* off,
+                       const uint32_t* qm, const uint32_t* d_group, const uint32_t* h_group, uint32_t G,
+                       GeneralBuffers& W, uint32_t* out_n, uint32_t* out_k, float* out_s, hipStream_t s) {
+    const uint32_t n_long = X.n_terms - X.n_short;
+    hipError_t e = hipMemsetAsync(W.lcount, 0, sizeof(uint32_t) * G, s);
+    if (e != hipSuccess) return e;
+    if (n_long) {
+        hipLaunchKernelGGL(k_gen_long, dim3(128, G), dim3(256), 0, s, X, P, qnorm, off, qm, d_group, W.cnt, W.kenc, 0);
+        hipLaunchKernelGGL(k_gen_long, dim3(128, G), dim3(256), 0, s, X, P, qnorm, off, qm, d_group, W.cnt, W.kenc, 1);
+    }
+    if (X.n_terms) {
+        const uint32_t gx = std::min<uint32_t>((X.n_terms + 255) / 256, 2048);
+        hipLaunchKernelGGL(k_gen_short, dim3(gx, G), dim3(256), 0, s, X, P, qnorm, off, qm, d_group, W.kenc);
+    }
+    if (X.n_keys) {
+        const uint32_t gx = std::min<uint32_t>((X.n_keys + 255) / 256, 2048);
+        hipLaunchKernelGGL(k_gen_compact, dim3(gx, G), dim3(256), 0, s, X.n_keys, W.kenc, W.list, W.lcount);
+    }
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    uint32_t counts[64];
+    if (G > 64) return hipErrorInvalidValue;
+    if ((e = hipMemcpyAsync(counts, W.lcount, sizeof(uint32_t) * G, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+    for (uint32_t gi = 0; gi < G; ++gi) {
+        const uint64_t* src = W.list + (size_t)gi * X.n_keys;
+        if (counts[gi] > 1) {
+            size_t bytes = W.temp_bytes;
+            e = hipcub::DeviceRadixSort::SortKeys(W.temp, bytes, src, W.sorted, (int)counts[gi], 0, 64, s);
+            if (e != hipSuccess) return e;
+            src = W.sorted;
+        }
+        const uint32_t cnt = std::min(counts[gi], P.limit);
+        const uint32_t gx = std::max<uint32_t>(1, std::min<uint32_t>((cnt + 255) / 256, 1024));
+        hipLaunchKernelGGL(k_gen_write, dim3(gx), dim3(256), 0, s, src, counts[gi], h_group[gi], P, out_n, out_k, out_s);
+    }
+    return hipGetLastError();
+}
+
+}  // namespace ngs
