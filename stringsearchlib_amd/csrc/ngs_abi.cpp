@@ -252,16 +252,14 @@ int device_search(Library& L, Context& c, const uint8_t* d_raw, const uint64_t* 
     const bool timing = L.timing.load();
     ngs_stats st{};
     st.queries = B;
-    if (timing) {
-        if (!HIP_CHECK(hipMemsetAsync(c.d_stats, 0, sizeof(DevStats), s))) return -4;
-        HIP_CHECK(hipEventRecord(c.ev[0], s));
-    }
+    if (!HIP_CHECK(hipMemsetAsync(c.d_stats, 0, sizeof(DevStats), s))) return -4;
+    if (timing) HIP_CHECK(hipEventRecord(c.ev[0], s));
     if (!HIP_CHECK(launch_prep(d_raw, d_off, B, P, c.d_norm, c.d_qm, s))) return -4;
     if (timing) HIP_CHECK(hipEventRecord(c.ev[1], s));
     if (!HIP_CHECK(hipMemsetAsync(c.d_gcount, 0, sizeof(uint32_t), s))) return -4;
     if (timing) HIP_CHECK(hipEventRecord(c.ev[2], s));
     if (!HIP_CHECK(launch_fast(L.dev, P, c.d_norm, d_off, c.d_qm, d_n, d_k, d_s, c.d_glist, c.d_gcount,
-                               timing ? c.d_stats : nullptr, s)))
+                               c.d_stats, s)))
         return -4;
     if (timing) HIP_CHECK(hipEventRecord(c.ev[3], s));
     uint32_t ngen = 0;
@@ -286,10 +284,15 @@ int device_search(Library& L, Context& c, const uint8_t* d_raw, const uint64_t* 
         }
         if (timing) HIP_CHECK(hipEventRecord(c.ev[5], s));
     }
-    if (!HIP_CHECK(hipStreamSynchronize(s))) return -4;
+    DevStats ds{};
+    if (!HIP_CHECK(hipMemcpyAsync(&ds, c.d_stats, sizeof(ds), hipMemcpyDeviceToHost, s)) ||
+        !HIP_CHECK(hipStreamSynchronize(s)))
+        return -4;
+    if (ds.errors) {
+        std::fprintf(stderr, "ngram_search: fused kernel reported internal error 0x%x\n", ds.errors);
+        return -5;
+    }
     if (timing) {
-        DevStats ds{};
-        HIP_CHECK(hipMemcpy(&ds, c.d_stats, sizeof(ds), hipMemcpyDeviceToHost));
         float ms = 0;
         st.fast_queries = ds.fast;
         st.general_queries = ngen;

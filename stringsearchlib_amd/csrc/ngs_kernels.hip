@@ -213,10 +213,10 @@ __device__ __forceinline__ bool emit_pending(EmitState& st, FastSmem& S, const D
 // whenever any thread finds it full. next(st) -> 0 exhausted, 1 term loaded into st, 2 skip.
 template <class Next>
 __device__ void produce(FastSmem& S, const DevIndex& X, const SearchParams& P, uint32_t m, uint32_t L,
-                        Next next) {
+                        unsigned* err, Next next) {
     EmitState st{0, 0, 0.0f, false};
     bool done = false;
-    for (;;) {
+    for (uint32_t rounds = 0;; ++rounds) {
         bool full = false;
         const uint64_t tau = S.tau;
         while (!full) {
@@ -227,10 +227,15 @@ __device__ void produce(FastSmem& S, const DevIndex& X, const SearchParams& P, u
         }
         if (!__syncthreads_or(full)) break;
         flush(S, L);
+        if (rounds > (1u << 24)) {  // each flush frees >= kCandCap - L slots: unreachable
+            if (threadIdx.x == 0) atomicOr(err, 2u);
+            break;
+        }
     }
 }
 
-__device__ __forceinline__ void table_insert(uint32_t* T, uint32_t rel, uint32_t mult) {
+__device__ __forceinline__ void table_insert(uint32_t* T, uint32_t rel, uint32_t mult, unsigned* err) {
+    uint32_t probes = 0;
     uint32_t h = (rel * 0x9E3779B1u) >> (32 - 13);
     static_assert(kTableSlots == 1 << 13, "hash width");
     const uint32_t want = rel << 8;
@@ -246,6 +251,10 @@ __device__ __forceinline__ void table_insert(uint32_t* T, uint32_t rel, uint32_t
             return;
         }
         h = (h + 1) & (kTableSlots - 1);
+        if (++probes > (uint32_t)kTableSlots) {  // cannot happen at <= 50 % load; never spin
+            atomicOr(err, 1u);
+            return;
+        }
     }
 }
 
@@ -304,7 +313,7 @@ __global__ __launch_bounds__(kFastThreads) void k_fast(DevIndex X, SearchParams 
         for (int i = 0; i < 8; ++i) qc[i] = (uint32_t)i < m ? S.q[i] : 0;
         uint32_t t = tid;
         const float fm = (float)m;
-        produce(S, X, P, m, L, [&](EmitState& st) -> int {
+        produce(S, X, P, m, L, &stats->errors, [&](EmitState& st) -> int {
             if (t >= X.n_short) return 0;
             const uint64_t a = X.term_off[t], b = X.term_off[t + 1];
             const uint32_t match = string_match(qc, m, X.term_bytes + a, (uint32_t)(b - a));
@@ -362,10 +371,14 @@ __global__ __launch_bounds__(kFastThreads) void k_fast(DevIndex X, SearchParams 
     }
     __syncthreads();
 
-    while (S.p_left) {
+    for (uint32_t parts = 0; S.p_left; ++parts) {
         const uint32_t lo = S.lo;
+        if (parts > n_long + 1u) {  // every part advances lo by >= 1: unreachable
+            if (tid == 0) atomicOr(&stats->errors, 4u);
+            break;
+        }
         // choose hi so that the part's postings fit the table at <= 50 % load
-        for (;;) {
+        for (uint32_t tries = 0;; ++tries) {
             const bool last = S.p_left <= (uint64_t)kPartCap && n_long - lo <= kMaxPartSpan;
             const uint32_t hi = last ? n_long : (uint32_t)min64(n_long, (uint64_t)lo + S.step);
             __syncthreads();
@@ -374,7 +387,9 @@ __global__ __launch_bounds__(kFastThreads) void k_fast(DevIndex X, SearchParams 
             uint64_t cnt = 0;
             if (tid < ng) {
                 uint64_t a = S.g_cur[tid], b = S.g_end[tid];
-                if (!last) {
+                if (last) {
+                    a = b;
+                } else {
                     while (a < b) {  // lower_bound(post[cur..end), hi)
                         const uint64_t mid = (a + b) >> 1;
                         if (X.post[mid] < hi) a = mid + 1; else b = mid;
@@ -386,7 +401,7 @@ __global__ __launch_bounds__(kFastThreads) void k_fast(DevIndex X, SearchParams 
             small_sum(cnt, &S.seg_total);
             __syncthreads();
             const uint64_t seg = S.seg_total;
-            if (seg <= (uint32_t)kPartCap || hi - lo <= 1) {
+            if (seg <= (uint64_t)kPartCap || hi - lo <= 1 || tries > 64) {
                 if (tid == 0) {
                     S.hi = hi;
                     const uint64_t grow = seg ? (uint64_t)(hi - lo) * (kPartCap * 3 / 4) / seg : (uint64_t)(hi - lo) * 4;
@@ -440,7 +455,7 @@ __global__ __launch_bounds__(kFastThreads) void k_fast(DevIndex X, SearchParams 
                 }
 #pragma unroll
                 for (int u = 0; u < 4; ++u)
-                    if (mu[u]) table_insert(S.table, tt[u] - lo_part + 1u, mu[u]);
+                    if (mu[u]) table_insert(S.table, tt[u] - lo_part + 1u, mu[u], &stats->errors);
             }
         }
         __syncthreads();
@@ -448,7 +463,7 @@ __global__ __launch_bounds__(kFastThreads) void k_fast(DevIndex X, SearchParams 
         {
             uint32_t i = 0;
             const float fn = (float)n;
-            produce(S, X, P, m, L, [&](EmitState& st) -> int {
+            produce(S, X, P, m, L, &stats->errors, [&](EmitState& st) -> int {
                 if (i >= (uint32_t)(kTableSlots / kFastThreads)) return 0;
                 const uint32_t slot = tid + i * kFastThreads;
                 ++i;
@@ -485,12 +500,10 @@ __global__ __launch_bounds__(kFastThreads) void k_fast(DevIndex X, SearchParams 
     }
     if (tid == 0) {
         out_n[q] = nres;
-        if (stats) {
-            atomicAdd(&stats->postings, (unsigned long long)p_total);
-            atomicAdd(&stats->lists, (unsigned long long)ng);
-            atomicAdd(&stats->results, (unsigned long long)nres);
-            atomicAdd(&stats->fast, 1ull);
-        }
+        atomicAdd(&stats->postings, (unsigned long long)p_total);
+        atomicAdd(&stats->lists, (unsigned long long)ng);
+        atomicAdd(&stats->results, (unsigned long long)nres);
+        atomicAdd(&stats->fast, 1ull);
     }
 }
 
