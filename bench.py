@@ -1,0 +1,254 @@
+#!/usr/bin/env python3
+"""bench.py — Mqueries/s and achieved HBM GB/s of the batched search() path on MI355X.
+
+Workload (BASELINE.json configs[2], the metric's config): 10M-row ASCII corpus, gSize 3,
+per-row float weights, batch of 65,536 queries per GPU, threshold 0.3, limit 100.
+Synthetic data (SURVEY.md §8(d) generator, stringsearchlib_amd/csrc/synth.c), built into
+the index with indexN and uploaded once; queries are resident in HBM before timing.
+
+A step = one ngsSearchDevice call over the GPU's batch (normalise + fused count/score/top-k
+kernel [+ library-wide kernels for the rare queries that need them]); with N > 1 ranks
+(one process per GPU, torchrun) each rank scores its own 65,536 queries (weak scaling) and
+the step also gathers the compacted top-k records on rank 0 over RCCL.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2]
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import torch  # first: libngram_search.so then binds to torch's HIP runtime (one runtime per process)
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import stringsearchlib_amd as ssl  # noqa: E402
+from stringsearchlib_amd import _native, shard  # noqa: E402
+
+METRIC = "Mqueries/sec + achieved HBM GB/s, 10M-row gSize=3 library, batch=65536"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+CONFIGS = {
+    # BASELINE.json configs[2]: the metric's configuration
+    "c3": dict(rows=10_000_000, batch=65536, threshold=0.3, limit=100, weights=True,
+               workload="C3: 10M-row ASCII corpus, gSize=3, rowSize=1, per-row float weights, "
+                        "batch=65536/GPU, threshold=0.3, limit=100"),
+    # BASELINE.json configs[1]
+    "c2": dict(rows=1_000_000, batch=4096, threshold=0.0, limit=100, weights=False,
+               workload="C2: 1M-row ASCII corpus, gSize=3, weight=NULL, batch=4096/GPU, threshold=0, limit=100"),
+}
+
+
+def log(rank, *a):
+    if rank == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+class Corpus:
+    """Synthetic rows + queries in C memory (10M rows would be slow as Python objects)."""
+
+    def __init__(self, rows: int, seed: int = 42):
+        S = _native.synth()
+        self.S, self.rows = S, rows
+        self.blob, self.words, self.weights, self.state = C.c_void_p(), C.POINTER(C.c_char_p)(), \
+            C.POINTER(C.c_float)(), C.c_uint64()
+        if S.ngs_synth_corpus(rows, seed, 8, 17, 1, C.byref(self.blob), C.byref(self.words), C.byref(self.weights),
+                              C.byref(self.state)):
+            raise MemoryError("synthetic corpus")
+
+    def queries(self, n: int, skip: int = 0):
+        """n queries after `skip` queries of the stream (rank slices of one global stream)."""
+        st = C.c_uint64(self.state.value)
+        qb, qo = C.c_void_p(), C.POINTER(C.c_uint64)()
+        if self.S.ngs_synth_queries(self.words, self.rows, 1, skip + n, C.byref(st), 12, C.byref(qb), C.byref(qo)):
+            raise MemoryError("synthetic queries")
+        lo, hi = qo[skip], qo[skip + n]
+        raw = C.string_at(qb.value + lo, hi - lo)
+        offs = [qo[skip + i] - lo for i in range(n + 1)]
+        self.S.ngs_synth_free(qb)
+        self.S.ngs_synth_free(C.cast(qo, C.c_void_p))
+        return raw, offs
+
+    def free(self):
+        for p in (self.blob, C.cast(self.words, C.c_void_p), C.cast(self.weights, C.c_void_p)):
+            self.S.ngs_synth_free(p)
+
+
+def build_index(corpus: Corpus, weights: bool, device: int) -> int:
+    L = _native.lib()
+    if L.ngsSetDevice(device):
+        raise RuntimeError(f"ngsSetDevice({device}) failed")
+    h = L.indexN(corpus.words, corpus.rows, 1, corpus.weights if weights else None)
+    if not h:
+        raise RuntimeError("indexN failed")
+    return h
+
+
+def cpu_baseline(corpus: Corpus, cfg: dict, raw: bytes, offs: list, target_s: float = 12.0):
+    """Time the oracle (oracle/, the CPU restatement of the reference path) on host cores."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_py
+    O = oracle_py.lib()
+    threads = max(1, min(16, os.cpu_count() or 1))
+    t0 = time.time()
+    h = O.ngo_build(corpus.words, corpus.rows, 1, corpus.weights if cfg["weights"] else None)
+    build_s = time.time() - t0
+    qs = [raw[offs[i]:offs[i + 1]] for i in range(len(offs) - 1)]
+    cap = cfg["limit"]
+
+    def run(n):
+        sample = [qs[i % len(qs)] for i in range(n)]
+        arr = (C.c_char_p * n)(*sample)
+        counts = (C.c_uint32 * n)()
+        keys = (C.c_uint32 * (n * cap))()
+        scores = (C.c_float * (n * cap))()
+        t = time.time()
+        O.ngo_search_batch(h, arr, n, cfg["threshold"], cfg["limit"], counts, keys, scores, cap, threads)
+        return time.time() - t
+
+    n = 1024
+    dt = run(n)
+    while dt < 2.0 and n < 1 << 22:
+        n *= 4
+        dt = run(n)
+    if dt < target_s:
+        n = min(1 << 23, int(n * target_s / max(dt, 1e-3)))
+        dt = run(n)
+    O.ngo_free(h)
+    return {"value": n / dt, "unit": "queries/s", "cores": threads, "kind": "port",
+            "sample": f"{n} queries of the same stream ({cfg['workload'].split(',')[0]} index, "
+                      f"threshold {cfg['threshold']}, limit {cfg['limit']}), oracle/ngs_oracle.c on {threads} "
+                      f"host threads; index build {build_s:.1f}s not timed"}
+
+
+def pmc_traffic(cfg_name: str):
+    """HBM bytes per fused-kernel launch from a committed rocprofv3 PMC pass, if any."""
+    p = os.path.join(ROOT, "profiles", f"pmc_{cfg_name}.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        with open(p) as f:
+            return json.load(f).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--rows", type=int, default=None, help="override corpus rows (debug only)")
+    ap.add_argument("--batch", type=int, default=None, help="override per-GPU batch (debug only)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+    cfg = dict(CONFIGS[args.config])
+    if args.rows:
+        cfg["rows"] = args.rows
+    if args.batch:
+        cfg["batch"] = args.batch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    t0 = time.time()
+    corpus = Corpus(cfg["rows"])
+    h = build_index(corpus, cfg["weights"], local)
+    index_s = time.time() - t0
+    L = _native.lib()
+    n_keys = L.ngsNumKeys(h)
+    log(rank, f"[bench] {cfg['workload']}: index built+uploaded in {index_s:.1f}s, "
+              f"{L.getSize(h)} terms, {L.getLibSize(h)} grams")
+
+    B = cfg["batch"]
+    raw, offs = corpus.queries(B, skip=rank * B)
+    d_raw = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(dev)
+    d_off = torch.tensor(offs, dtype=torch.int64, device=dev)
+    stride = min(cfg["limit"], n_keys)
+    d_cnt = torch.zeros(B, dtype=torch.int32, device=dev)
+    d_key = torch.zeros(B * stride, dtype=torch.int32, device=dev)
+    d_sc = torch.zeros(B * stride, dtype=torch.float32, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    L.ngsSetTiming(h, 1)
+    st = _native.NgsStats()
+
+    def step():
+        rc = L.ngsSearchDevice(h, d_raw.data_ptr(), d_off.data_ptr(), B, cfg["threshold"], cfg["limit"], stride,
+                               d_cnt.data_ptr(), d_key.data_ptr(), d_sc.data_ptr(), stream)
+        if rc:
+            raise RuntimeError(f"ngsSearchDevice -> {rc}")
+        L.ngsLastStats(h, C.byref(st))
+        if world > 1:
+            c, k, s = shard.compact(d_cnt, d_key, d_sc, stride)
+            shard.gather_to_root(c, k, s)
+        return st.fast_kernel_ms, st.prep_kernel_ms, st.general_ms
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t_start = time.perf_counter()
+    ktimes = []
+    for _ in range(args.steps):
+        ktimes.append(step())
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    if world > 1:
+        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+
+    # per-launch algorithmic bytes of the fused kernel
+    qbytes = offs[-1]
+    alg_bytes = (4 * st.postings + 16 * st.lists + qbytes + 16 * st.survivors + 8 * st.results + 4 * B)
+    fast_ms = sum(k[0] for k in ktimes) / len(ktimes)
+    achieved = alg_bytes / (fast_ms * 1e-3) / 1e9
+    total_q = B * world * args.steps
+    value = total_q / elapsed / 1e6
+    out = {
+        "metric": METRIC, "value": round(value, 4), "unit": "Mqueries/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+        "config": {"workload": cfg["workload"], "rows": cfg["rows"], "batch_per_gpu": B,
+                   "threshold": cfg["threshold"], "limit": cfg["limit"], "weights": cfg["weights"],
+                   "parallelism": f"query-shard x{world}" + (" + RCCL gather of top-k" if world > 1 else "")},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(args.config),
+                     "kernel": "k_fast", "kernel_ms": round(fast_ms, 4), "alg_bytes_per_launch": alg_bytes,
+                     "postings_per_query": round(st.postings / max(1, st.fast_queries), 1)},
+        "detail": {"prep_ms": round(sum(k[1] for k in ktimes) / len(ktimes), 4),
+                   "general_ms": round(sum(k[2] for k in ktimes) / len(ktimes), 4),
+                   "general_queries": int(st.general_queries), "results_per_query": round(st.results / B, 2),
+                   "survivors_per_query": round(st.survivors / B, 2), "index_build_s": round(index_s, 1)},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(corpus, cfg, raw, offs)
+    else:
+        out["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    L.dispose(h)
+    corpus.free()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -111,7 +111,8 @@ typedef struct {
     uint64_t general_queries;  /* handled by the dense library-wide kernels */
     uint64_t postings;         /* sum over fast queries of posting ids read (distinct grams) */
     uint64_t lists;            /* posting lists opened */
-    uint64_t results;          /* results written */
+    uint64_t results;          /* results written by the fused kernel */
+    uint64_t survivors;        /* terms whose match ratio passed the threshold (fused kernel) */
     double fast_kernel_ms;     /* fused kernel time from HIP events on the call's stream */
     double prep_kernel_ms;     /* normalisation kernel time */
     double general_ms;         /* general path time (all its kernels) */

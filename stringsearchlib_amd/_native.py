@@ -22,7 +22,7 @@ CSRC = os.path.join(PKG, "csrc")
 
 class NgsStats(C.Structure):
     _fields_ = [("queries", C.c_uint64), ("fast_queries", C.c_uint64), ("general_queries", C.c_uint64),
-                ("postings", C.c_uint64), ("lists", C.c_uint64), ("results", C.c_uint64),
+                ("postings", C.c_uint64), ("lists", C.c_uint64), ("results", C.c_uint64), ("survivors", C.c_uint64),
                 ("fast_kernel_ms", C.c_double), ("prep_kernel_ms", C.c_double), ("general_ms", C.c_double)]
 
 

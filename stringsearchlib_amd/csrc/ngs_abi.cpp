@@ -299,6 +299,7 @@ int device_search(Library& L, Context& c, const uint8_t* d_raw, const uint64_t* 
         st.postings = ds.postings;
         st.lists = ds.lists;
         st.results = ds.results;
+        st.survivors = ds.survivors;
         if (hipEventElapsedTime(&ms, c.ev[0], c.ev[1]) == hipSuccess) st.prep_kernel_ms = ms;
         if (hipEventElapsedTime(&ms, c.ev[2], c.ev[3]) == hipSuccess) st.fast_kernel_ms = ms;
         if (ngen && hipEventElapsedTime(&ms, c.ev[4], c.ev[5]) == hipSuccess) st.general_ms = ms;

@@ -72,6 +72,7 @@ struct DevStats {  // accumulated by the fused kernel (one atomic per block)
     unsigned long long lists;
     unsigned long long results;
     unsigned long long fast;
+    unsigned long long survivors;  // scored terms that passed the threshold
     unsigned errors;  // bit 0 table overflow, 1 flush rounds, 2 part rounds: all "cannot happen"
     unsigned pad;
 };

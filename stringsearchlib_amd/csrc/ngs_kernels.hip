@@ -122,7 +122,7 @@ struct FastSmem {
     uint64_t tau;                  // records >= tau cannot enter the top-L
     uint64_t p_left;
     unsigned long long seg_total;
-    uint32_t ng, cand_n, n_valid, pad0;
+    uint32_t ng, cand_n, n_valid, survivors;
     uint32_t lo, hi, step, pad;
 };
 
@@ -303,8 +303,11 @@ __global__ __launch_bounds__(kFastThreads) void k_fast(DevIndex X, SearchParams 
         S.tau = kNoCand;
         S.ng = 0;
         S.seg_total = 0;
+        S.survivors = 0;
     }
     __syncthreads();
+
+    uint32_t surv = 0;  // terms of this thread that passed the threshold (stats only)
 
     // ---- searchShort over shortLib (nGramSearch.hpp:262-270), 4 <= m < 9 ----
     if (m < kShortQueryLen && X.n_short) {
@@ -321,6 +324,7 @@ __global__ __launch_bounds__(kFastThreads) void k_fast(DevIndex X, SearchParams 
             const uint32_t id = t;
             t += kFastThreads;
             if (s < P.thr) return 2;  // nGramSearch.hpp:315
+            ++surv;
             st.p = X.tk_off[id];
             st.pe = X.tk_off[id + 1];
             st.s = s;
@@ -473,6 +477,7 @@ __global__ __launch_bounds__(kFastThreads) void k_fast(DevIndex X, SearchParams 
                 const uint32_t t = X.n_short + lo_part + (v >> 8) - 1u;
                 const float s = (float)(v & 255u) / fn;  // nGramSearch.hpp:300
                 if (s < P.thr) return 2;                 // nGramSearch.hpp:315
+                ++surv;
                 st.p = X.tk_off[t];
                 st.pe = X.tk_off[t + 1];
                 st.s = s;
@@ -490,6 +495,7 @@ __global__ __launch_bounds__(kFastThreads) void k_fast(DevIndex X, SearchParams 
         __syncthreads();
     }
 
+    if (surv) atomicAdd(&S.survivors, surv);
     flush(S, L);
     const uint32_t nres = S.cand_n;
     for (uint32_t i = tid; i < nres; i += kFastThreads) {
@@ -504,6 +510,7 @@ __global__ __launch_bounds__(kFastThreads) void k_fast(DevIndex X, SearchParams 
         atomicAdd(&stats->lists, (unsigned long long)ng);
         atomicAdd(&stats->results, (unsigned long long)nres);
         atomicAdd(&stats->fast, 1ull);
+        atomicAdd(&stats->survivors, (unsigned long long)S.survivors);
     }
 }
 

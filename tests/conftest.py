@@ -5,6 +5,11 @@ import sys
 
 import pytest
 
+try:  # one HIP runtime per process: torch's bundled runtime must be loaded before the library
+    import torch  # noqa: F401  (libngram_search.so then binds to it by SONAME)
+except ImportError:  # pragma: no cover
+    torch = None
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
