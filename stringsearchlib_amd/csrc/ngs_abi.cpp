@@ -147,7 +147,7 @@ bool upload(Library& L) {
     X.n_keys = H.n_keys;
     std::vector<uint8_t> kb(H.key_bytes.begin(), H.key_bytes.end());
     uint64_t *gram_off, *term_off, *key_off;
-    uint32_t *post, *tk_off, *wild_key;
+    uint32_t *post, *tk_off, *wild_key, *gram_row, *skip;
     uint8_t *term_bytes, *key_bytes;
     uint2* tk;
     float *wild_w, *wild_score;
@@ -156,7 +156,8 @@ bool upload(Library& L) {
               dev_upload(&term_off, H.term_off, L.owned) && dev_upload(&term_bytes, H.term_bytes, L.owned) &&
               dev_upload(&tk_off, H.tk_off, L.owned) && dev_upload(&tk, H.tk, L.owned) &&
               dev_upload(&key_off, H.key_off, L.owned) && dev_upload(&key_bytes, kb, L.owned) &&
-              dev_upload(&wild_w, H.wild_w, L.owned);
+              dev_upload(&wild_w, H.wild_w, L.owned) && dev_upload(&gram_row, H.gram_row, L.owned) &&
+              dev_upload(&skip, H.skip, L.owned);
     if (!ok) return false;
     if (!dev_alloc(&wild_key, H.n_keys)) return false;
     L.owned.push_back(wild_key);
@@ -165,6 +166,10 @@ bool upload(Library& L) {
     if (!HIP_CHECK(build_wildcard(wild_w, H.n_keys, wild_key, wild_score, nullptr))) return false;
     X.gram_off = gram_off;
     X.post = post;
+    X.gram_row = gram_row;
+    X.skip = skip;
+    X.n_buckets = H.n_buckets;
+    X.bucket_span = H.bucket_span;
     X.term_off = term_off;
     X.term_bytes = term_bytes;
     X.tk_off = tk_off;
@@ -176,6 +181,8 @@ bool upload(Library& L) {
     // the device copy is authoritative for the search; keep only what marshalling needs
     std::vector<uint64_t>().swap(H.gram_off);
     std::vector<uint32_t>().swap(H.post);
+    std::vector<uint32_t>().swap(H.gram_row);
+    std::vector<uint32_t>().swap(H.skip);
     std::vector<uint64_t>().swap(H.term_off);
     std::vector<uint8_t>().swap(H.term_bytes);
     std::vector<uint32_t>().swap(H.tk_off);

@@ -42,9 +42,16 @@ constexpr uint32_t kFastMaxLimit = kCandCap / 2;
 constexpr uint32_t kFastMaxGrams = 255;  // u8 counts in the table slot
 constexpr uint32_t kMaxPartSpan = (1u << 24) - 2;  // 24-bit relative term id in the slot
 
+// bucket skip table: K <= kMaxBuckets term-id buckets of >= kMinBucketTerms terms each
+constexpr uint32_t kMaxBuckets = 64;
+constexpr uint32_t kMinBucketTerms = 4096;
+
 struct DevIndex {  // passed by value to kernels; all pointers are device pointers
     const uint64_t* gram_off;   // [kGramSpace + 1] -> post
     const uint32_t* post;       // long-term ids (0-based within longLib), sorted per gram
+    const uint32_t* gram_row;   // [kGramSpace] -> row of skip (UINT32_MAX = empty)
+    const uint32_t* skip;       // [rows][n_buckets + 1] offset of the first posting >= b * bucket_span
+    uint32_t n_buckets, bucket_span;
     const uint64_t* term_off;   // [n_terms + 1] -> term_bytes (normalised terms)
     const uint8_t* term_bytes;
     const uint32_t* tk_off;     // [n_terms + 1] -> tk

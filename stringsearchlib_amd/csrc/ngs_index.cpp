@@ -288,6 +288,38 @@ void build_index(HostIndex& ix, char* const* words, uint64_t size, uint16_t rowS
             for (uint32_t i = 0; i < n; ++i) ix.post[cur[g[i]]++] = id - ix.n_short;
         }
     });
+    counts.clear();
+
+    // bucket skip table: for every non-empty list, the offset of its first posting in each of
+    // K equal term-id buckets. Lets a query cut its lists into term-id parts with one load per
+    // (gram, bucket) instead of a binary search (DESIGN.md §Index layout).
+    ix.n_buckets = 1;
+    while (ix.n_buckets < kMaxBuckets && (uint64_t)ix.n_buckets * kMinBucketTerms < n_long) ix.n_buckets <<= 1;
+    ix.bucket_span = n_long ? (n_long + ix.n_buckets - 1) / ix.n_buckets : 1;
+    ix.gram_row.assign(kGramSpace, UINT32_MAX);
+    std::vector<uint32_t> rows;
+    for (uint32_t g = 0; g < kGramSpace; ++g)
+        if (ix.gram_off[g + 1] > ix.gram_off[g]) {
+            ix.gram_row[g] = (uint32_t)rows.size();
+            rows.push_back(g);
+        }
+    const uint32_t K = ix.n_buckets;
+    ix.skip.assign((size_t)rows.size() * (K + 1), 0);
+    run([&](unsigned t) {
+        for (size_t r = t; r < rows.size(); r += threads) {
+            const uint32_t g = rows[r];
+            const uint32_t* p = ix.post.data() + ix.gram_off[g];
+            const uint32_t len = (uint32_t)(ix.gram_off[g + 1] - ix.gram_off[g]);
+            uint32_t* out = ix.skip.data() + r * (K + 1);
+            uint32_t i = 0;
+            for (uint32_t b = 0; b <= K; ++b) {
+                const uint64_t lo = (uint64_t)b * ix.bucket_span;
+                while (i < len && p[i] < lo) ++i;
+                out[b] = i;
+            }
+            out[K] = len;
+        }
+    });
     ix.indexed = true;                                                    // hpp:45
 }
 

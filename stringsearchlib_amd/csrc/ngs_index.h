@@ -24,6 +24,9 @@ struct HostIndex {
     uint64_t n_grams = 0;                   // distinct grams -> getLibSize
     std::vector<uint64_t> gram_off;         // kGramSpace + 1
     std::vector<uint32_t> post;
+    uint32_t n_buckets = 1, bucket_span = 1; // term-id buckets of the skip table
+    std::vector<uint32_t> gram_row;         // kGramSpace: row of the skip table, UINT32_MAX = empty list
+    std::vector<uint32_t> skip;             // rows x (n_buckets + 1) list offsets
     std::vector<uint64_t> term_off;
     std::vector<uint8_t> term_bytes;
     std::vector<uint32_t> tk_off;

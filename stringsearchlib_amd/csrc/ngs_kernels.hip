@@ -112,18 +112,22 @@ __device__ __forceinline__ uint32_t string_match(const uint8_t (&qc)[8], uint32_
 struct FastSmem {
     uint32_t table[kTableSlots];   // (term - lo + 1) << 8 | count
     uint64_t cand[kCandCap];       // (~enc) << 32 | key
-    uint64_t g_cur[256];           // per distinct gram: next posting to read
-    uint64_t g_end[256];           // end of its list
+    uint64_t g_base[256];          // per distinct gram: start of its posting list
+    uint64_t g_cur[256];           // first posting of the current part
+    uint64_t g_end[256];           // end of the current bucket range
     uint64_t g_stop[256];          // end of the current part's segment
+    uint32_t g_row[256];           // skip-table row
     uint32_t g_mult[256];          // multiplicity of the gram in the query
     uint32_t g_code[256];
+    uint32_t btot[kMaxBuckets];    // postings per term-id bucket
+    uint2 part[kMaxBuckets];       // parts: bucket range [x, y & 0x7fffffff), y >> 31 = oversized
     uint32_t pre[260];             // segment prefix sums
     uint8_t q[264];
     uint64_t tau;                  // records >= tau cannot enter the top-L
     uint64_t p_left;
     unsigned long long seg_total;
     uint32_t ng, cand_n, n_valid, survivors;
-    uint32_t lo, hi, step, pad;
+    uint32_t nparts, pad1, pad2, pad3;
 };
 
 __device__ __forceinline__ uint32_t next_pow2(uint32_t x) { return x <= 1 ? 1u : 1u << (32 - __clz(x - 1)); }
@@ -264,6 +268,79 @@ __device__ __forceinline__ void small_sum(uint64_t v, unsigned long long* dst) {
     if ((threadIdx.x & 63) == 0 && threadIdx.x < 256 && v) atomicAdd(dst, (unsigned long long)v);
 }
 
+// One term-id part of searchLong: the segments [g_cur, g_stop) of every distinct gram hold
+// the postings with term ids in [lo, lo + span) (span < 2^24). Counts them in the LDS table
+// (<= 50 % load), then scans the table: s = count / n, threshold, calcScore.
+__device__ void long_part(FastSmem& S, const DevIndex& X, const SearchParams& P, uint32_t m, uint32_t n,
+                          uint32_t L, uint32_t lo, uint32_t ng, uint32_t& surv, unsigned* err) {
+    const uint32_t tid = threadIdx.x;
+    // segment prefix sums (wave 0; ng <= 255 -> 4 entries per lane)
+    if (tid < 64) {
+        uint32_t v[4], sum = 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t g = tid * 4 + u;
+            v[u] = g < ng ? (uint32_t)(S.g_stop[g] - S.g_cur[g]) : 0u;
+            sum += v[u];
+        }
+        uint32_t incl = sum;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o);
+            if ((int)tid >= o) incl += y;
+        }
+        uint32_t run = incl - sum;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            S.pre[tid * 4 + u] = run;
+            run += v[u];
+        }
+        if (tid == 63) S.pre[256] = incl;
+    }
+    __syncthreads();
+    const uint32_t total = S.pre[ng];
+    // count: every posting of the part into the LDS table (4 loads in flight per thread)
+    {
+        uint32_t g = 0;
+        for (uint32_t j0 = tid; j0 < total; j0 += 4 * kFastThreads) {
+            uint32_t tt[4], mu[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t j = j0 + u * kFastThreads;
+                mu[u] = 0;
+                if (j < total) {
+                    while (S.pre[g + 1] <= j) ++g;
+                    tt[u] = X.post[S.g_cur[g] + (j - S.pre[g])];
+                    mu[u] = S.g_mult[g];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (mu[u]) table_insert(S.table, tt[u] - lo + 1u, mu[u], err);
+        }
+    }
+    __syncthreads();
+    // extract: s = count / n, threshold, calcScore; the scan also clears the table
+    uint32_t i = 0;
+    const float fn = (float)n;
+    produce(S, X, P, m, L, err, [&](EmitState& st) -> int {
+        if (i >= (uint32_t)(kTableSlots / kFastThreads)) return 0;
+        const uint32_t slot = tid + i * kFastThreads;
+        ++i;
+        const uint32_t v = S.table[slot];
+        if (!v) return 2;
+        S.table[slot] = 0;
+        const uint32_t t = X.n_short + lo + (v >> 8) - 1u;
+        const float s = (float)(v & 255u) / fn;  // nGramSearch.hpp:300
+        if (s < P.thr) return 2;                 // nGramSearch.hpp:315
+        ++surv;
+        st.p = X.tk_off[t];
+        st.pe = X.tk_off[t + 1];
+        st.s = s;
+        st.promo = (double)s > 0.999;            // nGramSearch.hpp:328
+        return 1;
+    });
+}
+
 __global__ __launch_bounds__(kFastThreads) void k_fast(DevIndex X, SearchParams P, const uint8_t* __restrict__ qnorm,
                                                        const uint64_t* __restrict__ qoff,
                                                        const uint32_t* __restrict__ qm, uint32_t* __restrict__ out_n,
@@ -339,6 +416,7 @@ __global__ __launch_bounds__(kFastThreads) void k_fast(DevIndex X, SearchParams 
         const uint32_t c0 = S.q[tid], c1 = S.q[tid + 1], c2 = S.q[tid + 2];
         S.g_code[tid] = ((c0 | c1 | c2) & 0x80u) ? 0xFFFFFFFFu : (c0 << 14) | (c1 << 7) | c2;
     }
+    if (tid < kMaxBuckets) S.btot[tid] = 0;
     __syncthreads();
     uint64_t my_len = 0;
     if (tid < n) {
@@ -355,8 +433,8 @@ __global__ __launch_bounds__(kFastThreads) void k_fast(DevIndex X, SearchParams 
             const uint64_t a = X.gram_off[g], b = X.gram_off[g + 1];
             if (b > a) {
                 const uint32_t slot = atomicAdd(&S.ng, 1u);
-                S.g_cur[slot] = a;
-                S.g_end[slot] = b;
+                S.g_base[slot] = a;
+                S.g_row[slot] = X.gram_row[g];
                 S.g_mult[slot] = mult;
                 my_len = b - a;
             }
@@ -366,133 +444,101 @@ __global__ __launch_bounds__(kFastThreads) void k_fast(DevIndex X, SearchParams 
     __syncthreads();
     const uint32_t ng = S.ng;
     const uint64_t p_total = S.seg_total;
-    if (tid == 0) {
-        S.p_left = p_total;
-        S.lo = 0;
-        // first guess of a part's term-id span from the average posting density
-        const uint64_t est = p_total ? (uint64_t)n_long * (kPartCap * 3 / 4) / p_total : n_long;
-        S.step = (uint32_t)max64(1, min64(est, kMaxPartSpan));
+    const uint32_t K = X.n_buckets, span = X.bucket_span;
+    // postings per term-id bucket, straight from the skip table
+    const bool one_part = p_total <= (uint64_t)kPartCap && n_long <= kMaxPartSpan;
+    if (!one_part) {
+        for (uint32_t idx = tid; idx < ng * K; idx += kFastThreads) {
+            const uint32_t g = idx / K, b = idx - g * K;
+            const uint32_t* sk = X.skip + (size_t)S.g_row[g] * (K + 1);
+            const uint32_t c = sk[b + 1] - sk[b];
+            if (c) atomicAdd(&S.btot[b], c);
+        }
     }
     __syncthreads();
-
-    for (uint32_t parts = 0; S.p_left; ++parts) {
-        const uint32_t lo = S.lo;
-        if (parts > n_long + 1u) {  // every part advances lo by >= 1: unreachable
-            if (tid == 0) atomicOr(&stats->errors, 4u);
-            break;
+    // greedy cut of the bucket sequence into parts of <= kPartCap postings (<= 50 % table load);
+    // a bucket alone above the cap becomes an "oversized" part, split by term id below
+    if (tid == 0) {
+        uint32_t np = 0;
+        if (one_part) {
+            if (p_total) S.part[np++] = make_uint2(0, K);
+        } else {
+            uint32_t b = 0;
+            while (b < K) {
+                if (S.btot[b] > (uint32_t)kPartCap || span > kMaxPartSpan) {
+                    if (S.btot[b]) S.part[np++] = make_uint2(b, (b + 1) | 0x80000000u);
+                    ++b;
+                    continue;
+                }
+                const uint32_t blo = b;
+                uint32_t tot = 0;
+                while (b < K && tot + S.btot[b] <= (uint32_t)kPartCap &&
+                       (uint64_t)(b + 1 - blo) * span <= kMaxPartSpan) tot += S.btot[b++];
+                if (tot) S.part[np++] = make_uint2(blo, b);
+            }
         }
-        // choose hi so that the part's postings fit the table at <= 50 % load
-        for (uint32_t tries = 0;; ++tries) {
-            const bool last = S.p_left <= (uint64_t)kPartCap && n_long - lo <= kMaxPartSpan;
-            const uint32_t hi = last ? n_long : (uint32_t)min64(n_long, (uint64_t)lo + S.step);
+        S.nparts = np;
+    }
+    __syncthreads();
+    const uint32_t nparts = S.nparts;
+    for (uint32_t pi = 0; pi < nparts; ++pi) {
+        const uint2 pr = S.part[pi];
+        const bool over = pr.y >> 31;
+        const uint32_t blo = pr.x, bhi = pr.y & 0x7FFFFFFFu;
+        const uint32_t lo_id = blo * span;
+        const uint32_t hi_id = (uint32_t)min64((uint64_t)bhi * span, n_long);
+        if (tid < ng) {
+            const uint32_t* sk = X.skip + (size_t)S.g_row[tid] * (K + 1);
+            S.g_cur[tid] = S.g_base[tid] + sk[blo];
+            S.g_end[tid] = S.g_base[tid] + sk[bhi];
+        }
+        __syncthreads();
+        if (!over) {
+            if (tid < ng) S.g_stop[tid] = S.g_end[tid];
             __syncthreads();
-            if (tid == 0) S.seg_total = 0;
-            __syncthreads();
-            uint64_t cnt = 0;
-            if (tid < ng) {
-                uint64_t a = S.g_cur[tid], b = S.g_end[tid];
-                if (last) {
-                    a = b;
-                } else {
+            long_part(S, X, P, m, n, L, lo_id, ng, surv, &stats->errors);
+            continue;
+        }
+        // oversized bucket: adaptive term-id sub-parts, lower_bound per list (rare)
+        uint32_t sub_lo = lo_id;
+        uint32_t step = (uint32_t)max64(1, min64((uint64_t)(hi_id - lo_id) * (kPartCap * 3 / 4) / S.btot[blo],
+                                                  kMaxPartSpan));
+        for (uint32_t guard = 0; sub_lo < hi_id; ++guard) {
+            if (guard > hi_id - lo_id + 1u) {
+                if (tid == 0) atomicOr(&stats->errors, 4u);
+                break;
+            }
+            uint32_t hi = 0;
+            for (uint32_t tries = 0;; ++tries) {
+                hi = (uint32_t)min64(hi_id, (uint64_t)sub_lo + step);
+                __syncthreads();
+                if (tid == 0) S.seg_total = 0;
+                __syncthreads();
+                uint64_t cnt = 0;
+                if (tid < ng) {
+                    uint64_t a = S.g_cur[tid], b = S.g_end[tid];
                     while (a < b) {  // lower_bound(post[cur..end), hi)
                         const uint64_t mid = (a + b) >> 1;
                         if (X.post[mid] < hi) a = mid + 1; else b = mid;
                     }
+                    S.g_stop[tid] = a;
+                    cnt = a - S.g_cur[tid];
                 }
-                S.g_stop[tid] = a;
-                cnt = a - S.g_cur[tid];
-            }
-            small_sum(cnt, &S.seg_total);
-            __syncthreads();
-            const uint64_t seg = S.seg_total;
-            if (seg <= (uint64_t)kPartCap || hi - lo <= 1 || tries > 64) {
-                if (tid == 0) {
-                    S.hi = hi;
-                    const uint64_t grow = seg ? (uint64_t)(hi - lo) * (kPartCap * 3 / 4) / seg : (uint64_t)(hi - lo) * 4;
-                    S.step = (uint32_t)max64(1, min64(max64(grow, 1), kMaxPartSpan));
+                small_sum(cnt, &S.seg_total);
+                __syncthreads();
+                const uint64_t seg = S.seg_total;
+                if (seg <= (uint64_t)kPartCap || hi - sub_lo <= 1 || tries > 64) {
+                    step = (uint32_t)max64(1, min64(seg ? (uint64_t)(hi - sub_lo) * (kPartCap * 3 / 4) / seg
+                                                        : (uint64_t)(hi - sub_lo) * 4, kMaxPartSpan));
+                    break;
                 }
-                break;
+                step = (uint32_t)max64(1, min64((uint64_t)(hi - sub_lo) * (kPartCap * 3 / 4) / seg, kMaxPartSpan));
             }
+            long_part(S, X, P, m, n, L, sub_lo, ng, surv, &stats->errors);
+            if (tid < ng) S.g_cur[tid] = S.g_stop[tid];
             __syncthreads();
-            if (tid == 0) S.step = (uint32_t)max64(1, (uint64_t)(hi - lo) * (kPartCap * 3 / 4) / seg);
-            __syncthreads();
+            sub_lo = hi;
         }
-        // segment prefix sums (wave 0; ng <= 255 -> 4 entries per lane)
-        if (tid < 64) {
-            uint32_t v[4], sum = 0;
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const uint32_t g = tid * 4 + u;
-                v[u] = g < ng ? (uint32_t)(S.g_stop[g] - S.g_cur[g]) : 0u;
-                sum += v[u];
-            }
-            uint32_t incl = sum;
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t y = __shfl_up(incl, o);
-                if ((int)tid >= o) incl += y;
-            }
-            uint32_t run = incl - sum;
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                S.pre[tid * 4 + u] = run;
-                run += v[u];
-            }
-            if (tid == 63) S.pre[256] = incl;
-        }
-        __syncthreads();
-        const uint32_t lo_part = S.lo;
-        const uint32_t total = S.pre[ng];
-        // count: every posting of the part into the LDS table (4 loads in flight per thread)
-        {
-            uint32_t g = 0;
-            for (uint32_t j0 = tid; j0 < total; j0 += 4 * kFastThreads) {
-                uint32_t tt[4], mu[4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const uint32_t j = j0 + u * kFastThreads;
-                    mu[u] = 0;
-                    if (j < total) {
-                        while (S.pre[g + 1] <= j) ++g;
-                        tt[u] = X.post[S.g_cur[g] + (j - S.pre[g])];
-                        mu[u] = S.g_mult[g];
-                    }
-                }
-#pragma unroll
-                for (int u = 0; u < 4; ++u)
-                    if (mu[u]) table_insert(S.table, tt[u] - lo_part + 1u, mu[u], &stats->errors);
-            }
-        }
-        __syncthreads();
-        // extract: s = count / n, threshold, calcScore; the scan also clears the table
-        {
-            uint32_t i = 0;
-            const float fn = (float)n;
-            produce(S, X, P, m, L, &stats->errors, [&](EmitState& st) -> int {
-                if (i >= (uint32_t)(kTableSlots / kFastThreads)) return 0;
-                const uint32_t slot = tid + i * kFastThreads;
-                ++i;
-                const uint32_t v = S.table[slot];
-                if (!v) return 2;
-                S.table[slot] = 0;
-                const uint32_t t = X.n_short + lo_part + (v >> 8) - 1u;
-                const float s = (float)(v & 255u) / fn;  // nGramSearch.hpp:300
-                if (s < P.thr) return 2;                 // nGramSearch.hpp:315
-                ++surv;
-                st.p = X.tk_off[t];
-                st.pe = X.tk_off[t + 1];
-                st.s = s;
-                st.promo = (double)s > 0.999;            // nGramSearch.hpp:328
-                return 1;
-            });
-        }
-        // next part
-        if (tid < ng) S.g_cur[tid] = S.g_stop[tid];
-        __syncthreads();
-        if (tid == 0) {
-            S.p_left -= total;
-            S.lo = S.hi;
-        }
-        __syncthreads();
     }
 
     if (surv) atomicAdd(&S.survivors, surv);
