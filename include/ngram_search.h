@@ -123,6 +123,10 @@ NGS_API int ngsLastStats(uint32_t handle, ngs_stats* out);
 /* Library build identification (e.g. "gfx950 ngram_search 0.1"). */
 NGS_API const char* ngsVersion(void);
 
+/* Diagnostics: per-phase block time of the fused kernel (100 MHz ticks, summed over blocks)
+ * in the instrumented build libngram_search_prof.so; -1 in the regular build. */
+NGS_API int ngsPhaseStats(uint64_t* out, int n, int reset);
+
 #ifdef __cplusplus
 }
 #endif

@@ -14,7 +14,9 @@ import subprocess
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 LIB_DIR = os.path.join(PKG, "lib")
-LIB_PATH = os.path.join(LIB_DIR, "libngram_search.so")
+# NGS_LIB=prof selects the phase-stamped diagnostic build (make -C csrc prof)
+LIB_PATH = os.path.join(LIB_DIR, "libngram_search_prof.so" if os.environ.get("NGS_LIB") == "prof"
+                        else "libngram_search.so")
 SYNTH_PATH = os.path.join(LIB_DIR, "libngs_synth.so")
 HEADER = os.path.join(ROOT, "include", "ngram_search.h")
 CSRC = os.path.join(PKG, "csrc")
@@ -82,6 +84,8 @@ def lib():
     L.ngsLastStats.argtypes = [u32, C.POINTER(NgsStats)]
     L.ngsVersion.restype = cp
     L.ngsVersion.argtypes = []
+    L.ngsPhaseStats.restype = C.c_int
+    L.ngsPhaseStats.argtypes = [C.POINTER(C.c_uint64), C.c_int, C.c_int]
     _lib = L
     return L
 

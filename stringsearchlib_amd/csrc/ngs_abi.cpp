@@ -59,7 +59,8 @@ struct Context {
     uint8_t* d_norm = nullptr;
     uint32_t* d_qm = nullptr;
     uint32_t* d_glist = nullptr;
-    uint32_t* d_gcount = nullptr;
+    uint32_t* d_list2 = nullptr;
+    uint32_t* d_gcount = nullptr;  // [0] general-path count, [1] tier-2 count
     uint32_t* d_group = nullptr;
     DevStats* d_stats = nullptr;
     uint32_t* d_n = nullptr;
@@ -71,7 +72,7 @@ struct Context {
 
     ~Context() {
         hipSetDevice(device);
-        for (void* p : {(void*)d_raw, (void*)d_off, (void*)d_norm, (void*)d_qm, (void*)d_glist, (void*)d_gcount,
+        for (void* p : {(void*)d_raw, (void*)d_off, (void*)d_norm, (void*)d_qm, (void*)d_glist, (void*)d_list2, (void*)d_gcount,
                         (void*)d_group, (void*)d_stats, (void*)d_n, (void*)d_k, (void*)d_s, (void*)gen.cnt,
                         (void*)gen.kenc, (void*)gen.list, (void*)gen.sorted, (void*)gen.lcount, gen.temp})
             if (p) hipFree(p);
@@ -117,7 +118,7 @@ struct Library {
         if (!HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking))) return nullptr;
         for (hipEvent_t& e : c->ev)
             if (!HIP_CHECK(hipEventCreate(&e))) return nullptr;
-        if (!dev_alloc(&c->d_gcount, 1) || !dev_alloc(&c->d_group, 64) || !dev_alloc(&c->d_stats, 1)) return nullptr;
+        if (!dev_alloc(&c->d_gcount, 2) || !dev_alloc(&c->d_group, 64) || !dev_alloc(&c->d_stats, 1)) return nullptr;
         return c;
     }
     void give_back(std::unique_ptr<Context> c) {
@@ -193,10 +194,12 @@ bool upload(Library& L) {
 
 bool ensure_queries(Context& c, size_t B, size_t bytes) {
     if (B > c.bcap) {
-        for (void** p : {(void**)&c.d_off, (void**)&c.d_qm, (void**)&c.d_glist})
+        for (void** p : {(void**)&c.d_off, (void**)&c.d_qm, (void**)&c.d_glist, (void**)&c.d_list2})
             if (*p) { hipFree(*p); *p = nullptr; }
         size_t nb = std::max<size_t>(B, 1024);
-        if (!dev_alloc(&c.d_off, nb + 1) || !dev_alloc(&c.d_qm, nb) || !dev_alloc(&c.d_glist, nb)) return false;
+        if (!dev_alloc(&c.d_off, nb + 1) || !dev_alloc(&c.d_qm, nb) || !dev_alloc(&c.d_glist, nb) ||
+            !dev_alloc(&c.d_list2, nb))
+            return false;
         c.bcap = nb;
     }
     if (bytes > c.qcap) {
@@ -263,10 +266,10 @@ int device_search(Library& L, Context& c, const uint8_t* d_raw, const uint64_t* 
     if (timing) HIP_CHECK(hipEventRecord(c.ev[0], s));
     if (!HIP_CHECK(launch_prep(d_raw, d_off, B, P, c.d_norm, c.d_qm, s))) return -4;
     if (timing) HIP_CHECK(hipEventRecord(c.ev[1], s));
-    if (!HIP_CHECK(hipMemsetAsync(c.d_gcount, 0, sizeof(uint32_t), s))) return -4;
+    if (!HIP_CHECK(hipMemsetAsync(c.d_gcount, 0, 2 * sizeof(uint32_t), s))) return -4;
     if (timing) HIP_CHECK(hipEventRecord(c.ev[2], s));
-    if (!HIP_CHECK(launch_fast(L.dev, P, c.d_norm, d_off, c.d_qm, d_n, d_k, d_s, c.d_glist, c.d_gcount,
-                               c.d_stats, s)))
+    if (!HIP_CHECK(launch_fast(L.dev, P, c.d_norm, d_off, c.d_qm, d_n, d_k, d_s, c.d_list2, c.d_gcount + 1,
+                               c.d_glist, c.d_gcount, c.d_stats, s)))
         return -4;
     if (timing) HIP_CHECK(hipEventRecord(c.ev[3], s));
     uint32_t ngen = 0;
@@ -571,5 +574,9 @@ NGS_API int ngsLastStats(uint32_t handle, ngs_stats* out) {
 }
 
 NGS_API const char* ngsVersion(void) { return "ngram_search 0.1 gfx950"; }
+
+NGS_API int ngsPhaseStats(uint64_t* out, int n, int reset) {
+    return phase_stats((unsigned long long*)out, n, reset != 0);
+}
 
 }  // extern "C"

@@ -46,6 +46,15 @@ constexpr uint32_t kMaxPartSpan = (1u << 24) - 2;  // 24-bit relative term id in
 constexpr uint32_t kMaxBuckets = 64;
 constexpr uint32_t kMinBucketTerms = 4096;
 
+// ---- wave kernel geometry (tier 1: one wave per query) ----
+constexpr int kWaveSlotBits = 11;
+constexpr int kWaveSlots = 1 << kWaveSlotBits;  // wave-private LDS hash table
+constexpr int kWaveCap = kWaveSlots / 2;        // postings per part (<= 50 % load)
+constexpr int kWaveCand = 256;                  // candidate buffer per query
+constexpr uint32_t kWaveMaxLimit = kWaveCand / 2;
+constexpr int kWaveSurv = 512;                  // survivor list (term, score) before calcScore
+constexpr uint32_t kWaveMaxGrams = 64;
+
 struct DevIndex {  // passed by value to kernels; all pointers are device pointers
     const uint64_t* gram_off;   // [kGramSpace + 1] -> post
     const uint32_t* post;       // long-term ids (0-based within longLib), sorted per gram

@@ -15,9 +15,11 @@ hipError_t launch_prep(const uint8_t* raw, const uint64_t* off, uint32_t B, cons
 // Fused per-query kernel: short Levenshtein scan of shortLib (4 <= m < 9), 3-gram posting
 // count in an LDS hash table per term-id part, threshold, term->key weighting, per-key max
 // merge and top-L in LDS. Queries it cannot take are appended to glist for the general path.
+// Tier 1 (k_wave, one wave per query: <= 64 grams, limit <= 128) then tier 2 (k_fast, one block
+// per query over list2: <= 255 grams, limit <= 1024); what remains goes to glist.
 hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* qnorm, const uint64_t* off,
-                       const uint32_t* qm, uint32_t* out_n, uint32_t* out_k, float* out_s, uint32_t* glist,
-                       uint32_t* gcount, DevStats* stats, hipStream_t s);
+                       const uint32_t* qm, uint32_t* out_n, uint32_t* out_k, float* out_s, uint32_t* list2,
+                       uint32_t* count2, uint32_t* glist, uint32_t* gcount, DevStats* stats, hipStream_t s);
 
 // Wildcard answer (nGramSearch.hpp:356-369): keys sorted by (weight desc, rank asc).
 hipError_t build_wildcard(const float* d_w, uint32_t n_keys, uint32_t* d_keys, float* d_scores, hipStream_t s);
@@ -35,6 +37,10 @@ struct GeneralBuffers {
     size_t temp_bytes = 0;
 };
 size_t general_sort_temp_bytes(uint32_t n_keys);
+
+// Diagnostic build (make prof, -DNGS_PHASE_STAMPS): accumulated block-time per k_fast phase in
+// 100 MHz ticks. Returns the number of phases, or -1 in the regular build.
+int phase_stats(unsigned long long* out, int n, bool reset);
 hipError_t run_general(const DevIndex& X, const SearchParams& P, const uint8_t* qnorm, const uint64_t* off,
                        const uint32_t* qm, const uint32_t* d_group, const uint32_t* h_group, uint32_t G,
                        GeneralBuffers& W, uint32_t* out_n, uint32_t* out_k, float* out_s, hipStream_t s);

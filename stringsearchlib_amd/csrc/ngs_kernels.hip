@@ -17,6 +17,19 @@
 namespace ngs {
 namespace {
 
+#ifdef NGS_PHASE_STAMPS
+// Diagnostic build only (make prof): block-time per phase of k_fast, in 100 MHz ticks.
+__device__ unsigned long long g_phase[16];
+#define STAMP(i)                                                          \
+    if (threadIdx.x == 0) {                                               \
+        const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();   \
+        atomicAdd(&g_phase[i], t_ - tp_);                                 \
+        tp_ = t_;                                                         \
+    }
+#else
+#define STAMP(i)
+#endif
+
 __device__ __forceinline__ uint64_t min64(uint64_t a, uint64_t b) { return a < b ? a : b; }
 __device__ __forceinline__ uint64_t max64(uint64_t a, uint64_t b) { return a > b ? a : b; }
 __device__ __forceinline__ bool dev_space(unsigned c) { return c == 32u || (c >= 9u && c <= 13u); }
@@ -272,7 +285,8 @@ __device__ __forceinline__ void small_sum(uint64_t v, unsigned long long* dst) {
 // the postings with term ids in [lo, lo + span) (span < 2^24). Counts them in the LDS table
 // (<= 50 % load), then scans the table: s = count / n, threshold, calcScore.
 __device__ void long_part(FastSmem& S, const DevIndex& X, const SearchParams& P, uint32_t m, uint32_t n,
-                          uint32_t L, uint32_t lo, uint32_t ng, uint32_t& surv, unsigned* err) {
+                          uint32_t L, uint32_t lo, uint32_t ng, uint32_t& surv, unsigned* err,
+                          unsigned long long& tp_) {
     const uint32_t tid = threadIdx.x;
     // segment prefix sums (wave 0; ng <= 255 -> 4 entries per lane)
     if (tid < 64) {
@@ -297,6 +311,7 @@ __device__ void long_part(FastSmem& S, const DevIndex& X, const SearchParams& P,
         if (tid == 63) S.pre[256] = incl;
     }
     __syncthreads();
+    STAMP(6);
     const uint32_t total = S.pre[ng];
     // count: every posting of the part into the LDS table (4 loads in flight per thread)
     {
@@ -319,6 +334,7 @@ __device__ void long_part(FastSmem& S, const DevIndex& X, const SearchParams& P,
         }
     }
     __syncthreads();
+    STAMP(7);
     // extract: s = count / n, threshold, calcScore; the scan also clears the table
     uint32_t i = 0;
     const float fn = (float)n;
@@ -339,16 +355,20 @@ __device__ void long_part(FastSmem& S, const DevIndex& X, const SearchParams& P,
         st.promo = (double)s > 0.999;            // nGramSearch.hpp:328
         return 1;
     });
+    STAMP(8);
 }
 
-__global__ __launch_bounds__(kFastThreads) void k_fast(DevIndex X, SearchParams P, const uint8_t* __restrict__ qnorm,
-                                                       const uint64_t* __restrict__ qoff,
-                                                       const uint32_t* __restrict__ qm, uint32_t* __restrict__ out_n,
-                                                       uint32_t* __restrict__ out_k, float* __restrict__ out_s,
-                                                       uint32_t* __restrict__ glist, uint32_t* __restrict__ gcount,
-                                                       DevStats* __restrict__ stats) {
-    __shared__ FastSmem S;
-    const uint32_t q = blockIdx.x, tid = threadIdx.x;
+// Tier 2: one 512-thread block per query (queries of up to 255 grams, limits up to 1024).
+__device__ void fast_one(const uint32_t q, FastSmem& S, const DevIndex& X, const SearchParams& P,
+                         const uint8_t* __restrict__ qnorm, const uint64_t* __restrict__ qoff,
+                         const uint32_t* __restrict__ qm, uint32_t* __restrict__ out_n, uint32_t* __restrict__ out_k,
+                         float* __restrict__ out_s, uint32_t* __restrict__ glist, uint32_t* __restrict__ gcount,
+                         DevStats* __restrict__ stats) {
+    const uint32_t tid = threadIdx.x;
+    unsigned long long tp_ = 0;
+#ifdef NGS_PHASE_STAMPS
+    if (tid == 0) tp_ = __builtin_amdgcn_s_memrealtime();
+#endif
     const uint32_t m = qm[q];
     const uint32_t L = P.limit;
     const size_t ob = (size_t)q * P.out_stride;
@@ -383,6 +403,7 @@ __global__ __launch_bounds__(kFastThreads) void k_fast(DevIndex X, SearchParams 
         S.survivors = 0;
     }
     __syncthreads();
+    STAMP(0);
 
     uint32_t surv = 0;  // terms of this thread that passed the threshold (stats only)
 
@@ -410,6 +431,7 @@ __global__ __launch_bounds__(kFastThreads) void k_fast(DevIndex X, SearchParams 
         });
     }
 
+    STAMP(1);
     // ---- searchLong (nGramSearch.hpp:278-301) ----
     // distinct grams with multiplicity
     if (tid < n) {
@@ -442,6 +464,7 @@ __global__ __launch_bounds__(kFastThreads) void k_fast(DevIndex X, SearchParams 
     }
     small_sum(my_len, &S.seg_total);
     __syncthreads();
+    STAMP(2);
     const uint32_t ng = S.ng;
     const uint64_t p_total = S.seg_total;
     const uint32_t K = X.n_buckets, span = X.bucket_span;
@@ -456,6 +479,7 @@ __global__ __launch_bounds__(kFastThreads) void k_fast(DevIndex X, SearchParams 
         }
     }
     __syncthreads();
+    STAMP(3);
     // greedy cut of the bucket sequence into parts of <= kPartCap postings (<= 50 % table load);
     // a bucket alone above the cap becomes an "oversized" part, split by term id below
     if (tid == 0) {
@@ -480,6 +504,7 @@ __global__ __launch_bounds__(kFastThreads) void k_fast(DevIndex X, SearchParams 
         S.nparts = np;
     }
     __syncthreads();
+    STAMP(4);
     const uint32_t nparts = S.nparts;
     for (uint32_t pi = 0; pi < nparts; ++pi) {
         const uint2 pr = S.part[pi];
@@ -493,10 +518,11 @@ __global__ __launch_bounds__(kFastThreads) void k_fast(DevIndex X, SearchParams 
             S.g_end[tid] = S.g_base[tid] + sk[bhi];
         }
         __syncthreads();
+        STAMP(5);
         if (!over) {
             if (tid < ng) S.g_stop[tid] = S.g_end[tid];
             __syncthreads();
-            long_part(S, X, P, m, n, L, lo_id, ng, surv, &stats->errors);
+            long_part(S, X, P, m, n, L, lo_id, ng, surv, &stats->errors, tp_);
             continue;
         }
         // oversized bucket: adaptive term-id sub-parts, lower_bound per list (rare)
@@ -534,7 +560,7 @@ __global__ __launch_bounds__(kFastThreads) void k_fast(DevIndex X, SearchParams 
                 }
                 step = (uint32_t)max64(1, min64((uint64_t)(hi - sub_lo) * (kPartCap * 3 / 4) / seg, kMaxPartSpan));
             }
-            long_part(S, X, P, m, n, L, sub_lo, ng, surv, &stats->errors);
+            long_part(S, X, P, m, n, L, sub_lo, ng, surv, &stats->errors, tp_);
             if (tid < ng) S.g_cur[tid] = S.g_stop[tid];
             __syncthreads();
             sub_lo = hi;
@@ -542,7 +568,9 @@ __global__ __launch_bounds__(kFastThreads) void k_fast(DevIndex X, SearchParams 
     }
 
     if (surv) atomicAdd(&S.survivors, surv);
+    STAMP(9);
     flush(S, L);
+    STAMP(10);
     const uint32_t nres = S.cand_n;
     for (uint32_t i = tid; i < nres; i += kFastThreads) {
         const uint64_t r = S.cand[i];
@@ -557,6 +585,412 @@ __global__ __launch_bounds__(kFastThreads) void k_fast(DevIndex X, SearchParams 
         atomicAdd(&stats->results, (unsigned long long)nres);
         atomicAdd(&stats->fast, 1ull);
         atomicAdd(&stats->survivors, (unsigned long long)S.survivors);
+    }
+    STAMP(11);
+}
+
+__global__ __launch_bounds__(kFastThreads) void k_fast(DevIndex X, SearchParams P, const uint8_t* __restrict__ qnorm,
+                                                       const uint64_t* __restrict__ qoff,
+                                                       const uint32_t* __restrict__ qm, uint32_t* __restrict__ out_n,
+                                                       uint32_t* __restrict__ out_k, float* __restrict__ out_s,
+                                                       const uint32_t* __restrict__ qlist,
+                                                       const uint32_t* __restrict__ qcount,
+                                                       uint32_t* __restrict__ glist, uint32_t* __restrict__ gcount,
+                                                       DevStats* __restrict__ stats) {
+    __shared__ FastSmem S;
+    const uint32_t cnt = *qcount;
+    for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
+        fast_one(qlist[i], S, X, P, qnorm, qoff, qm, out_n, out_k, out_s, glist, gcount, stats);
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------- wave kernel --------
+// Tier 1: ONE WAVE PER QUERY with a wave-private LDS table. No block barriers, ~11 queries
+// in flight per CU; the only dependent global round trips per query are the gram lists'
+// offsets, one posting sweep per term-id part and one batched calcScore for the survivors.
+struct WaveSmem {
+    uint32_t table[kWaveSlots];  // (term - lo + 1) << 8 | count
+    uint64_t cand[kWaveCand];    // (~enc) << 32 | key
+    uint2 surv[kWaveSurv];       // (term, score bits) that passed the threshold
+    uint64_t seg_start[64];      // current part: first posting of each gram's segment
+    uint32_t seg_pre[68];        // exclusive prefix of segment lengths
+    uint32_t seg_mult[64];
+    uint8_t q[kWaveMaxGrams + 8];
+    uint32_t surv_total;         // stats: survivors of this query
+};
+
+__device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
+__device__ __forceinline__ unsigned long long lanes_below() { return (1ull << lane_id()) - 1ull; }
+
+template <class T>
+__device__ __forceinline__ T wave_sum(T v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// Wave-local running top-L over the candidate buffer (same algorithm as flush()).
+__device__ void wave_flush(WaveSmem& S, uint32_t& cand_n, uint64_t& tau, uint32_t L) {
+    const uint32_t lane = lane_id();
+    const uint32_t n = min(cand_n, (uint32_t)kWaveCand);
+    const uint32_t P2 = next_pow2(max(n, 2u));
+    for (uint32_t i = lane; i < P2; i += 64) {
+        const uint64_t r = i < n ? S.cand[i] : kNoCand;
+        S.cand[i] = i < n ? ((r << 32) | (r >> 32)) : kNoCand;
+    }
+    __syncthreads();
+    for (int pass = 0; pass < 2; ++pass) {
+        for (uint32_t k = 2; k <= P2; k <<= 1) {
+            for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                for (uint32_t p = lane; p < P2 / 2; p += 64) {
+                    const uint32_t i = (p / j) * 2 * j + (p % j), l = i + j;
+                    const uint64_t x = S.cand[i], y = S.cand[l];
+                    if ((x > y) == ((i & k) == 0)) { S.cand[i] = y; S.cand[l] = x; }
+                }
+                __syncthreads();
+            }
+        }
+        if (pass == 1) break;
+        uint64_t keep[kWaveCand / 64];
+#pragma unroll
+        for (int u = 0; u < kWaveCand / 64; ++u) {
+            const uint32_t i = lane + u * 64;
+            keep[u] = kNoCand;
+            if (i < P2) {
+                const uint64_t d = S.cand[i];
+                if (d != kNoCand && (i == 0 || (S.cand[i - 1] >> 32) != (d >> 32))) keep[u] = (d << 32) | (d >> 32);
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < kWaveCand / 64; ++u) {
+            const uint32_t i = lane + u * 64;
+            if (i < P2) S.cand[i] = keep[u];
+        }
+        __syncthreads();
+    }
+    uint32_t mine = 0;
+    for (uint32_t i = lane; i < P2; i += 64) mine += S.cand[i] != kNoCand;
+    const uint32_t nv = wave_sum(mine);
+    cand_n = min(nv, L);
+    tau = nv >= L ? S.cand[L - 1] : kNoCand;
+    __syncthreads();
+}
+
+// calcScore (nGramSearch.hpp:310-341) for the survivor list: term -> (key, weight) pairs,
+// max(w*s, 0), exact-match promotion, appended to the candidate buffer.
+__device__ void wave_emit(WaveSmem& S, const DevIndex& X, const SearchParams& P, uint32_t m, uint32_t L,
+                          uint32_t& surv_n, uint32_t& cand_n, uint64_t& tau) {
+    const uint32_t lane = lane_id();
+    S.surv_total += surv_n;
+    __syncthreads();
+    for (uint32_t base = 0; base < surv_n; base += 64) {
+        const uint32_t i = base + lane;
+        uint32_t p = 0, pe = 0;
+        float s = 0.0f;
+        if (i < surv_n) {
+            const uint2 e = S.surv[i];
+            p = X.tk_off[e.x];
+            pe = X.tk_off[e.x + 1];
+            s = __uint_as_float(e.y);
+        }
+        const bool promo = (double)s > 0.999;  // nGramSearch.hpp:328
+        while (__ballot(p < pe)) {
+            uint64_t rec = kNoCand;
+            if (p < pe) {
+                const uint2 kw = X.tk[p++];
+                const uint32_t enc = pair_enc(kw, s, promo, X, S.q, m, P.valid);
+                rec = ((uint64_t)(~enc) << 32) | kw.x;
+            }
+            if (cand_n + 64 > (uint32_t)kWaveCand) wave_flush(S, cand_n, tau, L);
+            const bool want = rec < tau;
+            const unsigned long long b = __ballot(want);
+            if (want) S.cand[cand_n + __popcll(b & lanes_below())] = rec;
+            cand_n += __popcll(b);
+        }
+    }
+    surv_n = 0;
+    __syncthreads();
+}
+
+__device__ __forceinline__ void wave_insert(uint32_t* T, uint32_t rel, uint32_t mult, unsigned* err) {
+    uint32_t probes = 0;
+    uint32_t h = (rel * 0x9E3779B1u) >> (32 - kWaveSlotBits);
+    const uint32_t want = rel << 8;
+    for (;;) {
+        uint32_t cur = T[h];
+        if (cur == 0) {
+            const uint32_t prev = atomicCAS(&T[h], 0u, want | mult);
+            if (prev == 0) return;
+            cur = prev;
+        }
+        if ((cur >> 8) == rel) {
+            atomicAdd(&T[h], mult);
+            return;
+        }
+        h = (h + 1) & (kWaveSlots - 1);
+        if (++probes > (uint32_t)kWaveSlots) {
+            atomicOr(err, 1u);
+            return;
+        }
+    }
+}
+
+// One term-id part: lane g < ng owns gram g's segment [base+cur, base+cur+len) of terms in
+// [lo, lo + 2^24). Counts it in the wave's table, then scans the table: count >= cmin ->
+// survivor (score = sc_lane(count), the precomputed (float)count / n).
+__device__ void wave_part(WaveSmem& S, const DevIndex& X, const SearchParams& P, uint32_t m, uint32_t L,
+                          uint32_t lo, uint32_t ng, uint64_t seg_start, uint32_t seg_len, uint32_t mult,
+                          uint32_t cmin, float sc_lane, uint32_t& surv_n, uint32_t& cand_n, uint64_t& tau,
+                          unsigned* err) {
+    const uint32_t lane = lane_id();
+    uint32_t incl = lane < ng ? seg_len : 0u;
+    const uint32_t mine = incl;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o);
+        if ((int)lane >= o) incl += y;
+    }
+    const uint32_t total = __shfl(incl, 63);
+    if (lane < ng) {
+        S.seg_start[lane] = seg_start;
+        S.seg_pre[lane] = incl - mine;
+        S.seg_mult[lane] = mult;
+    }
+    if (lane == 0) S.seg_pre[ng] = total;
+    __syncthreads();
+    uint32_t g = 0;
+    for (uint32_t j0 = lane; j0 < total; j0 += 8 * 64) {
+        uint32_t tt[8], mu[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const uint32_t j = j0 + u * 64;
+            mu[u] = 0;
+            if (j < total) {
+                while (S.seg_pre[g + 1] <= j) ++g;
+                tt[u] = X.post[S.seg_start[g] + (j - S.seg_pre[g])];
+                mu[u] = S.seg_mult[g];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (mu[u]) wave_insert(S.table, tt[u] - lo + 1u, mu[u], err);
+    }
+    __syncthreads();
+    // scan + clear, 4 slots per lane per step
+    uint4* T4 = reinterpret_cast<uint4*>(S.table);
+    for (uint32_t i = lane; i < (uint32_t)kWaveSlots / 4; i += 64) {
+        if (surv_n + 256 > (uint32_t)kWaveSurv) wave_emit(S, X, P, m, L, surv_n, cand_n, tau);
+        const uint4 v = T4[i];
+        T4[i] = make_uint4(0, 0, 0, 0);
+        const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const uint32_t cnt = vv[c] & 255u;
+            const float s = __shfl(sc_lane, (int)cnt);  // (float)count / n, nGramSearch.hpp:300
+            const bool pass = vv[c] != 0 && cnt >= cmin; // !(s < thr), nGramSearch.hpp:315
+            const unsigned long long b = __ballot(pass);
+            if (pass)
+                S.surv[surv_n + __popcll(b & lanes_below())] =
+                    make_uint2(X.n_short + lo + (vv[c] >> 8) - 1u, __float_as_uint(s));
+            surv_n += __popcll(b);
+        }
+    }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(64) void k_wave(DevIndex X, SearchParams P, const uint8_t* __restrict__ qnorm,
+                                             const uint64_t* __restrict__ qoff, const uint32_t* __restrict__ qm,
+                                             uint32_t* __restrict__ out_n, uint32_t* __restrict__ out_k,
+                                             float* __restrict__ out_s, uint32_t* __restrict__ list2,
+                                             uint32_t* __restrict__ count2, DevStats* __restrict__ stats) {
+    __shared__ WaveSmem S;
+    const uint32_t q = blockIdx.x, lane = lane_id();
+    const uint32_t m = qm[q];
+    const uint32_t L = P.limit;
+    const size_t ob = (size_t)q * P.out_stride;
+    if (m == kQueryWildcard) {  // nGramSearch.hpp:356-369, answer precomputed at index time
+        const uint32_t n = min(L, X.n_keys);
+        for (uint32_t i = lane; i < n; i += 64) {
+            out_k[ob + i] = X.wild_key[i];
+            out_s[ob + i] = X.wild_score[i];
+        }
+        if (lane == 0) out_n[q] = n;
+        return;
+    }
+    if (m == 0) {  // nothing left after normalisation, nGramSearch.hpp:374-375
+        if (lane == 0) out_n[q] = 0;
+        return;
+    }
+    if (m <= kFullScanQueryLen || m - 2 > kWaveMaxGrams || L > kWaveMaxLimit) {
+        if (lane == 0) list2[atomicAdd(count2, 1u)] = q;  // tier 2 / library-wide path
+        return;
+    }
+    const uint32_t n = m - 2;
+    const uint32_t n_long = X.n_terms - X.n_short;
+    const uint8_t* qg = qnorm + qoff[q];
+    for (uint32_t i = lane; i < m; i += 64) S.q[i] = qg[i];
+    if (lane == 0) S.surv_total = 0;
+    {
+        uint4* T4 = reinterpret_cast<uint4*>(S.table);
+        for (uint32_t i = lane; i < (uint32_t)kWaveSlots / 4; i += 64) T4[i] = make_uint4(0, 0, 0, 0);
+    }
+    __syncthreads();
+    uint32_t cand_n = 0, surv_n = 0;
+    uint64_t tau = kNoCand;
+    unsigned* err = &stats->errors;
+
+    // ---- searchShort over shortLib (nGramSearch.hpp:262-270), 4 <= m < 9 ----
+    if (m < kShortQueryLen && X.n_short) {
+        uint8_t qc[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) qc[i] = (uint32_t)i < m ? S.q[i] : 0;
+        const float s_lane = lane <= m ? (float)lane / (float)m : 0.0f;  // nGramSearch.hpp:244
+        const bool ok_lane = lane <= m && !(s_lane < P.thr);
+        const unsigned long long okm = __ballot(ok_lane);
+        const uint32_t cmin_s = okm ? (uint32_t)(__ffsll((long long)okm) - 1) : 64u;
+        for (uint32_t t0 = 0; t0 < X.n_short; t0 += 64) {
+            if (surv_n + 64 > (uint32_t)kWaveSurv) wave_emit(S, X, P, m, L, surv_n, cand_n, tau);
+            const uint32_t t = t0 + lane;
+            uint32_t match = 0;
+            if (t < X.n_short) {
+                const uint64_t a = X.term_off[t], b = X.term_off[t + 1];
+                match = string_match(qc, m, X.term_bytes + a, (uint32_t)(b - a));
+            }
+            const float s = __shfl(s_lane, (int)match);
+            const bool pass = t < X.n_short && match >= cmin_s;
+            const unsigned long long bb = __ballot(pass);
+            if (pass) S.surv[surv_n + __popcll(bb & lanes_below())] = make_uint2(t, __float_as_uint(s));
+            surv_n += __popcll(bb);
+        }
+    }
+
+    // ---- searchLong (nGramSearch.hpp:278-301) ----
+    // lane i: gram i of the query; dedup with multiplicity; lane g < ng then owns a distinct gram
+    uint32_t code = 0xFFFFFFFFu;
+    if (lane < n) {
+        const uint32_t c0 = S.q[lane], c1 = S.q[lane + 1], c2 = S.q[lane + 2];
+        if (!((c0 | c1 | c2) & 0x80u)) code = (c0 << 14) | (c1 << 7) | c2;
+    }
+    uint32_t mult = 0;
+    bool first = true;
+    for (uint32_t j = 0; j < n; ++j) {
+        const uint32_t cj = __shfl(code, (int)j);
+        if (cj == code) {
+            mult += 1;
+            first &= j >= lane;
+        }
+    }
+    uint64_t gbase = 0, glen = 0;
+    uint32_t grow = 0;
+    bool have = false;
+    if (lane < n && first && code != 0xFFFFFFFFu) {
+        gbase = X.gram_off[code];
+        glen = X.gram_off[code + 1] - gbase;
+        grow = X.gram_row[code];
+        have = glen != 0;
+    }
+    const unsigned long long hb = __ballot(have);
+    const uint32_t ng = __popcll(hb);
+    const uint32_t slot = __popcll(hb & lanes_below());
+    // compact the distinct non-empty grams into lanes 0..ng-1
+    {
+        uint32_t src = 0;
+        unsigned long long rest = hb;
+        for (uint32_t k = 0; k <= lane && rest; ++k) {  // lane k takes the k-th set bit
+            src = __ffsll((long long)rest) - 1;
+            rest &= rest - 1;
+        }
+        (void)slot;
+        const uint64_t b2 = __shfl(gbase, (int)src);
+        const uint64_t l2 = __shfl(glen, (int)src);
+        const uint32_t r2 = __shfl(grow, (int)src);
+        const uint32_t m2 = __shfl(mult, (int)src);
+        gbase = lane < ng ? b2 : 0;
+        glen = lane < ng ? l2 : 0;
+        grow = lane < ng ? r2 : 0;
+        mult = lane < ng ? m2 : 0;
+    }
+    const uint64_t p_total = wave_sum(glen);
+    // score of `count` hits held by lane `count`: (float)count / n (nGramSearch.hpp:300)
+    const float sc_lane = lane <= n ? (float)lane / (float)n : 0.0f;
+    const unsigned long long pm = __ballot(lane <= n && lane > 0 && !(sc_lane < P.thr));
+    const uint32_t cmin = pm ? (uint32_t)(__ffsll((long long)pm) - 1) : 1000u;
+    const uint32_t K = X.n_buckets, span = X.bucket_span;
+    if (p_total && cmin <= n) {
+        if (p_total <= (uint64_t)kWaveCap && n_long <= kMaxPartSpan) {
+            wave_part(S, X, P, m, L, 0, ng, gbase, (uint32_t)glen, mult, cmin, sc_lane, surv_n, cand_n, tau, err);
+        } else {
+            const uint32_t wmax = (uint32_t)max64(1, min64(K, kMaxPartSpan / max(span, 1u)));
+            uint32_t w = (uint32_t)max64(1, min64(wmax, (uint64_t)K * (kWaveCap * 3 / 4) / p_total));
+            uint32_t cur = 0;  // lane g: offset of the part's first posting within its list
+            const uint32_t* sk = X.skip + (size_t)grow * (K + 1);
+            uint32_t blo = 0;
+            for (uint32_t guard = 0; blo < K; ++guard) {
+                if (guard > 4 * K + 64) {
+                    if (lane == 0) atomicOr(err, 4u);
+                    break;
+                }
+                const uint32_t bhi = min(K, blo + w);
+                const uint32_t s1 = lane < ng ? sk[bhi] : 0u;
+                const uint32_t tot = wave_sum(s1 - cur);
+                if (tot > (uint32_t)kWaveCap && bhi - blo > 1) {
+                    w = max(1u, (uint32_t)((uint64_t)(bhi - blo) * (kWaveCap * 3 / 4) / tot));
+                    continue;
+                }
+                if (tot > (uint32_t)kWaveCap || span > kMaxPartSpan) {
+                    // a single bucket above the cap: term-id sub-parts by lower_bound per lane (rare)
+                    const uint32_t hi_lim = (uint32_t)min64((uint64_t)bhi * span, n_long);
+                    uint32_t sub_lo = blo * span;
+                    uint32_t step = (uint32_t)max64(1, min64((uint64_t)(hi_lim - sub_lo) * (kWaveCap * 3 / 4) /
+                                                                 max(tot, 1u), kMaxPartSpan));
+                    for (uint32_t g2 = 0; sub_lo < hi_lim; ++g2) {
+                        if (g2 > 4u * (hi_lim - blo * span) + 64u) {
+                            if (lane == 0) atomicOr(err, 4u);
+                            break;
+                        }
+                        const uint32_t hi = (uint32_t)min64(hi_lim, (uint64_t)sub_lo + step);
+                        uint32_t a = cur, b = s1;
+                        if (lane < ng) {
+                            while (a < b) {
+                                const uint32_t mid = (a + b) >> 1;
+                                if (X.post[gbase + mid] < hi) a = mid + 1; else b = mid;
+                            }
+                        }
+                        const uint32_t t2 = wave_sum(lane < ng ? a - cur : 0u);
+                        if (t2 > (uint32_t)kWaveCap && hi - sub_lo > 1) {
+                            step = max(1u, (uint32_t)((uint64_t)(hi - sub_lo) * (kWaveCap * 3 / 4) / t2));
+                            continue;
+                        }
+                        wave_part(S, X, P, m, L, sub_lo, ng, gbase + cur, a - cur, mult, cmin, sc_lane, surv_n,
+                                  cand_n, tau, err);
+                        cur = a;
+                        sub_lo = hi;
+                    }
+                } else if (tot) {
+                    wave_part(S, X, P, m, L, blo * span, ng, gbase + cur, s1 - cur, mult, cmin, sc_lane, surv_n,
+                              cand_n, tau, err);
+                }
+                cur = s1;
+                blo = bhi;
+                if (tot < (uint32_t)kWaveCap / 3) w = min(wmax, w * 2);
+            }
+        }
+    }
+    if (surv_n) wave_emit(S, X, P, m, L, surv_n, cand_n, tau);
+    wave_flush(S, cand_n, tau, L);
+    for (uint32_t i = lane; i < cand_n; i += 64) {
+        const uint64_t r = S.cand[i];
+        const uint32_t enc = ~(uint32_t)(r >> 32);
+        out_k[ob + i] = (uint32_t)r;
+        out_s[ob + i] = enc == kPromoted ? 100.0f : __uint_as_float(enc - 1u);
+    }
+    if (lane == 0) {
+        out_n[q] = cand_n;
+        atomicAdd(&stats->postings, (unsigned long long)p_total);
+        atomicAdd(&stats->lists, (unsigned long long)ng);
+        atomicAdd(&stats->results, (unsigned long long)cand_n);
+        atomicAdd(&stats->fast, 1ull);
+        atomicAdd(&stats->survivors, (unsigned long long)S.surv_total);
     }
 }
 
@@ -693,6 +1127,22 @@ hipError_t build_wildcard(const float* d_w, uint32_t n_keys, uint32_t* d_keys, f
     return e;
 }
 
+int phase_stats(unsigned long long* out, int n, bool reset) {
+#ifdef NGS_PHASE_STAMPS
+    unsigned long long h[16];
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_phase), sizeof(h)) != hipSuccess) return -1;
+    for (int i = 0; i < n && i < 16; ++i) out[i] = h[i];
+    if (reset) {
+        unsigned long long z[16] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 16;
+#else
+    (void)out; (void)n; (void)reset;
+    return -1;
+#endif
+}
+
 hipError_t launch_prep(const uint8_t* raw, const uint64_t* off, uint32_t B, const SearchParams& P, uint8_t* qnorm,
                        uint32_t* qm, hipStream_t s) {
     if (!B) return hipSuccess;
@@ -701,11 +1151,14 @@ hipError_t launch_prep(const uint8_t* raw, const uint64_t* off, uint32_t B, cons
 }
 
 hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* qnorm, const uint64_t* off,
-                       const uint32_t* qm, uint32_t* out_n, uint32_t* out_k, float* out_s, uint32_t* glist,
-                       uint32_t* gcount, DevStats* stats, hipStream_t s) {
+                       const uint32_t* qm, uint32_t* out_n, uint32_t* out_k, float* out_s, uint32_t* list2,
+                       uint32_t* count2, uint32_t* glist, uint32_t* gcount, DevStats* stats, hipStream_t s) {
     if (!P.n_queries) return hipSuccess;
-    hipLaunchKernelGGL(k_fast, dim3(P.n_queries), dim3(kFastThreads), 0, s, X, P, qnorm, off, qm, out_n, out_k,
-                       out_s, glist, gcount, stats);
+    hipLaunchKernelGGL(k_wave, dim3(P.n_queries), dim3(64), 0, s, X, P, qnorm, off, qm, out_n, out_k, out_s, list2,
+                       count2, stats);
+    const uint32_t grid2 = std::min<uint32_t>(P.n_queries, 1024);
+    hipLaunchKernelGGL(k_fast, dim3(grid2), dim3(kFastThreads), 0, s, X, P, qnorm, off, qm, out_n, out_k, out_s,
+                       (const uint32_t*)list2, (const uint32_t*)count2, glist, gcount, stats);
     return hipGetLastError();
 }
 
