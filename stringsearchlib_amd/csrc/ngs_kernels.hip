@@ -616,6 +616,9 @@ struct WaveSmem {
     uint64_t seg_start[64];      // current part: first posting of each gram's segment
     uint32_t seg_pre[68];        // exclusive prefix of segment lengths
     uint32_t seg_mult[64];
+    uint64_t pseg_start[2][64];  // pipelined parts: double-buffered segment descriptors
+    uint32_t pseg_pre[2][68];
+    uint32_t pseg_mult[2][64];
     uint8_t q[kWaveMaxGrams + 8];
     uint32_t surv_total;         // stats: survivors of this query
 };
@@ -798,6 +801,81 @@ __device__ void wave_part(WaveSmem& S, const DevIndex& X, const SearchParams& P,
     __syncthreads();
 }
 
+// ---- software-pipelined parts (tier 1) ----
+// A part's postings are loaded lane-strided into 16 registers per lane (kWaveCap = 16 * 64)
+// one part AHEAD of the part being counted, so each wave keeps ~1k posting loads in flight
+// while it works on the table. Segment descriptors are double-buffered in LDS.
+static_assert(kWaveCap == 16 * 64, "one register per lane per 64 postings");
+
+// Publishes the part's segments (lane g < ng: [start, start + len)) into LDS buffer `buf` and
+// issues every posting load of the part; returns the part's posting count.
+__device__ __forceinline__ uint32_t part_issue(WaveSmem& S, int buf, const DevIndex& X, uint32_t ng,
+                                               uint64_t start, uint32_t len, uint32_t mult, uint32_t (&t)[16]) {
+    const uint32_t lane = lane_id();
+    uint32_t incl = lane < ng ? len : 0u;
+    const uint32_t mine = incl;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o);
+        if ((int)lane >= o) incl += y;
+    }
+    const uint32_t total = __shfl(incl, 63);
+    if (lane < ng) {
+        S.pseg_start[buf][lane] = start;
+        S.pseg_pre[buf][lane] = incl - mine;
+        S.pseg_mult[buf][lane] = mult;
+    }
+    if (lane == 0) S.pseg_pre[buf][ng] = total;
+    __syncthreads();
+    uint32_t g = 0;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+        const uint32_t j = lane + u * 64;
+        t[u] = 0;
+        if (j < total) {
+            while (S.pseg_pre[buf][g + 1] <= j) ++g;
+            t[u] = X.post[S.pseg_start[buf][g] + (j - S.pseg_pre[buf][g])];
+        }
+    }
+    return total;
+}
+
+// Counts the part held in registers into the table, then scans it (as wave_part).
+__device__ __forceinline__ void part_consume(WaveSmem& S, int buf, const DevIndex& X, const SearchParams& P,
+                                             uint32_t m, uint32_t L, uint32_t lo, uint32_t total,
+                                             const uint32_t (&t)[16], uint32_t cmin, float sc_lane,
+                                             uint32_t& surv_n, uint32_t& cand_n, uint64_t& tau, unsigned* err) {
+    const uint32_t lane = lane_id();
+    uint32_t g = 0;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+        const uint32_t j = lane + u * 64;
+        if (j < total) {
+            while (S.pseg_pre[buf][g + 1] <= j) ++g;
+            wave_insert(S.table, t[u] - lo + 1u, S.pseg_mult[buf][g], err);
+        }
+    }
+    __syncthreads();
+    uint4* T4 = reinterpret_cast<uint4*>(S.table);
+    for (uint32_t i = lane; i < (uint32_t)kWaveSlots / 4; i += 64) {
+        if (surv_n + 256 > (uint32_t)kWaveSurv) wave_emit(S, X, P, m, L, surv_n, cand_n, tau);
+        const uint4 v = T4[i];
+        T4[i] = make_uint4(0, 0, 0, 0);
+        const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const uint32_t cnt = vv[c] & 255u;
+            const float s = __shfl(sc_lane, (int)cnt);
+            const bool pass = vv[c] != 0 && cnt >= cmin;
+            const unsigned long long b = __ballot(pass);
+            if (pass)
+                S.surv[surv_n + __popcll(b & lanes_below())] =
+                    make_uint2(X.n_short + lo + (vv[c] >> 8) - 1u, __float_as_uint(s));
+            surv_n += __popcll(b);
+        }
+    }
+    __syncthreads();
+}
+
 __global__ __launch_bounds__(64) void k_wave(DevIndex X, SearchParams P, const uint8_t* __restrict__ qnorm,
                                              const uint64_t* __restrict__ qoff, const uint32_t* __restrict__ qm,
                                              uint32_t* __restrict__ out_n, uint32_t* __restrict__ out_k,
@@ -920,59 +998,76 @@ __global__ __launch_bounds__(64) void k_wave(DevIndex X, SearchParams P, const u
         if (p_total <= (uint64_t)kWaveCap && n_long <= kMaxPartSpan) {
             wave_part(S, X, P, m, L, 0, ng, gbase, (uint32_t)glen, mult, cmin, sc_lane, surv_n, cand_n, tau, err);
         } else {
+            // fixed part width w (buckets) from the average density; part p = buckets
+            // [p*w, (p+1)*w). e0/e1/e2: per-lane list offsets of the ends of parts p, p+1, p+2.
             const uint32_t wmax = (uint32_t)max64(1, min64(K, kMaxPartSpan / max(span, 1u)));
-            uint32_t w = (uint32_t)max64(1, min64(wmax, (uint64_t)K * (kWaveCap * 3 / 4) / p_total));
-            uint32_t cur = 0;  // lane g: offset of the part's first posting within its list
+            const uint32_t w = (uint32_t)max64(1, min64(wmax, (uint64_t)K * (kWaveCap * 5 / 8) / p_total));
+            const uint32_t np = (K + w - 1) / w;
             const uint32_t* sk = X.skip + (size_t)grow * (K + 1);
-            uint32_t blo = 0;
-            for (uint32_t guard = 0; blo < K; ++guard) {
-                if (guard > 4 * K + 64) {
-                    if (lane == 0) atomicOr(err, 4u);
-                    break;
+            auto bound = [&](uint32_t p) -> uint32_t { return lane < ng ? sk[min(K, (p + 1) * w)] : 0u; };
+            uint32_t cur = 0, e0 = bound(0), e1 = np > 1 ? bound(1) : 0u;
+            uint32_t tNext[16];
+            uint32_t totNext = 0;
+            bool fastNext = false;
+            // part 0: segments + posting loads in flight
+            {
+                const uint32_t tot = wave_sum(e0 - cur);
+                fastNext = tot <= (uint32_t)kWaveCap && span * min(w, K) <= kMaxPartSpan;
+                if (fastNext && tot) totNext = part_issue(S, 0, X, ng, gbase + cur, e0 - cur, mult, tNext);
+            }
+            for (uint32_t p = 0; p < np; ++p) {
+                const int buf = p & 1;
+                uint32_t tCur[16];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) tCur[u] = tNext[u];  // waits for part p's loads only
+                const uint32_t totCur = totNext;
+                const bool fastCur = fastNext;
+                const uint32_t e2 = p + 2 < np ? bound(p + 2) : 0u;
+                // prefetch part p+1 while part p is counted
+                totNext = 0;
+                fastNext = false;
+                if (p + 1 < np) {
+                    const uint32_t tot = wave_sum(e1 - e0);
+                    fastNext = tot <= (uint32_t)kWaveCap && span * min(w, K) <= kMaxPartSpan;
+                    if (fastNext && tot) totNext = part_issue(S, buf ^ 1, X, ng, gbase + e0, e1 - e0, mult, tNext);
                 }
-                const uint32_t bhi = min(K, blo + w);
-                const uint32_t s1 = lane < ng ? sk[bhi] : 0u;
-                const uint32_t tot = wave_sum(s1 - cur);
-                if (tot > (uint32_t)kWaveCap && bhi - blo > 1) {
-                    w = max(1u, (uint32_t)((uint64_t)(bhi - blo) * (kWaveCap * 3 / 4) / tot));
-                    continue;
-                }
-                if (tot > (uint32_t)kWaveCap || span > kMaxPartSpan) {
-                    // a single bucket above the cap: term-id sub-parts by lower_bound per lane (rare)
-                    const uint32_t hi_lim = (uint32_t)min64((uint64_t)bhi * span, n_long);
-                    uint32_t sub_lo = blo * span;
-                    uint32_t step = (uint32_t)max64(1, min64((uint64_t)(hi_lim - sub_lo) * (kWaveCap * 3 / 4) /
-                                                                 max(tot, 1u), kMaxPartSpan));
+                if (fastCur) {
+                    if (totCur) part_consume(S, buf, X, P, m, L, p * w * span, totCur, tCur, cmin, sc_lane, surv_n,
+                                             cand_n, tau, err);
+                } else {
+                    // a part above the cap: term-id sub-parts by lower_bound per lane (rare)
+                    const uint32_t lo_lim = p * w * span;
+                    const uint32_t hi_lim = (uint32_t)min64((uint64_t)min(K, (p + 1) * w) * span, n_long);
+                    uint32_t sub_lo = lo_lim, cc = cur;
+                    uint32_t step = (uint32_t)max64(1, min64((uint64_t)(hi_lim - lo_lim) * (kWaveCap * 3 / 4) /
+                                                                 max(wave_sum(e0 - cur), 1u), kMaxPartSpan));
                     for (uint32_t g2 = 0; sub_lo < hi_lim; ++g2) {
-                        if (g2 > 4u * (hi_lim - blo * span) + 64u) {
+                        if (g2 > 4u * (hi_lim - lo_lim) + 64u) {
                             if (lane == 0) atomicOr(err, 4u);
                             break;
                         }
                         const uint32_t hi = (uint32_t)min64(hi_lim, (uint64_t)sub_lo + step);
-                        uint32_t a = cur, b = s1;
+                        uint32_t a2 = cc, b2 = e0;
                         if (lane < ng) {
-                            while (a < b) {
-                                const uint32_t mid = (a + b) >> 1;
-                                if (X.post[gbase + mid] < hi) a = mid + 1; else b = mid;
+                            while (a2 < b2) {
+                                const uint32_t mid = (a2 + b2) >> 1;
+                                if (X.post[gbase + mid] < hi) a2 = mid + 1; else b2 = mid;
                             }
                         }
-                        const uint32_t t2 = wave_sum(lane < ng ? a - cur : 0u);
+                        const uint32_t t2 = wave_sum(lane < ng ? a2 - cc : 0u);
                         if (t2 > (uint32_t)kWaveCap && hi - sub_lo > 1) {
                             step = max(1u, (uint32_t)((uint64_t)(hi - sub_lo) * (kWaveCap * 3 / 4) / t2));
                             continue;
                         }
-                        wave_part(S, X, P, m, L, sub_lo, ng, gbase + cur, a - cur, mult, cmin, sc_lane, surv_n,
+                        wave_part(S, X, P, m, L, sub_lo, ng, gbase + cc, a2 - cc, mult, cmin, sc_lane, surv_n,
                                   cand_n, tau, err);
-                        cur = a;
+                        cc = a2;
                         sub_lo = hi;
                     }
-                } else if (tot) {
-                    wave_part(S, X, P, m, L, blo * span, ng, gbase + cur, s1 - cur, mult, cmin, sc_lane, surv_n,
-                              cand_n, tau, err);
                 }
-                cur = s1;
-                blo = bhi;
-                if (tot < (uint32_t)kWaveCap / 3) w = min(wmax, w * 2);
+                cur = e0;
+                e0 = e1;
+                e1 = e2;
             }
         }
     }
