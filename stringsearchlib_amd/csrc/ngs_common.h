@@ -52,8 +52,8 @@ constexpr int kWaveSlots = 1 << kWaveSlotBits;  // wave-private LDS hash table
 constexpr int kWaveCap = kWaveSlots / 2;        // postings per part (<= 50 % load)
 constexpr int kWaveCand = 256;                  // candidate buffer per query
 constexpr uint32_t kWaveMaxLimit = kWaveCand / 2;
-constexpr int kWaveSurv = 512;                  // survivor list (term, score) before calcScore
-constexpr uint32_t kWaveMaxGrams = 64;
+constexpr int kWaveSurv = kWaveCap + 256;       // survivor list (term, count) before calcScore
+constexpr uint32_t kWaveMaxGrams = 63;          // counts <= 63: one lane per count value
 
 struct DevIndex {  // passed by value to kernels; all pointers are device pointers
     const uint64_t* gram_off;   // [kGramSpace + 1] -> post

@@ -606,21 +606,22 @@ __global__ __launch_bounds__(kFastThreads) void k_fast(DevIndex X, SearchParams 
 }
 
 // ---------------------------------------------------------------- wave kernel --------
-// Tier 1: ONE WAVE PER QUERY with a wave-private LDS table. No block barriers, ~11 queries
-// in flight per CU; the only dependent global round trips per query are the gram lists'
-// offsets, one posting sweep per term-id part and one batched calcScore for the survivors.
+// Tier 1: ONE WAVE PER QUERY, wave-private LDS (no block barriers; ~8 queries in flight per
+// CU). A query's lists are cut into term-id parts of <= kWaveCap postings (bucket skip table;
+// oversized buckets are split by lower_bound); part p+1's postings are loaded into registers
+// while part p is counted. Terms reaching cmin go to a survivor list that calcScore consumes
+// in batches; the running top-L lives in the wave's candidate buffer.
 struct WaveSmem {
-    uint32_t table[kWaveSlots];  // (term - lo + 1) << 8 | count
-    uint64_t cand[kWaveCand];    // (~enc) << 32 | key
-    uint2 surv[kWaveSurv];       // (term, score bits) that passed the threshold
-    uint64_t seg_start[64];      // current part: first posting of each gram's segment
-    uint32_t seg_pre[68];        // exclusive prefix of segment lengths
-    uint32_t seg_mult[64];
-    uint64_t pseg_start[2][64];  // pipelined parts: double-buffered segment descriptors
-    uint32_t pseg_pre[2][68];
-    uint32_t pseg_mult[2][64];
+    uint32_t table[kWaveSlots];    // exact: (term - lo + 1) << 8 | count; sketch: 2 x u16 counters
+    uint64_t cand[kWaveCand];      // (~enc) << 32 | key
+    uint32_t surv_t[kWaveSurv];    // survivor terms
+    uint8_t surv_c[kWaveSurv];     // hit count, | 0x80 for a Levenshtein (short search) match count
+    uint64_t pseg_start[2][64];    // part segments, double-buffered: first posting of each gram
+    uint32_t pseg_pre[2][68];      //   exclusive prefix of the segment lengths
+    uint32_t pseg_mult[2][64];     //   multiplicity of the gram in the query
+    uint2 cbuf[64];                // sketch candidates (term, mult)
     uint8_t q[kWaveMaxGrams + 8];
-    uint32_t surv_total;         // stats: survivors of this query
+    uint32_t surv_total;           // stats
 };
 
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
@@ -639,7 +640,7 @@ __device__ void wave_flush(WaveSmem& S, uint32_t& cand_n, uint64_t& tau, uint32_
     const uint32_t P2 = next_pow2(max(n, 2u));
     for (uint32_t i = lane; i < P2; i += 64) {
         const uint64_t r = i < n ? S.cand[i] : kNoCand;
-        S.cand[i] = i < n ? ((r << 32) | (r >> 32)) : kNoCand;
+        S.cand[i] = i < n ? ((r << 32) | (r >> 32)) : kNoCand;  // key-major for the dedup
     }
     __syncthreads();
     for (int pass = 0; pass < 2; ++pass) {
@@ -680,23 +681,24 @@ __device__ void wave_flush(WaveSmem& S, uint32_t& cand_n, uint64_t& tau, uint32_
     __syncthreads();
 }
 
-// calcScore (nGramSearch.hpp:310-341) for the survivor list: term -> (key, weight) pairs,
-// max(w*s, 0), exact-match promotion, appended to the candidate buffer.
+// calcScore (nGramSearch.hpp:310-341) over the survivor list: term -> (key, weight) pairs,
+// max(w*s, 0), exact-match promotion, into the running top-L.
 __device__ void wave_emit(WaveSmem& S, const DevIndex& X, const SearchParams& P, uint32_t m, uint32_t L,
-                          uint32_t& surv_n, uint32_t& cand_n, uint64_t& tau) {
+                          float sc_long, float sc_short, uint32_t& surv_n, uint32_t& cand_n, uint64_t& tau) {
     const uint32_t lane = lane_id();
     S.surv_total += surv_n;
     __syncthreads();
     for (uint32_t base = 0; base < surv_n; base += 64) {
         const uint32_t i = base + lane;
-        uint32_t p = 0, pe = 0;
-        float s = 0.0f;
+        uint32_t p = 0, pe = 0, code = 0;
         if (i < surv_n) {
-            const uint2 e = S.surv[i];
-            p = X.tk_off[e.x];
-            pe = X.tk_off[e.x + 1];
-            s = __uint_as_float(e.y);
+            const uint32_t t = S.surv_t[i];
+            code = S.surv_c[i];
+            p = X.tk_off[t];
+            pe = X.tk_off[t + 1];
         }
+        const float s_l = __shfl(sc_long, (int)(code & 63u)), s_s = __shfl(sc_short, (int)(code & 63u));
+        const float s = (code & 0x80u) ? s_s : s_l;
         const bool promo = (double)s > 0.999;  // nGramSearch.hpp:328
         while (__ballot(p < pe)) {
             uint64_t rec = kNoCand;
@@ -716,99 +718,20 @@ __device__ void wave_emit(WaveSmem& S, const DevIndex& X, const SearchParams& P,
     __syncthreads();
 }
 
-__device__ __forceinline__ void wave_insert(uint32_t* T, uint32_t rel, uint32_t mult, unsigned* err) {
-    uint32_t probes = 0;
-    uint32_t h = (rel * 0x9E3779B1u) >> (32 - kWaveSlotBits);
-    const uint32_t want = rel << 8;
-    for (;;) {
-        uint32_t cur = T[h];
-        if (cur == 0) {
-            const uint32_t prev = atomicCAS(&T[h], 0u, want | mult);
-            if (prev == 0) return;
-            cur = prev;
-        }
-        if ((cur >> 8) == rel) {
-            atomicAdd(&T[h], mult);
-            return;
-        }
-        h = (h + 1) & (kWaveSlots - 1);
-        if (++probes > (uint32_t)kWaveSlots) {
-            atomicOr(err, 1u);
-            return;
-        }
+__device__ __forceinline__ void surv_append(WaveSmem& S, bool pass, uint32_t t, uint32_t code, uint32_t& surv_n) {
+    const unsigned long long b = __ballot(pass);
+    if (pass) {
+        const uint32_t i = surv_n + __popcll(b & lanes_below());
+        S.surv_t[i] = t;
+        S.surv_c[i] = (uint8_t)code;
     }
+    surv_n += __popcll(b);
 }
 
-// One term-id part: lane g < ng owns gram g's segment [base+cur, base+cur+len) of terms in
-// [lo, lo + 2^24). Counts it in the wave's table, then scans the table: count >= cmin ->
-// survivor (score = sc_lane(count), the precomputed (float)count / n).
-__device__ void wave_part(WaveSmem& S, const DevIndex& X, const SearchParams& P, uint32_t m, uint32_t L,
-                          uint32_t lo, uint32_t ng, uint64_t seg_start, uint32_t seg_len, uint32_t mult,
-                          uint32_t cmin, float sc_lane, uint32_t& surv_n, uint32_t& cand_n, uint64_t& tau,
-                          unsigned* err) {
-    const uint32_t lane = lane_id();
-    uint32_t incl = lane < ng ? seg_len : 0u;
-    const uint32_t mine = incl;
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(incl, o);
-        if ((int)lane >= o) incl += y;
-    }
-    const uint32_t total = __shfl(incl, 63);
-    if (lane < ng) {
-        S.seg_start[lane] = seg_start;
-        S.seg_pre[lane] = incl - mine;
-        S.seg_mult[lane] = mult;
-    }
-    if (lane == 0) S.seg_pre[ng] = total;
-    __syncthreads();
-    uint32_t g = 0;
-    for (uint32_t j0 = lane; j0 < total; j0 += 8 * 64) {
-        uint32_t tt[8], mu[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const uint32_t j = j0 + u * 64;
-            mu[u] = 0;
-            if (j < total) {
-                while (S.seg_pre[g + 1] <= j) ++g;
-                tt[u] = X.post[S.seg_start[g] + (j - S.seg_pre[g])];
-                mu[u] = S.seg_mult[g];
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-            if (mu[u]) wave_insert(S.table, tt[u] - lo + 1u, mu[u], err);
-    }
-    __syncthreads();
-    // scan + clear, 4 slots per lane per step
-    uint4* T4 = reinterpret_cast<uint4*>(S.table);
-    for (uint32_t i = lane; i < (uint32_t)kWaveSlots / 4; i += 64) {
-        if (surv_n + 256 > (uint32_t)kWaveSurv) wave_emit(S, X, P, m, L, surv_n, cand_n, tau);
-        const uint4 v = T4[i];
-        T4[i] = make_uint4(0, 0, 0, 0);
-        const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const uint32_t cnt = vv[c] & 255u;
-            const float s = __shfl(sc_lane, (int)cnt);  // (float)count / n, nGramSearch.hpp:300
-            const bool pass = vv[c] != 0 && cnt >= cmin; // !(s < thr), nGramSearch.hpp:315
-            const unsigned long long b = __ballot(pass);
-            if (pass)
-                S.surv[surv_n + __popcll(b & lanes_below())] =
-                    make_uint2(X.n_short + lo + (vv[c] >> 8) - 1u, __float_as_uint(s));
-            surv_n += __popcll(b);
-        }
-    }
-    __syncthreads();
-}
-
-// ---- software-pipelined parts (tier 1) ----
-// A part's postings are loaded lane-strided into 16 registers per lane (kWaveCap = 16 * 64)
-// one part AHEAD of the part being counted, so each wave keeps ~1k posting loads in flight
-// while it works on the table. Segment descriptors are double-buffered in LDS.
-static_assert(kWaveCap == 16 * 64, "one register per lane per 64 postings");
+static_assert(kWaveCap == 16 * 64, "a part is one register per lane per 64 postings");
 
 // Publishes the part's segments (lane g < ng: [start, start + len)) into LDS buffer `buf` and
-// issues every posting load of the part; returns the part's posting count.
+// issues every posting load of the part into t[]; returns the part's posting count.
 __device__ __forceinline__ uint32_t part_issue(WaveSmem& S, int buf, const DevIndex& X, uint32_t ng,
                                                uint64_t start, uint32_t len, uint32_t mult, uint32_t (&t)[16]) {
     const uint32_t lane = lane_id();
@@ -826,54 +749,141 @@ __device__ __forceinline__ uint32_t part_issue(WaveSmem& S, int buf, const DevIn
     }
     if (lane == 0) S.pseg_pre[buf][ng] = total;
     __syncthreads();
-    uint32_t g = 0;
+    uint32_t g = 0, nxt = S.pseg_pre[buf][1];
+    uint64_t base = S.pseg_start[buf][0];
 #pragma unroll
     for (int u = 0; u < 16; ++u) {
         const uint32_t j = lane + u * 64;
         t[u] = 0;
         if (j < total) {
-            while (S.pseg_pre[buf][g + 1] <= j) ++g;
-            t[u] = X.post[S.pseg_start[buf][g] + (j - S.pseg_pre[buf][g])];
+            while (j >= nxt) {
+                ++g;
+                nxt = S.pseg_pre[buf][g + 1];
+                base = S.pseg_start[buf][g] - S.pseg_pre[buf][g];
+            }
+            t[u] = X.post[base + j];
         }
     }
     return total;
 }
 
-// Counts the part held in registers into the table, then scans it (as wave_part).
-__device__ __forceinline__ void part_consume(WaveSmem& S, int buf, const DevIndex& X, const SearchParams& P,
-                                             uint32_t m, uint32_t L, uint32_t lo, uint32_t total,
-                                             const uint32_t (&t)[16], uint32_t cmin, float sc_lane,
-                                             uint32_t& surv_n, uint32_t& cand_n, uint64_t& tau, unsigned* err) {
-    const uint32_t lane = lane_id();
+__device__ __forceinline__ uint32_t part_mult(WaveSmem& S, int buf, uint32_t j) {
     uint32_t g = 0;
+    while (S.pseg_pre[buf][g + 1] <= j) ++g;
+    return S.pseg_mult[buf][g];
+}
+
+__device__ __forceinline__ uint32_t wave_insert_slot(uint32_t* T, uint32_t rel, uint32_t mult, unsigned* err) {
+    uint32_t probes = 0;
+    uint32_t h = (rel * 0x9E3779B1u) >> (32 - kWaveSlotBits);
+    const uint32_t want = rel << 8;
+    for (;;) {
+        uint32_t cur = T[h];
+        if (cur == 0) {
+            const uint32_t prev = atomicCAS(&T[h], 0u, want | mult);
+            if (prev == 0) return h;
+            cur = prev;
+        }
+        if ((cur >> 8) == rel) {
+            atomicAdd(&T[h], mult);
+            return h;
+        }
+        h = (h + 1) & (kWaveSlots - 1);
+        if (++probes > (uint32_t)kWaveSlots) {
+            atomicOr(err, 1u);
+            return h;
+        }
+    }
+}
+
+__device__ __forceinline__ uint32_t sketch_cell(uint32_t t) { return (t * 0x9E3779B1u) >> (32 - kWaveSlotBits - 1); }
+
+// Exact count of a part: LDS hash table; each posting keeps its slot, and the extraction
+// exchanges the slot with 0 so the first holder of a term owns its count (no table scan).
+__device__ __forceinline__ void part_exact(WaveSmem& S, int buf, uint32_t lo, uint32_t total, bool uni_mult,
+                                           const uint32_t (&t)[16], uint32_t cmin, uint32_t n_short,
+                                           uint32_t& surv_n, unsigned* err) {
+    const uint32_t lane = lane_id();
+    uint32_t sl[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+        const uint32_t j = lane + u * 64;
+        sl[u] = 0;
+        if (j < total) sl[u] = wave_insert_slot(S.table, t[u] - lo + 1u, uni_mult ? 1u : part_mult(S, buf, j), err);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+        const uint32_t j = lane + u * 64;
+        const uint32_t v = j < total ? atomicExch(&S.table[sl[u]], 0u) : 0u;
+        const uint32_t cnt = v & 255u;  // s = cnt / n; s >= thr <=> cnt >= cmin (nGramSearch.hpp:300,315)
+        surv_append(S, v != 0 && cnt >= cmin, n_short + lo + (v >> 8) - 1u, cnt, surv_n);
+    }
+    __syncthreads();
+}
+
+// Sketch count of a part (cmin >= 3): 2 x u16 counters per table word (never undercounts);
+// returns false when more than 64 postings can reach cmin (the caller then counts exactly).
+__device__ __forceinline__ bool part_sketch(WaveSmem& S, int buf, uint32_t total, bool uni_mult,
+                                            const uint32_t (&t)[16], uint32_t cmin, uint32_t n_short,
+                                            uint32_t& surv_n) {
+    const uint32_t lane = lane_id();
 #pragma unroll
     for (int u = 0; u < 16; ++u) {
         const uint32_t j = lane + u * 64;
         if (j < total) {
-            while (S.pseg_pre[buf][g + 1] <= j) ++g;
-            wave_insert(S.table, t[u] - lo + 1u, S.pseg_mult[buf][g], err);
+            const uint32_t c = sketch_cell(t[u]);
+            atomicAdd(&S.table[c >> 1], (uni_mult ? 1u : part_mult(S, buf, j)) << ((c & 1u) << 4));
         }
     }
     __syncthreads();
-    uint4* T4 = reinterpret_cast<uint4*>(S.table);
-    for (uint32_t i = lane; i < (uint32_t)kWaveSlots / 4; i += 64) {
-        if (surv_n + 256 > (uint32_t)kWaveSurv) wave_emit(S, X, P, m, L, surv_n, cand_n, tau);
-        const uint4 v = T4[i];
-        T4[i] = make_uint4(0, 0, 0, 0);
-        const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+    uint32_t nc = 0;
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const uint32_t cnt = vv[c] & 255u;
-            const float s = __shfl(sc_lane, (int)cnt);
-            const bool pass = vv[c] != 0 && cnt >= cmin;
-            const unsigned long long b = __ballot(pass);
-            if (pass)
-                S.surv[surv_n + __popcll(b & lanes_below())] =
-                    make_uint2(X.n_short + lo + (vv[c] >> 8) - 1u, __float_as_uint(s));
-            surv_n += __popcll(b);
+    for (int u = 0; u < 16; ++u) {
+        const uint32_t j = lane + u * 64;
+        bool pass = false;
+        if (j < total) {
+            const uint32_t c = sketch_cell(t[u]);
+            pass = ((S.table[c >> 1] >> ((c & 1u) << 4)) & 0xFFFFu) >= cmin;
         }
+        const unsigned long long b = __ballot(pass);
+        const uint32_t idx = nc + __popcll(b & lanes_below());
+        if (pass && idx < 64) S.cbuf[idx] = make_uint2(t[u], uni_mult ? 1u : part_mult(S, buf, j));
+        nc += __popcll(b);
     }
     __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+        const uint32_t j = lane + u * 64;
+        if (j < total) S.table[sketch_cell(t[u]) >> 1] = 0;
+    }
+    __syncthreads();
+    if (nc > 64) return false;
+    if (nc == 0) return true;
+    // exact counts of the <= 64 candidate postings: bitonic sort of (term, mult) across lanes
+    uint32_t key = lane < nc ? S.cbuf[lane].x : 0xFFFFFFFFu;
+    uint32_t val = lane < nc ? S.cbuf[lane].y : 0u;
+    for (uint32_t k = 2; k <= 64; k <<= 1) {
+        for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
+            const uint32_t ok = __shfl_xor(key, (int)jj), ov = __shfl_xor(val, (int)jj);
+            const bool up = (lane & k) == 0, lower = (lane & jj) == 0;
+            if (lower == up ? ok < key : ok > key) {
+                key = ok;
+                val = ov;
+            }
+        }
+    }
+    const uint32_t prevk = __shfl_up(key, 1);
+    const bool head = key != 0xFFFFFFFFu && (lane == 0 || prevk != key);
+    uint32_t acc = val;
+    for (uint32_t d = 1; d < 64; ++d) {
+        const uint32_t nk = __shfl_down(key, (int)d), nv = __shfl_down(val, (int)d);
+        const bool more = lane + d < 64 && nk == key;
+        if (!__ballot(more)) break;
+        if (more) acc += nv;
+    }
+    surv_append(S, head && acc >= cmin, n_short + key, acc, surv_n);
+    return true;
 }
 
 __global__ __launch_bounds__(64) void k_wave(DevIndex X, SearchParams P, const uint8_t* __restrict__ qnorm,
@@ -916,34 +926,32 @@ __global__ __launch_bounds__(64) void k_wave(DevIndex X, SearchParams P, const u
     uint32_t cand_n = 0, surv_n = 0;
     uint64_t tau = kNoCand;
     unsigned* err = &stats->errors;
+    // lane c holds the fp32 score of c hits: (float)c / n (hpp:300) and (float)c / m (hpp:244)
+    const float sc_long = lane <= n ? (float)lane / (float)n : 0.0f;
+    const float sc_short = lane <= m ? (float)lane / (float)m : 0.0f;
 
     // ---- searchShort over shortLib (nGramSearch.hpp:262-270), 4 <= m < 9 ----
     if (m < kShortQueryLen && X.n_short) {
         uint8_t qc[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) qc[i] = (uint32_t)i < m ? S.q[i] : 0;
-        const float s_lane = lane <= m ? (float)lane / (float)m : 0.0f;  // nGramSearch.hpp:244
-        const bool ok_lane = lane <= m && !(s_lane < P.thr);
-        const unsigned long long okm = __ballot(ok_lane);
+        const unsigned long long okm = __ballot(lane <= m && !(sc_short < P.thr));  // hpp:315
         const uint32_t cmin_s = okm ? (uint32_t)(__ffsll((long long)okm) - 1) : 64u;
         for (uint32_t t0 = 0; t0 < X.n_short; t0 += 64) {
-            if (surv_n + 64 > (uint32_t)kWaveSurv) wave_emit(S, X, P, m, L, surv_n, cand_n, tau);
+            if (surv_n + 64 > (uint32_t)kWaveSurv) wave_emit(S, X, P, m, L, sc_long, sc_short, surv_n, cand_n, tau);
             const uint32_t t = t0 + lane;
             uint32_t match = 0;
             if (t < X.n_short) {
                 const uint64_t a = X.term_off[t], b = X.term_off[t + 1];
                 match = string_match(qc, m, X.term_bytes + a, (uint32_t)(b - a));
             }
-            const float s = __shfl(s_lane, (int)match);
-            const bool pass = t < X.n_short && match >= cmin_s;
-            const unsigned long long bb = __ballot(pass);
-            if (pass) S.surv[surv_n + __popcll(bb & lanes_below())] = make_uint2(t, __float_as_uint(s));
-            surv_n += __popcll(bb);
+            surv_append(S, t < X.n_short && match >= cmin_s, t, match | 0x80u, surv_n);
         }
     }
 
     // ---- searchLong (nGramSearch.hpp:278-301) ----
-    // lane i: gram i of the query; dedup with multiplicity; lane g < ng then owns a distinct gram
+    // lane i: gram i of the query; dedup with multiplicity; lanes 0..ng-1 then own the
+    // distinct grams that have postings
     uint32_t code = 0xFFFFFFFFu;
     if (lane < n) {
         const uint32_t c0 = S.q[lane], c1 = S.q[lane + 1], c2 = S.q[lane + 2];
@@ -958,19 +966,17 @@ __global__ __launch_bounds__(64) void k_wave(DevIndex X, SearchParams P, const u
             first &= j >= lane;
         }
     }
-    uint64_t gbase = 0, glen = 0;
-    uint32_t grow = 0;
+    uint64_t gbase = 0;
+    uint32_t glen = 0, grow = 0;
     bool have = false;
     if (lane < n && first && code != 0xFFFFFFFFu) {
         gbase = X.gram_off[code];
-        glen = X.gram_off[code + 1] - gbase;
+        glen = (uint32_t)(X.gram_off[code + 1] - gbase);
         grow = X.gram_row[code];
         have = glen != 0;
     }
     const unsigned long long hb = __ballot(have);
     const uint32_t ng = __popcll(hb);
-    const uint32_t slot = __popcll(hb & lanes_below());
-    // compact the distinct non-empty grams into lanes 0..ng-1
     {
         uint32_t src = 0;
         unsigned long long rest = hb;
@@ -978,100 +984,112 @@ __global__ __launch_bounds__(64) void k_wave(DevIndex X, SearchParams P, const u
             src = __ffsll((long long)rest) - 1;
             rest &= rest - 1;
         }
-        (void)slot;
         const uint64_t b2 = __shfl(gbase, (int)src);
-        const uint64_t l2 = __shfl(glen, (int)src);
-        const uint32_t r2 = __shfl(grow, (int)src);
-        const uint32_t m2 = __shfl(mult, (int)src);
+        const uint32_t l2 = __shfl(glen, (int)src), r2 = __shfl(grow, (int)src), m2 = __shfl(mult, (int)src);
         gbase = lane < ng ? b2 : 0;
         glen = lane < ng ? l2 : 0;
         grow = lane < ng ? r2 : 0;
         mult = lane < ng ? m2 : 0;
     }
-    const uint64_t p_total = wave_sum(glen);
-    // score of `count` hits held by lane `count`: (float)count / n (nGramSearch.hpp:300)
-    const float sc_lane = lane <= n ? (float)lane / (float)n : 0.0f;
-    const unsigned long long pm = __ballot(lane <= n && lane > 0 && !(sc_lane < P.thr));
+    const uint64_t p_total = wave_sum((uint64_t)glen);
+    const unsigned long long pm = __ballot(lane <= n && lane > 0 && !(sc_long < P.thr));  // hpp:315
     const uint32_t cmin = pm ? (uint32_t)(__ffsll((long long)pm) - 1) : 1000u;
-    const uint32_t K = X.n_buckets, span = X.bucket_span;
+    const bool uni_mult = !__ballot(lane < ng && mult != 1);
+    const bool sketch = cmin >= 3;
     if (p_total && cmin <= n) {
-        if (p_total <= (uint64_t)kWaveCap && n_long <= kMaxPartSpan) {
-            wave_part(S, X, P, m, L, 0, ng, gbase, (uint32_t)glen, mult, cmin, sc_lane, surv_n, cand_n, tau, err);
-        } else {
-            // fixed part width w (buckets) from the average density; part p = buckets
-            // [p*w, (p+1)*w). e0/e1/e2: per-lane list offsets of the ends of parts p, p+1, p+2.
-            const uint32_t wmax = (uint32_t)max64(1, min64(K, kMaxPartSpan / max(span, 1u)));
-            const uint32_t w = (uint32_t)max64(1, min64(wmax, (uint64_t)K * (kWaveCap * 5 / 8) / p_total));
-            const uint32_t np = (K + w - 1) / w;
-            const uint32_t* sk = X.skip + (size_t)grow * (K + 1);
-            auto bound = [&](uint32_t p) -> uint32_t { return lane < ng ? sk[min(K, (p + 1) * w)] : 0u; };
-            uint32_t cur = 0, e0 = bound(0), e1 = np > 1 ? bound(1) : 0u;
-            uint32_t tNext[16];
-            uint32_t totNext = 0;
-            bool fastNext = false;
-            // part 0: segments + posting loads in flight
-            {
-                const uint32_t tot = wave_sum(e0 - cur);
-                fastNext = tot <= (uint32_t)kWaveCap && span * min(w, K) <= kMaxPartSpan;
-                if (fastNext && tot) totNext = part_issue(S, 0, X, ng, gbase + cur, e0 - cur, mult, tNext);
-            }
-            for (uint32_t p = 0; p < np; ++p) {
-                const int buf = p & 1;
-                uint32_t tCur[16];
-#pragma unroll
-                for (int u = 0; u < 16; ++u) tCur[u] = tNext[u];  // waits for part p's loads only
-                const uint32_t totCur = totNext;
-                const bool fastCur = fastNext;
-                const uint32_t e2 = p + 2 < np ? bound(p + 2) : 0u;
-                // prefetch part p+1 while part p is counted
-                totNext = 0;
-                fastNext = false;
-                if (p + 1 < np) {
-                    const uint32_t tot = wave_sum(e1 - e0);
-                    fastNext = tot <= (uint32_t)kWaveCap && span * min(w, K) <= kMaxPartSpan;
-                    if (fastNext && tot) totNext = part_issue(S, buf ^ 1, X, ng, gbase + e0, e1 - e0, mult, tNext);
+        const uint32_t K = X.n_buckets, span = X.bucket_span;
+        const uint32_t wmax = (uint32_t)max64(1, min64(K, kMaxPartSpan / max(span, 1u)));
+        const uint32_t w = (uint32_t)max64(1, min64(wmax, (uint64_t)K * (kWaveCap * 5 / 8) / p_total));
+        const uint32_t* sk = X.skip + (size_t)grow * (K + 1);
+        // part iterator: buckets [bnext, bnext + w) unless one is above the cap, then term-id sub-parts
+        uint32_t cur = 0, bnext = 0;
+        uint32_t e_pre = lane < ng ? sk[min(K, w)] : 0u;  // prefetched end of the next bucket part
+        bool in_sub = false;
+        uint32_t sub_lo = 0, hi_lim = 0, sub_end = 0, sub_bnext = 0, step = 1;
+        uint32_t guard = 0;
+        auto next_part = [&](uint32_t& lo, uint64_t& start, uint32_t& len) -> bool {
+            for (;;) {
+                if (++guard > 8u * K + 4096u) {
+                    if (lane == 0) atomicOr(err, 4u);
+                    return false;
                 }
-                if (fastCur) {
-                    if (totCur) part_consume(S, buf, X, P, m, L, p * w * span, totCur, tCur, cmin, sc_lane, surv_n,
-                                             cand_n, tau, err);
-                } else {
-                    // a part above the cap: term-id sub-parts by lower_bound per lane (rare)
-                    const uint32_t lo_lim = p * w * span;
-                    const uint32_t hi_lim = (uint32_t)min64((uint64_t)min(K, (p + 1) * w) * span, n_long);
-                    uint32_t sub_lo = lo_lim, cc = cur;
-                    uint32_t step = (uint32_t)max64(1, min64((uint64_t)(hi_lim - lo_lim) * (kWaveCap * 3 / 4) /
-                                                                 max(wave_sum(e0 - cur), 1u), kMaxPartSpan));
-                    for (uint32_t g2 = 0; sub_lo < hi_lim; ++g2) {
-                        if (g2 > 4u * (hi_lim - lo_lim) + 64u) {
-                            if (lane == 0) atomicOr(err, 4u);
-                            break;
-                        }
-                        const uint32_t hi = (uint32_t)min64(hi_lim, (uint64_t)sub_lo + step);
-                        uint32_t a2 = cc, b2 = e0;
-                        if (lane < ng) {
-                            while (a2 < b2) {
-                                const uint32_t mid = (a2 + b2) >> 1;
-                                if (X.post[gbase + mid] < hi) a2 = mid + 1; else b2 = mid;
-                            }
-                        }
-                        const uint32_t t2 = wave_sum(lane < ng ? a2 - cc : 0u);
-                        if (t2 > (uint32_t)kWaveCap && hi - sub_lo > 1) {
-                            step = max(1u, (uint32_t)((uint64_t)(hi - sub_lo) * (kWaveCap * 3 / 4) / t2));
-                            continue;
-                        }
-                        wave_part(S, X, P, m, L, sub_lo, ng, gbase + cc, a2 - cc, mult, cmin, sc_lane, surv_n,
-                                  cand_n, tau, err);
-                        cc = a2;
-                        sub_lo = hi;
+                if (!in_sub) {
+                    if (bnext >= K) return false;
+                    const uint32_t bhi = min(K, bnext + w), e = e_pre;
+                    const uint32_t tot = wave_sum(lane < ng ? e - cur : 0u);
+                    if (tot <= (uint32_t)kWaveCap && (uint64_t)span * (bhi - bnext) <= kMaxPartSpan) {
+                        lo = bnext * span;
+                        start = gbase + cur;
+                        len = e - cur;
+                        cur = e;
+                        bnext = bhi;
+                        e_pre = lane < ng && bnext < K ? sk[min(K, bnext + w)] : 0u;
+                        if (tot) return true;
+                        continue;
+                    }
+                    in_sub = true;
+                    sub_lo = bnext * span;
+                    hi_lim = (uint32_t)min64((uint64_t)bhi * span, n_long);
+                    sub_end = e;
+                    sub_bnext = bhi;
+                    step = (uint32_t)max64(1, min64((uint64_t)(hi_lim - sub_lo) * (kWaveCap * 3 / 4) / max(tot, 1u),
+                                                    kMaxPartSpan));
+                }
+                const uint32_t hi = (uint32_t)min64(hi_lim, (uint64_t)sub_lo + step);
+                uint32_t a = cur, b = sub_end;
+                if (lane < ng) {
+                    while (a < b) {  // lower_bound(list, hi)
+                        const uint32_t mid = (a + b) >> 1;
+                        if (X.post[gbase + mid] < hi) a = mid + 1; else b = mid;
                     }
                 }
-                cur = e0;
-                e0 = e1;
-                e1 = e2;
+                const uint32_t t2 = wave_sum(lane < ng ? a - cur : 0u);
+                if (t2 > (uint32_t)kWaveCap && hi - sub_lo > 1) {
+                    step = max(1u, (uint32_t)((uint64_t)(hi - sub_lo) * (kWaveCap * 3 / 4) / t2));
+                    continue;
+                }
+                lo = sub_lo;
+                start = gbase + cur;
+                len = a - cur;
+                cur = a;
+                sub_lo = hi;
+                if (sub_lo >= hi_lim) {
+                    in_sub = false;
+                    bnext = sub_bnext;
+                    e_pre = lane < ng && bnext < K ? sk[min(K, bnext + w)] : 0u;
+                }
+                if (t2) return true;
             }
+        };
+        uint32_t tNext[16];
+        uint32_t totNext = 0, loNext = 0;
+        bool have_next = false;
+#pragma unroll
+        for (int u = 0; u < 16; ++u) tNext[u] = 0;
+        for (uint32_t it = 0;; ++it) {
+            uint32_t tCur[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) tCur[u] = tNext[u];  // part it-1: loaded one part ago
+            const bool have_cur = have_next;
+            const uint32_t totCur = totNext, loCur = loNext;
+            uint32_t lo = 0, len = 0;
+            uint64_t start = 0;
+            have_next = next_part(lo, start, len);
+            if (have_next) {
+                totNext = part_issue(S, it & 1, X, ng, start, len, mult, tNext);
+                loNext = lo;
+            }
+            if (have_cur) {
+                if (surv_n + kWaveCap > (uint32_t)kWaveSurv)
+                    wave_emit(S, X, P, m, L, sc_long, sc_short, surv_n, cand_n, tau);
+                const int buf = (it - 1) & 1;
+                const bool done = sketch && part_sketch(S, buf, totCur, uni_mult, tCur, cmin, X.n_short, surv_n);
+                if (!done) part_exact(S, buf, loCur, totCur, uni_mult, tCur, cmin, X.n_short, surv_n, err);
+            }
+            if (!have_next) break;
         }
     }
-    if (surv_n) wave_emit(S, X, P, m, L, surv_n, cand_n, tau);
+    if (surv_n) wave_emit(S, X, P, m, L, sc_long, sc_short, surv_n, cand_n, tau);
     wave_flush(S, cand_n, tau, L);
     for (uint32_t i = lane; i < cand_n; i += 64) {
         const uint64_t r = S.cand[i];
