@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <memory>
@@ -254,6 +255,11 @@ int device_search(Library& L, Context& c, const uint8_t* d_raw, const uint64_t* 
     P.limit = limit;
     P.out_stride = stride;
     P.n_queries = B;
+    static const uint32_t dbg = [] {
+        const char* e = std::getenv("NGS_DEBUG");
+        return e ? (uint32_t)std::strtoul(e, nullptr, 0) : 0u;
+    }();
+    P.dbg = dbg;
     {
         std::lock_guard<std::mutex> g(L.valid_mu);
         std::memcpy(P.valid, L.valid, sizeof(P.valid));

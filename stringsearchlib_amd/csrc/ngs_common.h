@@ -52,7 +52,7 @@ constexpr int kWaveSlots = 1 << kWaveSlotBits;  // wave-private LDS hash table
 constexpr int kWaveCap = kWaveSlots / 2;        // postings per part (<= 50 % load)
 constexpr int kWaveCand = 256;                  // candidate buffer per query
 constexpr uint32_t kWaveMaxLimit = kWaveCand / 2;
-constexpr int kWaveSurv = kWaveCap + 256;       // survivor list (term, count) before calcScore
+constexpr int kWaveSurv = 320;                  // survivor list (term, count) before calcScore
 constexpr uint32_t kWaveMaxGrams = 63;          // counts <= 63: one lane per count value
 
 struct DevIndex {  // passed by value to kernels; all pointers are device pointers
@@ -78,6 +78,7 @@ struct SearchParams {
     uint32_t out_stride;
     uint32_t n_queries;
     uint32_t valid[8];   // 256-bit validChar mask (h:307-313 / setValidChar)
+    uint32_t dbg;        // ablation switches for performance experiments (NGS_DEBUG); 0 in production
 };
 
 // per-query normalised length sentinels written by the prep kernel

@@ -19,15 +19,23 @@ namespace {
 
 #ifdef NGS_PHASE_STAMPS
 // Diagnostic build only (make prof): block-time per phase of k_fast, in 100 MHz ticks.
-__device__ unsigned long long g_phase[16];
+__device__ unsigned long long g_phase[32];
 #define STAMP(i)                                                          \
     if (threadIdx.x == 0) {                                               \
         const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();   \
         atomicAdd(&g_phase[i], t_ - tp_);                                 \
         tp_ = t_;                                                         \
     }
+// wave kernel: cycles (s_memtime) per phase, phases 16..31
+#define WSTAMP(i)                                                         \
+    {                                                                     \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();       \
+        wacc_[i] += t_ - wt_;                                             \
+        wt_ = t_;                                                         \
+    }
 #else
 #define STAMP(i)
+#define WSTAMP(i)
 #endif
 
 __device__ __forceinline__ uint64_t min64(uint64_t a, uint64_t b) { return a < b ? a : b; }
@@ -606,26 +614,35 @@ __global__ __launch_bounds__(kFastThreads) void k_fast(DevIndex X, SearchParams 
 }
 
 // ---------------------------------------------------------------- wave kernel --------
-// Tier 1: ONE WAVE PER QUERY, wave-private LDS (no block barriers; ~8 queries in flight per
-// CU). A query's lists are cut into term-id parts of <= kWaveCap postings (bucket skip table;
-// oversized buckets are split by lower_bound); part p+1's postings are loaded into registers
-// while part p is counted. Terms reaching cmin go to a survivor list that calcScore consumes
-// in batches; the running top-L lives in the wave's candidate buffer.
+// Tier 1: ONE WAVE PER QUERY, wave-private LDS (no block barriers). A query's gram lists are
+// cut into term-id parts of <= kWaveCap postings (bucket skip table; a bucket above the cap is
+// split by lower_bound). Each part is DMA'd list-segment by list-segment straight into an LDS
+// stage (global_load_lds: uniform addressing, no per-posting index walk), then counted from
+// LDS with predication only. A repeated query gram is kept as a separate occurrence (its list
+// is read once per occurrence), which is the reference's multiplicity (hpp:289-298).
 struct WaveSmem {
     uint32_t table[kWaveSlots];    // exact: (term - lo + 1) << 8 | count; sketch: 2 x u16 counters
+    uint32_t stage[kWaveCap];      // the part's postings; the exact form reuses it for slot ids
     uint64_t cand[kWaveCand];      // (~enc) << 32 | key
     uint32_t surv_t[kWaveSurv];    // survivor terms
     uint8_t surv_c[kWaveSurv];     // hit count, | 0x80 for a Levenshtein (short search) match count
-    uint64_t pseg_start[2][64];    // part segments, double-buffered: first posting of each gram
-    uint32_t pseg_pre[2][68];      //   exclusive prefix of the segment lengths
-    uint32_t pseg_mult[2][64];     //   multiplicity of the gram in the query
-    uint2 cbuf[64];                // sketch candidates (term, mult)
+    uint2 cbuf[64];                // sketch candidates (term, 1)
+    uint32_t mkey[128];            // their exact-count table (0xFFFFFFFF = empty)
+    uint32_t mcnt[128];
     uint8_t q[kWaveMaxGrams + 8];
     uint32_t surv_total;           // stats
 };
 
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
 __device__ __forceinline__ unsigned long long lanes_below() { return (1ull << lane_id()) - 1ull; }
+
+// Ordering point for the wave-private LDS. A wave's LDS instructions execute in order, so
+// no barrier and no wait is needed: only keep the compiler from moving LDS accesses across.
+// (__syncthreads() would also drain every outstanding global load.)
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
 
 template <class T>
 __device__ __forceinline__ T wave_sum(T v) {
@@ -642,7 +659,7 @@ __device__ void wave_flush(WaveSmem& S, uint32_t& cand_n, uint64_t& tau, uint32_
         const uint64_t r = i < n ? S.cand[i] : kNoCand;
         S.cand[i] = i < n ? ((r << 32) | (r >> 32)) : kNoCand;  // key-major for the dedup
     }
-    __syncthreads();
+    wave_sync();
     for (int pass = 0; pass < 2; ++pass) {
         for (uint32_t k = 2; k <= P2; k <<= 1) {
             for (uint32_t j = k >> 1; j > 0; j >>= 1) {
@@ -651,7 +668,7 @@ __device__ void wave_flush(WaveSmem& S, uint32_t& cand_n, uint64_t& tau, uint32_
                     const uint64_t x = S.cand[i], y = S.cand[l];
                     if ((x > y) == ((i & k) == 0)) { S.cand[i] = y; S.cand[l] = x; }
                 }
-                __syncthreads();
+                wave_sync();
             }
         }
         if (pass == 1) break;
@@ -665,20 +682,20 @@ __device__ void wave_flush(WaveSmem& S, uint32_t& cand_n, uint64_t& tau, uint32_
                 if (d != kNoCand && (i == 0 || (S.cand[i - 1] >> 32) != (d >> 32))) keep[u] = (d << 32) | (d >> 32);
             }
         }
-        __syncthreads();
+        wave_sync();
 #pragma unroll
         for (int u = 0; u < kWaveCand / 64; ++u) {
             const uint32_t i = lane + u * 64;
             if (i < P2) S.cand[i] = keep[u];
         }
-        __syncthreads();
+        wave_sync();
     }
     uint32_t mine = 0;
     for (uint32_t i = lane; i < P2; i += 64) mine += S.cand[i] != kNoCand;
     const uint32_t nv = wave_sum(mine);
     cand_n = min(nv, L);
     tau = nv >= L ? S.cand[L - 1] : kNoCand;
-    __syncthreads();
+    wave_sync();
 }
 
 // calcScore (nGramSearch.hpp:310-341) over the survivor list: term -> (key, weight) pairs,
@@ -687,7 +704,7 @@ __device__ void wave_emit(WaveSmem& S, const DevIndex& X, const SearchParams& P,
                           float sc_long, float sc_short, uint32_t& surv_n, uint32_t& cand_n, uint64_t& tau) {
     const uint32_t lane = lane_id();
     S.surv_total += surv_n;
-    __syncthreads();
+    wave_sync();
     for (uint32_t base = 0; base < surv_n; base += 64) {
         const uint32_t i = base + lane;
         uint32_t p = 0, pe = 0, code = 0;
@@ -715,7 +732,7 @@ __device__ void wave_emit(WaveSmem& S, const DevIndex& X, const SearchParams& P,
         }
     }
     surv_n = 0;
-    __syncthreads();
+    wave_sync();
 }
 
 __device__ __forceinline__ void surv_append(WaveSmem& S, bool pass, uint32_t t, uint32_t code, uint32_t& surv_n) {
@@ -728,64 +745,19 @@ __device__ __forceinline__ void surv_append(WaveSmem& S, bool pass, uint32_t t, 
     surv_n += __popcll(b);
 }
 
-static_assert(kWaveCap == 16 * 64, "a part is one register per lane per 64 postings");
-
-// Publishes the part's segments (lane g < ng: [start, start + len)) into LDS buffer `buf` and
-// issues every posting load of the part into t[]; returns the part's posting count.
-__device__ __forceinline__ uint32_t part_issue(WaveSmem& S, int buf, const DevIndex& X, uint32_t ng,
-                                               uint64_t start, uint32_t len, uint32_t mult, uint32_t (&t)[16]) {
-    const uint32_t lane = lane_id();
-    uint32_t incl = lane < ng ? len : 0u;
-    const uint32_t mine = incl;
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(incl, o);
-        if ((int)lane >= o) incl += y;
-    }
-    const uint32_t total = __shfl(incl, 63);
-    if (lane < ng) {
-        S.pseg_start[buf][lane] = start;
-        S.pseg_pre[buf][lane] = incl - mine;
-        S.pseg_mult[buf][lane] = mult;
-    }
-    if (lane == 0) S.pseg_pre[buf][ng] = total;
-    __syncthreads();
-    uint32_t g = 0, nxt = S.pseg_pre[buf][1];
-    uint64_t base = S.pseg_start[buf][0];
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-        const uint32_t j = lane + u * 64;
-        t[u] = 0;
-        if (j < total) {
-            while (j >= nxt) {
-                ++g;
-                nxt = S.pseg_pre[buf][g + 1];
-                base = S.pseg_start[buf][g] - S.pseg_pre[buf][g];
-            }
-            t[u] = X.post[base + j];
-        }
-    }
-    return total;
-}
-
-__device__ __forceinline__ uint32_t part_mult(WaveSmem& S, int buf, uint32_t j) {
-    uint32_t g = 0;
-    while (S.pseg_pre[buf][g + 1] <= j) ++g;
-    return S.pseg_mult[buf][g];
-}
-
-__device__ __forceinline__ uint32_t wave_insert_slot(uint32_t* T, uint32_t rel, uint32_t mult, unsigned* err) {
+__device__ __forceinline__ uint32_t wave_insert_slot(uint32_t* T, uint32_t rel, unsigned* err) {
     uint32_t probes = 0;
     uint32_t h = (rel * 0x9E3779B1u) >> (32 - kWaveSlotBits);
     const uint32_t want = rel << 8;
     for (;;) {
         uint32_t cur = T[h];
         if (cur == 0) {
-            const uint32_t prev = atomicCAS(&T[h], 0u, want | mult);
+            const uint32_t prev = atomicCAS(&T[h], 0u, want | 1u);
             if (prev == 0) return h;
             cur = prev;
         }
         if ((cur >> 8) == rel) {
-            atomicAdd(&T[h], mult);
+            atomicAdd(&T[h], 1u);
             return h;
         }
         h = (h + 1) & (kWaveSlots - 1);
@@ -798,91 +770,74 @@ __device__ __forceinline__ uint32_t wave_insert_slot(uint32_t* T, uint32_t rel, 
 
 __device__ __forceinline__ uint32_t sketch_cell(uint32_t t) { return (t * 0x9E3779B1u) >> (32 - kWaveSlotBits - 1); }
 
-// Exact count of a part: LDS hash table; each posting keeps its slot, and the extraction
-// exchanges the slot with 0 so the first holder of a term owns its count (no table scan).
-__device__ __forceinline__ void part_exact(WaveSmem& S, int buf, uint32_t lo, uint32_t total, bool uni_mult,
-                                           const uint32_t (&t)[16], uint32_t cmin, uint32_t n_short,
-                                           uint32_t& surv_n, unsigned* err) {
+// Exact count of the staged part: LDS hash table term -> count; each posting's slot replaces
+// it in the stage, and the extraction exchanges the slot with 0, so the first holder of a term
+// owns its count (no table scan; the table ends empty).
+__device__ void part_exact(WaveSmem& S, const DevIndex& X, const SearchParams& P, uint32_t m, uint32_t L,
+                           uint32_t lo, uint32_t total, uint32_t cmin, float sc_long, float sc_short,
+                           uint32_t& surv_n, uint32_t& cand_n, uint64_t& tau, unsigned* err) {
     const uint32_t lane = lane_id();
-    uint32_t sl[16];
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-        const uint32_t j = lane + u * 64;
-        sl[u] = 0;
-        if (j < total) sl[u] = wave_insert_slot(S.table, t[u] - lo + 1u, uni_mult ? 1u : part_mult(S, buf, j), err);
-    }
-    __syncthreads();
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-        const uint32_t j = lane + u * 64;
-        const uint32_t v = j < total ? atomicExch(&S.table[sl[u]], 0u) : 0u;
+    for (uint32_t j = lane; j < total; j += 64) S.stage[j] = wave_insert_slot(S.table, S.stage[j] - lo + 1u, err);
+    wave_sync();
+    for (uint32_t j0 = 0; j0 < total; j0 += 64) {
+        if (surv_n + 64 > (uint32_t)kWaveSurv) wave_emit(S, X, P, m, L, sc_long, sc_short, surv_n, cand_n, tau);
+        const uint32_t j = j0 + lane;
+        const uint32_t v = j < total ? atomicExch(&S.table[S.stage[j]], 0u) : 0u;
         const uint32_t cnt = v & 255u;  // s = cnt / n; s >= thr <=> cnt >= cmin (nGramSearch.hpp:300,315)
-        surv_append(S, v != 0 && cnt >= cmin, n_short + lo + (v >> 8) - 1u, cnt, surv_n);
+        surv_append(S, v != 0 && cnt >= cmin, X.n_short + lo + (v >> 8) - 1u, cnt, surv_n);
     }
-    __syncthreads();
+    wave_sync();
 }
 
-// Sketch count of a part (cmin >= 3): 2 x u16 counters per table word (never undercounts);
-// returns false when more than 64 postings can reach cmin (the caller then counts exactly).
-__device__ __forceinline__ bool part_sketch(WaveSmem& S, int buf, uint32_t total, bool uni_mult,
-                                            const uint32_t (&t)[16], uint32_t cmin, uint32_t n_short,
-                                            uint32_t& surv_n) {
+// Sketch count of the staged part (cmin >= 3): 2 x u16 counters per table word, never an
+// undercount; only postings whose cell reaches cmin are counted exactly (128-slot table).
+// Returns false when more than 64 postings pass (the caller then counts the part exactly).
+__device__ bool part_sketch(WaveSmem& S, uint32_t total, uint32_t cmin, uint32_t n_short, uint32_t& surv_n) {
     const uint32_t lane = lane_id();
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-        const uint32_t j = lane + u * 64;
-        if (j < total) {
-            const uint32_t c = sketch_cell(t[u]);
-            atomicAdd(&S.table[c >> 1], (uni_mult ? 1u : part_mult(S, buf, j)) << ((c & 1u) << 4));
-        }
+    const uint32_t rounds = (total + 63) >> 6;
+    for (uint32_t r = 0; r < rounds; ++r) {
+        const uint32_t j = lane + (r << 6);
+        const uint32_t c = sketch_cell(S.stage[min(j, total - 1)]);
+        atomicAdd(&S.table[c >> 1], (j < total ? 1u : 0u) << ((c & 1u) << 4));
     }
-    __syncthreads();
+    wave_sync();
     uint32_t nc = 0;
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-        const uint32_t j = lane + u * 64;
-        bool pass = false;
-        if (j < total) {
-            const uint32_t c = sketch_cell(t[u]);
-            pass = ((S.table[c >> 1] >> ((c & 1u) << 4)) & 0xFFFFu) >= cmin;
-        }
+    for (uint32_t r = 0; r < rounds; ++r) {
+        const uint32_t j = lane + (r << 6);
+        const uint32_t t = S.stage[min(j, total - 1)];
+        const uint32_t c = sketch_cell(t);
+        const bool pass = j < total && ((S.table[c >> 1] >> ((c & 1u) << 4)) & 0xFFFFu) >= cmin;
         const unsigned long long b = __ballot(pass);
         const uint32_t idx = nc + __popcll(b & lanes_below());
-        if (pass && idx < 64) S.cbuf[idx] = make_uint2(t[u], uni_mult ? 1u : part_mult(S, buf, j));
+        if (pass && idx < 64) S.cbuf[idx] = make_uint2(t, 1u);
         nc += __popcll(b);
     }
-    __syncthreads();
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-        const uint32_t j = lane + u * 64;
-        if (j < total) S.table[sketch_cell(t[u]) >> 1] = 0;
+    wave_sync();
+    {
+        uint4* T4 = reinterpret_cast<uint4*>(S.table);
+        for (uint32_t i = lane; i < (uint32_t)kWaveSlots / 4; i += 64) T4[i] = make_uint4(0, 0, 0, 0);
     }
-    __syncthreads();
+    wave_sync();
     if (nc > 64) return false;
     if (nc == 0) return true;
-    // exact counts of the <= 64 candidate postings: bitonic sort of (term, mult) across lanes
-    uint32_t key = lane < nc ? S.cbuf[lane].x : 0xFFFFFFFFu;
-    uint32_t val = lane < nc ? S.cbuf[lane].y : 0u;
-    for (uint32_t k = 2; k <= 64; k <<= 1) {
-        for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
-            const uint32_t ok = __shfl_xor(key, (int)jj), ov = __shfl_xor(val, (int)jj);
-            const bool up = (lane & k) == 0, lower = (lane & jj) == 0;
-            if (lower == up ? ok < key : ok > key) {
-                key = ok;
-                val = ov;
-            }
+    // exact counts of the <= 64 candidate postings; the lane that exchanges a slot's count
+    // with 0 first owns the term
+    const bool act = lane < nc;
+    const uint32_t key = act ? S.cbuf[lane].x : 0u;
+    uint32_t h = (key * 0x9E3779B1u) >> 25;
+    if (act) {
+        for (uint32_t probe = 0; probe < 128; ++probe, h = (h + 1) & 127u) {
+            const uint32_t prev = atomicCAS(&S.mkey[h], 0xFFFFFFFFu, key);
+            if (prev == 0xFFFFFFFFu || prev == key) break;
         }
+        atomicAdd(&S.mcnt[h], 1u);
     }
-    const uint32_t prevk = __shfl_up(key, 1);
-    const bool head = key != 0xFFFFFFFFu && (lane == 0 || prevk != key);
-    uint32_t acc = val;
-    for (uint32_t d = 1; d < 64; ++d) {
-        const uint32_t nk = __shfl_down(key, (int)d), nv = __shfl_down(val, (int)d);
-        const bool more = lane + d < 64 && nk == key;
-        if (!__ballot(more)) break;
-        if (more) acc += nv;
-    }
-    surv_append(S, head && acc >= cmin, n_short + key, acc, surv_n);
+    wave_sync();
+    const uint32_t acc = act ? atomicExch(&S.mcnt[h], 0u) : 0u;
+    wave_sync();
+    if (act) S.mkey[h] = 0xFFFFFFFFu;
+    wave_sync();
+    surv_append(S, acc != 0 && acc >= cmin, n_short + key, acc, surv_n);
     return true;
 }
 
@@ -915,14 +870,22 @@ __global__ __launch_bounds__(64) void k_wave(DevIndex X, SearchParams P, const u
     }
     const uint32_t n = m - 2;
     const uint32_t n_long = X.n_terms - X.n_short;
+#ifdef NGS_PHASE_STAMPS
+    unsigned long long wt_ = __builtin_amdgcn_s_memtime();
+    unsigned long long wacc_[11] = {};
+#endif
     const uint8_t* qg = qnorm + qoff[q];
     for (uint32_t i = lane; i < m; i += 64) S.q[i] = qg[i];
     if (lane == 0) S.surv_total = 0;
+    S.mkey[lane] = 0xFFFFFFFFu;
+    S.mkey[lane + 64] = 0xFFFFFFFFu;
+    S.mcnt[lane] = 0;
+    S.mcnt[lane + 64] = 0;
     {
         uint4* T4 = reinterpret_cast<uint4*>(S.table);
         for (uint32_t i = lane; i < (uint32_t)kWaveSlots / 4; i += 64) T4[i] = make_uint4(0, 0, 0, 0);
     }
-    __syncthreads();
+    wave_sync();
     uint32_t cand_n = 0, surv_n = 0;
     uint64_t tau = kNoCand;
     unsigned* err = &stats->errors;
@@ -948,32 +911,23 @@ __global__ __launch_bounds__(64) void k_wave(DevIndex X, SearchParams P, const u
             surv_append(S, t < X.n_short && match >= cmin_s, t, match | 0x80u, surv_n);
         }
     }
+    WSTAMP(0);
 
     // ---- searchLong (nGramSearch.hpp:278-301) ----
-    // lane i: gram i of the query; dedup with multiplicity; lanes 0..ng-1 then own the
-    // distinct grams that have postings
-    uint32_t code = 0xFFFFFFFFu;
-    if (lane < n) {
-        const uint32_t c0 = S.q[lane], c1 = S.q[lane + 1], c2 = S.q[lane + 2];
-        if (!((c0 | c1 | c2) & 0x80u)) code = (c0 << 14) | (c1 << 7) | c2;
-    }
-    uint32_t mult = 0;
-    bool first = true;
-    for (uint32_t j = 0; j < n; ++j) {
-        const uint32_t cj = __shfl(code, (int)j);
-        if (cj == code) {
-            mult += 1;
-            first &= j >= lane;
-        }
-    }
+    // lane i: occurrence i of a query gram; lanes 0..ng-1 then own the occurrences whose gram
+    // has postings (a gram repeated k times owns k lanes: count with multiplicity)
     uint64_t gbase = 0;
     uint32_t glen = 0, grow = 0;
     bool have = false;
-    if (lane < n && first && code != 0xFFFFFFFFu) {
-        gbase = X.gram_off[code];
-        glen = (uint32_t)(X.gram_off[code + 1] - gbase);
-        grow = X.gram_row[code];
-        have = glen != 0;
+    if (lane < n) {
+        const uint32_t c0 = S.q[lane], c1 = S.q[lane + 1], c2 = S.q[lane + 2];
+        if (!((c0 | c1 | c2) & 0x80u)) {
+            const uint32_t code = (c0 << 14) | (c1 << 7) | c2;
+            gbase = X.gram_off[code];
+            glen = (uint32_t)(X.gram_off[code + 1] - gbase);
+            grow = X.gram_row[code];
+            have = glen != 0;
+        }
     }
     const unsigned long long hb = __ballot(have);
     const uint32_t ng = __popcll(hb);
@@ -985,17 +939,16 @@ __global__ __launch_bounds__(64) void k_wave(DevIndex X, SearchParams P, const u
             rest &= rest - 1;
         }
         const uint64_t b2 = __shfl(gbase, (int)src);
-        const uint32_t l2 = __shfl(glen, (int)src), r2 = __shfl(grow, (int)src), m2 = __shfl(mult, (int)src);
+        const uint32_t l2 = __shfl(glen, (int)src), r2 = __shfl(grow, (int)src);
         gbase = lane < ng ? b2 : 0;
         glen = lane < ng ? l2 : 0;
         grow = lane < ng ? r2 : 0;
-        mult = lane < ng ? m2 : 0;
     }
     const uint64_t p_total = wave_sum((uint64_t)glen);
     const unsigned long long pm = __ballot(lane <= n && lane > 0 && !(sc_long < P.thr));  // hpp:315
     const uint32_t cmin = pm ? (uint32_t)(__ffsll((long long)pm) - 1) : 1000u;
-    const bool uni_mult = !__ballot(lane < ng && mult != 1);
     const bool sketch = cmin >= 3;
+    WSTAMP(1);
     if (p_total && cmin <= n) {
         const uint32_t K = X.n_buckets, span = X.bucket_span;
         const uint32_t wmax = (uint32_t)max64(1, min64(K, kMaxPartSpan / max(span, 1u)));
@@ -1003,28 +956,29 @@ __global__ __launch_bounds__(64) void k_wave(DevIndex X, SearchParams P, const u
         const uint32_t* sk = X.skip + (size_t)grow * (K + 1);
         // part iterator: buckets [bnext, bnext + w) unless one is above the cap, then term-id sub-parts
         uint32_t cur = 0, bnext = 0;
-        uint32_t e_pre = lane < ng ? sk[min(K, w)] : 0u;  // prefetched end of the next bucket part
+        uint32_t e_pre = sk[min(K, w)];  // end of the next bucket part (row 0 for idle lanes)
         bool in_sub = false;
         uint32_t sub_lo = 0, hi_lim = 0, sub_end = 0, sub_bnext = 0, step = 1;
-        uint32_t guard = 0;
-        auto next_part = [&](uint32_t& lo, uint64_t& start, uint32_t& len) -> bool {
+        for (uint32_t guard = 0;;) {
+            // ---- next part: [lo, ...) with per-lane segments [gbase + cur, gbase + cur + len) ----
+            uint32_t lo = 0, len = 0;
+            bool have_part = false;
             for (;;) {
                 if (++guard > 8u * K + 4096u) {
                     if (lane == 0) atomicOr(err, 4u);
-                    return false;
+                    break;
                 }
                 if (!in_sub) {
-                    if (bnext >= K) return false;
-                    const uint32_t bhi = min(K, bnext + w), e = e_pre;
-                    const uint32_t tot = wave_sum(lane < ng ? e - cur : 0u);
+                    if (bnext >= K) break;
+                    const uint32_t bhi = min(K, bnext + w), e = lane < ng ? e_pre : 0u;
+                    const uint32_t tot = wave_sum(e - cur);
                     if (tot <= (uint32_t)kWaveCap && (uint64_t)span * (bhi - bnext) <= kMaxPartSpan) {
                         lo = bnext * span;
-                        start = gbase + cur;
                         len = e - cur;
-                        cur = e;
                         bnext = bhi;
-                        e_pre = lane < ng && bnext < K ? sk[min(K, bnext + w)] : 0u;
-                        if (tot) return true;
+                        e_pre = sk[min(K, bnext + w)];
+                        if (tot) { have_part = true; break; }
+                        cur = e;
                         continue;
                     }
                     in_sub = true;
@@ -1049,48 +1003,51 @@ __global__ __launch_bounds__(64) void k_wave(DevIndex X, SearchParams P, const u
                     continue;
                 }
                 lo = sub_lo;
-                start = gbase + cur;
-                len = a - cur;
-                cur = a;
+                len = lane < ng ? a - cur : 0u;
                 sub_lo = hi;
                 if (sub_lo >= hi_lim) {
                     in_sub = false;
                     bnext = sub_bnext;
-                    e_pre = lane < ng && bnext < K ? sk[min(K, bnext + w)] : 0u;
+                    e_pre = sk[min(K, bnext + w)];
                 }
-                if (t2) return true;
+                if (t2) { have_part = true; break; }
+                cur = a;
             }
-        };
-        uint32_t tNext[16];
-        uint32_t totNext = 0, loNext = 0;
-        bool have_next = false;
-#pragma unroll
-        for (int u = 0; u < 16; ++u) tNext[u] = 0;
-        for (uint32_t it = 0;; ++it) {
-            uint32_t tCur[16];
-#pragma unroll
-            for (int u = 0; u < 16; ++u) tCur[u] = tNext[u];  // part it-1: loaded one part ago
-            const bool have_cur = have_next;
-            const uint32_t totCur = totNext, loCur = loNext;
-            uint32_t lo = 0, len = 0;
-            uint64_t start = 0;
-            have_next = next_part(lo, start, len);
-            if (have_next) {
-                totNext = part_issue(S, it & 1, X, ng, start, len, mult, tNext);
-                loNext = lo;
+            WSTAMP(3);
+            if (!have_part) break;
+            // ---- stage the part: one DMA per 64 postings of each list segment ----
+            uint32_t off = 0;
+            for (uint32_t g = 0; g < ng; ++g) {
+                const uint32_t sl = __builtin_amdgcn_readlane(len, g);
+                const uint32_t c0 = __builtin_amdgcn_readlane(cur, g);
+                const uint64_t gb = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(gbase >> 32), g) << 32) |
+                                    __builtin_amdgcn_readlane((uint32_t)gbase, g);
+                const uint32_t* src = X.post + gb + c0;
+                for (uint32_t k = 0; k < sl; k += 64) {
+                    if (k + lane < sl)
+                        __builtin_amdgcn_global_load_lds(src + k + lane,
+                                                         (__attribute__((address_space(3))) void*)(S.stage + off + k),
+                                                         4, 0, 0);
+                }
+                off += sl;
             }
-            if (have_cur) {
-                if (surv_n + kWaveCap > (uint32_t)kWaveSurv)
-                    wave_emit(S, X, P, m, L, sc_long, sc_short, surv_n, cand_n, tau);
-                const int buf = (it - 1) & 1;
-                const bool done = sketch && part_sketch(S, buf, totCur, uni_mult, tCur, cmin, X.n_short, surv_n);
-                if (!done) part_exact(S, buf, loCur, totCur, uni_mult, tCur, cmin, X.n_short, surv_n, err);
-            }
-            if (!have_next) break;
+            cur += len;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            wave_sync();
+            WSTAMP(4);
+            const uint32_t total = off;
+            if (surv_n + 64 > (uint32_t)kWaveSurv) wave_emit(S, X, P, m, L, sc_long, sc_short, surv_n, cand_n, tau);
+            const bool done = sketch && part_sketch(S, total, cmin, X.n_short, surv_n);
+            WSTAMP(5);
+            if (!done) part_exact(S, X, P, m, L, lo, total, cmin, sc_long, sc_short, surv_n, cand_n, tau, err);
+            WSTAMP(6);
         }
     }
+    WSTAMP(7);
     if (surv_n) wave_emit(S, X, P, m, L, sc_long, sc_short, surv_n, cand_n, tau);
+    WSTAMP(8);
     wave_flush(S, cand_n, tau, L);
+    WSTAMP(9);
     for (uint32_t i = lane; i < cand_n; i += 64) {
         const uint64_t r = S.cand[i];
         const uint32_t enc = ~(uint32_t)(r >> 32);
@@ -1105,6 +1062,11 @@ __global__ __launch_bounds__(64) void k_wave(DevIndex X, SearchParams P, const u
         atomicAdd(&stats->fast, 1ull);
         atomicAdd(&stats->survivors, (unsigned long long)S.surv_total);
     }
+    WSTAMP(10);
+#ifdef NGS_PHASE_STAMPS
+    if (lane == 0)
+        for (int i = 0; i < 11; ++i) atomicAdd(&g_phase[16 + i], wacc_[i]);
+#endif
 }
 
 // ---------------------------------------------------------------- general path -------
@@ -1242,14 +1204,14 @@ hipError_t build_wildcard(const float* d_w, uint32_t n_keys, uint32_t* d_keys, f
 
 int phase_stats(unsigned long long* out, int n, bool reset) {
 #ifdef NGS_PHASE_STAMPS
-    unsigned long long h[16];
+    unsigned long long h[32];
     if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_phase), sizeof(h)) != hipSuccess) return -1;
-    for (int i = 0; i < n && i < 16; ++i) out[i] = h[i];
+    for (int i = 0; i < n && i < 32; ++i) out[i] = h[i];
     if (reset) {
-        unsigned long long z[16] = {};
+        unsigned long long z[32] = {};
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof(z)) != hipSuccess) return -1;
     }
-    return 16;
+    return 32;
 #else
     (void)out; (void)n; (void)reset;
     return -1;

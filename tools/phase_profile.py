@@ -26,14 +26,20 @@ def main():
     arr = (C.c_char_p * B)(*qs)
     counts = (C.c_uint32 * B)()
     for it in range(3):
-        out = (C.c_uint64 * 16)()
-        L.ngsPhaseStats(out, 16, 1)
+        out = (C.c_uint64 * 32)()
+        L.ngsPhaseStats(out, 32, 1)
         res, sc = C.POINTER(C.POINTER(C.c_char))(), C.POINTER(C.c_float)()
         t = time.time()
         L.scoreBatch(h, arr, B, thr, 100, counts, C.byref(res), C.byref(sc))
         dt = time.time() - t
         L.release(h, res, sc)
-        L.ngsPhaseStats(out, 16, 1)
+        L.ngsPhaseStats(out, 32, 1)
+    wn = ["setup+short", "grams", "loop-top", "next_part", "issue", "sketch", "exact", "loop-exit", "emit",
+          "flush", "write"]
+    wt = sum(out[16 + i] for i in range(len(wn)))
+    print(f"k_wave: per-query wave time {wt/B:.0f} cycles")
+    for i, nm in enumerate(wn):
+        print(f"  {nm:10s} {out[16+i]/B:9.0f} cyc/query  {100*out[16+i]/max(wt,1):5.1f} %")
     tot = sum(out[i] for i in range(12))
     print(f"rows={rows} B={B} thr={thr} wall={dt*1e3:.1f} ms; per-query block time {tot/B/100:.2f} us")
     for i, nm in enumerate(NAMES):
