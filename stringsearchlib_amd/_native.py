@@ -14,9 +14,10 @@ import subprocess
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 LIB_DIR = os.path.join(PKG, "lib")
-# NGS_LIB=prof selects the phase-stamped diagnostic build (make -C csrc prof)
-LIB_PATH = os.path.join(LIB_DIR, "libngram_search_prof.so" if os.environ.get("NGS_LIB") == "prof"
-                        else "libngram_search.so")
+# NGS_LIB=prof selects the phase-stamped diagnostic build (make -C csrc prof); NGS_LIB=<name>
+# selects lib/libngram_search_<name>.so (experiment builds)
+_variant = os.environ.get("NGS_LIB", "")
+LIB_PATH = os.path.join(LIB_DIR, f"libngram_search_{_variant}.so" if _variant else "libngram_search.so")
 SYNTH_PATH = os.path.join(LIB_DIR, "libngs_synth.so")
 HEADER = os.path.join(ROOT, "include", "ngram_search.h")
 CSRC = os.path.join(PKG, "csrc")

@@ -44,9 +44,10 @@ bool dev_alloc(T** p, size_t n) {
 }
 
 template <class T>
-bool dev_upload(T** p, const std::vector<T>& v, std::vector<void*>& owned) {
-    if (!dev_alloc(p, v.size())) return false;
+bool dev_upload(T** p, const std::vector<T>& v, std::vector<void*>& owned, size_t pad = 0) {
+    if (!dev_alloc(p, v.size() + pad)) return false;
     owned.push_back(*p);
+    if (pad && !HIP_CHECK(hipMemset(*p + v.size(), 0, pad * sizeof(T)))) return false;
     return v.empty() || HIP_CHECK(hipMemcpy(*p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
 }
 
@@ -154,7 +155,7 @@ bool upload(Library& L) {
     uint2* tk;
     float *wild_w, *wild_score;
     L.on_device = true;  // from here on the destructor frees what was allocated
-    bool ok = dev_upload(&gram_off, H.gram_off, L.owned) && dev_upload(&post, H.post, L.owned) &&
+    bool ok = dev_upload(&gram_off, H.gram_off, L.owned) && dev_upload(&post, H.post, L.owned, 4) /* k_wave stages whole 16-byte chunks */ &&
               dev_upload(&term_off, H.term_off, L.owned) && dev_upload(&term_bytes, H.term_bytes, L.owned) &&
               dev_upload(&tk_off, H.tk_off, L.owned) && dev_upload(&tk, H.tk, L.owned) &&
               dev_upload(&key_off, H.key_off, L.owned) && dev_upload(&key_bytes, kb, L.owned) &&

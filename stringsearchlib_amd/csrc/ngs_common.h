@@ -43,7 +43,7 @@ constexpr uint32_t kFastMaxGrams = 255;  // u8 counts in the table slot
 constexpr uint32_t kMaxPartSpan = (1u << 24) - 2;  // 24-bit relative term id in the slot
 
 // bucket skip table: K <= kMaxBuckets term-id buckets of >= kMinBucketTerms terms each
-constexpr uint32_t kMaxBuckets = 64;
+constexpr uint32_t kMaxBuckets = 256;
 constexpr uint32_t kMinBucketTerms = 4096;
 
 // ---- wave kernel geometry (tier 1: one wave per query) ----
@@ -52,6 +52,10 @@ constexpr int kWaveSlots = 1 << kWaveSlotBits;  // wave-private LDS hash table
 constexpr int kWaveCap = kWaveSlots / 2;        // postings per part (<= 50 % load)
 constexpr int kWaveCand = 256;                  // candidate buffer per query
 constexpr uint32_t kWaveMaxLimit = kWaveCand / 2;
+constexpr int kWaveChunks = kWaveCap / 4;       // 16-byte chunks per stage buffer
+constexpr int kDmaRounds = kWaveChunks / 64;    // dwordx4 LDS-DMAs to fill one
+constexpr int kWaveTarget = kWaveCap * 5 / 8;   // postings per part the bucket grouping aims at
+constexpr uint32_t kStray = 0xFFFFFFFFu;        // staged entry outside its list segment
 constexpr int kWaveSurv = 320;                  // survivor list (term, count) before calcScore
 constexpr uint32_t kWaveMaxGrams = 63;          // counts <= 63: one lane per count value
 

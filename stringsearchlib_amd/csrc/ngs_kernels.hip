@@ -620,9 +620,9 @@ __global__ __launch_bounds__(kFastThreads) void k_fast(DevIndex X, SearchParams 
 // stage (global_load_lds: uniform addressing, no per-posting index walk), then counted from
 // LDS with predication only. A repeated query gram is kept as a separate occurrence (its list
 // is read once per occurrence), which is the reference's multiplicity (hpp:289-298).
-struct WaveSmem {
+struct alignas(16) WaveSmem {
     uint32_t table[kWaveSlots];    // exact: (term - lo + 1) << 8 | count; sketch: 2 x u16 counters
-    uint32_t stage[kWaveCap];      // the part's postings; the exact form reuses it for slot ids
+    uint32_t stage[2 * kWaveCap];  // two parts' postings (DMA double buffer); exact form: slot ids
     uint64_t cand[kWaveCand];      // (~enc) << 32 | key
     uint32_t surv_t[kWaveSurv];    // survivor terms
     uint8_t surv_c[kWaveSurv];     // hit count, | 0x80 for a Levenshtein (short search) match count
@@ -634,6 +634,23 @@ struct WaveSmem {
 };
 
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
+
+// One LDS-DMA dword per active lane: LDS[lds_base + 4 * lane] = *g. Issued from asm so the
+// compiler's wait-count pass does not treat it as aliasing every later LDS access (it would
+// drain it before each ds_read); vmcnt is in-order, so the compiler's own waits only over-wait.
+// The caller makes the data visible with an explicit s_waitcnt vmcnt(0).
+__device__ __forceinline__ void dma_dword(const uint32_t* g, uint32_t lds_base) {
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(g), "s"(lds_base)
+                 : "memory", "m0");
+}
+// Same for 16 bytes per lane: LDS[lds_base + 16 * lane ..] = *g.
+__device__ __forceinline__ void dma_x4(const uint4* g, uint32_t lds_base) {
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(lds_base)
+                 : "memory", "m0");
+}
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
 __device__ __forceinline__ unsigned long long lanes_below() { return (1ull << lane_id()) - 1ull; }
 
 // Ordering point for the wave-private LDS. A wave's LDS instructions execute in order, so
@@ -647,6 +664,40 @@ __device__ __forceinline__ void wave_sync() {
 template <class T>
 __device__ __forceinline__ T wave_sum(T v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+template <int Ctrl>
+__device__ __forceinline__ uint32_t dpp_mov(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, Ctrl, 0xf, 0xf, false);
+}
+
+// Wave-uniform u32 sum in DPP steps (quad perms, row rotations, row broadcasts) instead of
+// six dependent ds_bpermute round trips; the total is read from lane 63 into an SGPR.
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+    v += dpp_mov<0xb1>(v);   // quad_perm [1,0,3,2]
+    v += dpp_mov<0x4e>(v);   // quad_perm [2,3,0,1]
+    v += dpp_mov<0x124>(v);  // row_ror:4
+    v += dpp_mov<0x128>(v);  // row_ror:8
+    v += dpp_mov<0x142>(v);  // row_bcast:15
+    v += dpp_mov<0x143>(v);  // row_bcast:31
+    return __builtin_amdgcn_readlane(v, 63);
+}
+
+template <int Ctrl, int RowMask>
+__device__ __forceinline__ uint32_t dpp_mov_rows(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, Ctrl, RowMask, 0xf, false);
+}
+
+// Inclusive prefix sum across the wave: row shifts within each 16-lane row, then the row
+// broadcasts carry rows 0 -> 1, 2 -> 3 and (0..1) -> (2..3). Lanes without a source add 0.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    v += dpp_mov_rows<0x111, 0xf>(v);  // row_shr:1
+    v += dpp_mov_rows<0x112, 0xf>(v);  // row_shr:2
+    v += dpp_mov_rows<0x114, 0xf>(v);  // row_shr:4
+    v += dpp_mov_rows<0x118, 0xf>(v);  // row_shr:8
+    v += dpp_mov_rows<0x142, 0xa>(v);  // row_bcast:15 into rows 1 and 3
+    v += dpp_mov_rows<0x143, 0xc>(v);  // row_bcast:31 into rows 2 and 3
     return v;
 }
 
@@ -773,18 +824,22 @@ __device__ __forceinline__ uint32_t sketch_cell(uint32_t t) { return (t * 0x9E37
 // Exact count of the staged part: LDS hash table term -> count; each posting's slot replaces
 // it in the stage, and the extraction exchanges the slot with 0, so the first holder of a term
 // owns its count (no table scan; the table ends empty).
-__device__ void part_exact(WaveSmem& S, const DevIndex& X, const SearchParams& P, uint32_t m, uint32_t L,
-                           uint32_t lo, uint32_t total, uint32_t cmin, float sc_long, float sc_short,
+__device__ void part_exact(WaveSmem& S, uint32_t* st, const DevIndex& X, const SearchParams& P, uint32_t m,
+                           uint32_t L, uint32_t lo, uint32_t total, uint32_t cmin, float sc_long, float sc_short,
                            uint32_t& surv_n, uint32_t& cand_n, uint64_t& tau, unsigned* err) {
     const uint32_t lane = lane_id();
-    for (uint32_t j = lane; j < total; j += 64) S.stage[j] = wave_insert_slot(S.table, S.stage[j] - lo + 1u, err);
+    for (uint32_t j = lane; j < total; j += 64) {
+        const uint32_t t = st[j];
+        st[j] = t != kStray ? wave_insert_slot(S.table, t - lo + 1u, err) : kStray;
+    }
     wave_sync();
     for (uint32_t j0 = 0; j0 < total; j0 += 64) {
         if (surv_n + 64 > (uint32_t)kWaveSurv) wave_emit(S, X, P, m, L, sc_long, sc_short, surv_n, cand_n, tau);
         const uint32_t j = j0 + lane;
-        const uint32_t v = j < total ? atomicExch(&S.table[S.stage[j]], 0u) : 0u;
+        const uint32_t sl = j < total ? st[j] : kStray;
+        const uint32_t v = sl != kStray ? atomicExch(&S.table[sl], 0u) : 0u;
         const uint32_t cnt = v & 255u;  // s = cnt / n; s >= thr <=> cnt >= cmin (nGramSearch.hpp:300,315)
-        surv_append(S, v != 0 && cnt >= cmin, X.n_short + lo + (v >> 8) - 1u, cnt, surv_n);
+        surv_append(S, v != 0 && cnt >= cmin, min(X.n_short + lo + (v >> 8) - 1u, X.n_terms - 1u), cnt, surv_n);
     }
     wave_sync();
 }
@@ -792,25 +847,38 @@ __device__ void part_exact(WaveSmem& S, const DevIndex& X, const SearchParams& P
 // Sketch count of the staged part (cmin >= 3): 2 x u16 counters per table word, never an
 // undercount; only postings whose cell reaches cmin are counted exactly (128-slot table).
 // Returns false when more than 64 postings pass (the caller then counts the part exactly).
-__device__ bool part_sketch(WaveSmem& S, uint32_t total, uint32_t cmin, uint32_t n_short, uint32_t& surv_n) {
+__device__ bool part_sketch(WaveSmem& S, const uint32_t* st, uint32_t total, uint32_t cmin, uint32_t n_short,
+                            uint32_t n_terms, uint32_t& surv_n) {
     const uint32_t lane = lane_id();
-    const uint32_t rounds = (total + 63) >> 6;
+    const uint4* st4 = reinterpret_cast<const uint4*>(st);
+    const uint32_t rounds = (total + 255) >> 8;  // 4 postings per lane per round (b128 reads)
     for (uint32_t r = 0; r < rounds; ++r) {
-        const uint32_t j = lane + (r << 6);
-        const uint32_t c = sketch_cell(S.stage[min(j, total - 1)]);
-        atomicAdd(&S.table[c >> 1], (j < total ? 1u : 0u) << ((c & 1u) << 4));
+        const uint4 v = st4[(r << 6) + lane];
+        const uint32_t j = (r << 8) + (lane << 2);
+        const uint32_t c0 = sketch_cell(v.x), c1 = sketch_cell(v.y), c2 = sketch_cell(v.z), c3 = sketch_cell(v.w);
+        atomicAdd(&S.table[c0 >> 1], (j + 0 < total && v.x != kStray ? 1u : 0u) << ((c0 & 1u) << 4));
+        atomicAdd(&S.table[c1 >> 1], (j + 1 < total && v.y != kStray ? 1u : 0u) << ((c1 & 1u) << 4));
+        atomicAdd(&S.table[c2 >> 1], (j + 2 < total && v.z != kStray ? 1u : 0u) << ((c2 & 1u) << 4));
+        atomicAdd(&S.table[c3 >> 1], (j + 3 < total && v.w != kStray ? 1u : 0u) << ((c3 & 1u) << 4));
     }
     wave_sync();
     uint32_t nc = 0;
     for (uint32_t r = 0; r < rounds; ++r) {
-        const uint32_t j = lane + (r << 6);
-        const uint32_t t = S.stage[min(j, total - 1)];
-        const uint32_t c = sketch_cell(t);
-        const bool pass = j < total && ((S.table[c >> 1] >> ((c & 1u) << 4)) & 0xFFFFu) >= cmin;
-        const unsigned long long b = __ballot(pass);
-        const uint32_t idx = nc + __popcll(b & lanes_below());
-        if (pass && idx < 64) S.cbuf[idx] = make_uint2(t, 1u);
-        nc += __popcll(b);
+        const uint4 v = st4[(r << 6) + lane];
+        const uint32_t j = (r << 8) + (lane << 2);
+        const uint32_t t[4] = {v.x, v.y, v.z, v.w};
+        uint32_t w[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) w[e] = S.table[sketch_cell(t[e]) >> 1];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const uint32_t c = sketch_cell(t[e]);
+            const bool pass = j + e < total && t[e] != kStray && ((w[e] >> ((c & 1u) << 4)) & 0xFFFFu) >= cmin;
+            const unsigned long long b = __ballot(pass);
+            const uint32_t idx = nc + __popcll(b & lanes_below());
+            if (pass && idx < 64) S.cbuf[idx] = make_uint2(t[e], 1u);
+            nc += __popcll(b);
+        }
     }
     wave_sync();
     {
@@ -837,7 +905,7 @@ __device__ bool part_sketch(WaveSmem& S, uint32_t total, uint32_t cmin, uint32_t
     wave_sync();
     if (act) S.mkey[h] = 0xFFFFFFFFu;
     wave_sync();
-    surv_append(S, acc != 0 && acc >= cmin, n_short + key, acc, surv_n);
+    surv_append(S, acc != 0 && acc >= cmin, min(n_short + key, n_terms - 1u), acc, surv_n);
     return true;
 }
 
@@ -952,14 +1020,34 @@ __global__ __launch_bounds__(64) void k_wave(DevIndex X, SearchParams P, const u
     if (p_total && cmin <= n) {
         const uint32_t K = X.n_buckets, span = X.bucket_span;
         const uint32_t wmax = (uint32_t)max64(1, min64(K, kMaxPartSpan / max(span, 1u)));
-        const uint32_t w = (uint32_t)max64(1, min64(wmax, (uint64_t)K * (kWaveCap * 5 / 8) / p_total));
+        const uint32_t w = (uint32_t)max64(1, min64(wmax, (uint64_t)K * kWaveTarget / p_total));
         const uint32_t* sk = X.skip + (size_t)grow * (K + 1);
-        // part iterator: buckets [bnext, bnext + w) unless one is above the cap, then term-id sub-parts
+        const uint4* post4 = reinterpret_cast<const uint4*>(X.post);
+        const uint32_t a0 = (uint32_t)gbase & 3u;  // list start within its 16-byte chunk
+        // entries [s, e) of this lane's list cover 16-byte chunks [(a0 + s) / 4, (a0 + e + 3) / 4)
+        auto chunks = [a0](uint32_t s, uint32_t e) -> uint32_t { return e > s ? ((a0 + e + 3) >> 2) - ((a0 + s) >> 2) : 0u; };
+        // part iterator: buckets [bnext, bnext + w) unless they exceed the stage, then term-id sub-parts
         uint32_t cur = 0, bnext = 0;
         uint32_t e_pre = sk[min(K, w)];  // end of the next bucket part (row 0 for idle lanes)
         bool in_sub = false;
         uint32_t sub_lo = 0, hi_lim = 0, sub_end = 0, sub_bnext = 0, step = 1;
+        // software pipeline over two stage buffers: wait for part i, DMA part i+1, count part i
+        int cb = -1;  // stage buffer holding the part to count (-1: none yet)
+        uint32_t c_lo = 0, c_tot = 0;                  // its term-id base and staged entries (4 per chunk)
+        uint32_t c_p = 0, c_n = 0, c_head = 0, c_tail = 0;  // this lane's segment: first chunk, chunks, strays
         for (uint32_t guard = 0;;) {
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // part cb has landed
+            wave_sync();
+            if (cb >= 0 && c_n) {  // the chunk edges hold up to 3 entries of neighbouring lists
+                uint32_t* st = S.stage + cb * kWaveCap;
+                for (uint32_t j = 0; j < 3; ++j) {
+                    if (j < c_head) st[4 * c_p + j] = kStray;
+                    if (j < c_tail) st[4 * (c_p + c_n) - 1 - j] = kStray;
+                }
+            }
+            wave_sync();
+            WSTAMP(2);
+            const uint32_t nb = cb == 0 ? 1u : 0u;
             // ---- next part: [lo, ...) with per-lane segments [gbase + cur, gbase + cur + len) ----
             uint32_t lo = 0, len = 0;
             bool have_part = false;
@@ -970,15 +1058,14 @@ __global__ __launch_bounds__(64) void k_wave(DevIndex X, SearchParams P, const u
                 }
                 if (!in_sub) {
                     if (bnext >= K) break;
-                    const uint32_t bhi = min(K, bnext + w), e = lane < ng ? e_pre : 0u;
-                    const uint32_t tot = wave_sum(e - cur);
-                    if (tot <= (uint32_t)kWaveCap && (uint64_t)span * (bhi - bnext) <= kMaxPartSpan) {
+                    const uint32_t bhi = min(K, bnext + w), e = lane < ng ? e_pre : cur;
+                    const uint32_t tot = wave_sum_u32(chunks(cur, e));
+                    if (tot <= (uint32_t)kWaveChunks && (uint64_t)span * (bhi - bnext) <= kMaxPartSpan) {
                         lo = bnext * span;
                         len = e - cur;
                         bnext = bhi;
                         e_pre = sk[min(K, bnext + w)];
                         if (tot) { have_part = true; break; }
-                        cur = e;
                         continue;
                     }
                     in_sub = true;
@@ -986,7 +1073,7 @@ __global__ __launch_bounds__(64) void k_wave(DevIndex X, SearchParams P, const u
                     hi_lim = (uint32_t)min64((uint64_t)bhi * span, n_long);
                     sub_end = e;
                     sub_bnext = bhi;
-                    step = (uint32_t)max64(1, min64((uint64_t)(hi_lim - sub_lo) * (kWaveCap * 3 / 4) / max(tot, 1u),
+                    step = (uint32_t)max64(1, min64((uint64_t)(hi_lim - sub_lo) * (kWaveChunks * 3 / 4) / max(tot, 1u),
                                                     kMaxPartSpan));
                 }
                 const uint32_t hi = (uint32_t)min64(hi_lim, (uint64_t)sub_lo + step);
@@ -997,9 +1084,9 @@ __global__ __launch_bounds__(64) void k_wave(DevIndex X, SearchParams P, const u
                         if (X.post[gbase + mid] < hi) a = mid + 1; else b = mid;
                     }
                 }
-                const uint32_t t2 = wave_sum(lane < ng ? a - cur : 0u);
-                if (t2 > (uint32_t)kWaveCap && hi - sub_lo > 1) {
-                    step = max(1u, (uint32_t)((uint64_t)(hi - sub_lo) * (kWaveCap * 3 / 4) / t2));
+                const uint32_t t2 = wave_sum_u32(lane < ng ? chunks(cur, a) : 0u);
+                if (t2 > (uint32_t)kWaveChunks && hi - sub_lo > 1) {
+                    step = max(1u, (uint32_t)((uint64_t)(hi - sub_lo) * (kWaveChunks * 3 / 4) / t2));
                     continue;
                 }
                 lo = sub_lo;
@@ -1014,33 +1101,56 @@ __global__ __launch_bounds__(64) void k_wave(DevIndex X, SearchParams P, const u
                 cur = a;
             }
             WSTAMP(3);
-            if (!have_part) break;
-            // ---- stage the part: one DMA per 64 postings of each list segment ----
-            uint32_t off = 0;
-            for (uint32_t g = 0; g < ng; ++g) {
-                const uint32_t sl = __builtin_amdgcn_readlane(len, g);
-                const uint32_t c0 = __builtin_amdgcn_readlane(cur, g);
-                const uint64_t gb = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(gbase >> 32), g) << 32) |
-                                    __builtin_amdgcn_readlane((uint32_t)gbase, g);
-                const uint32_t* src = X.post + gb + c0;
-                for (uint32_t k = 0; k < sl; k += 64) {
-                    if (k + lane < sl)
-                        __builtin_amdgcn_global_load_lds(src + k + lane,
-                                                         (__attribute__((address_space(3))) void*)(S.stage + off + k),
-                                                         4, 0, 0);
+            // ---- stage part i+1: its lists' 16-byte chunks packed across the wave, <= kDmaRounds DMAs ----
+            uint32_t n_tot = 0, n_p = 0, n_n = 0, n_head = 0, n_tail = 0;
+            if (have_part && (!(P.dbg & 2u) || cb < 0)) {  // dbg 2: stage only the first part
+                const uint32_t nch = chunks(cur, cur + len);
+                const uint32_t incl = wave_incl_scan(nch);
+                const uint32_t pre = incl - nch;
+                const uint32_t tch = __builtin_amdgcn_readlane(incl, 63);
+                const uint32_t cs = (uint32_t)((gbase + cur) >> 2) - pre;  // chunk c of the part <- cs + c
+                uint32_t src[kDmaRounds] = {};
+                for (uint32_t g = 0; g < ng; ++g) {  // the last non-empty segment starting at or before c
+                    if (__builtin_amdgcn_readlane(nch, g) == 0) continue;
+                    const uint32_t sp = __builtin_amdgcn_readlane(pre, g), sb = __builtin_amdgcn_readlane(cs, g);
+#pragma unroll
+                    for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r)
+                        if (64 * r + lane >= sp) src[r] = sb + 64 * r + lane;
                 }
-                off += sl;
+                const uint32_t d0 = lds_addr(S.stage + nb * kWaveCap);
+#pragma unroll
+                for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) {
+                    if (64 * r < tch && 64 * r + lane < tch) dma_x4(post4 + src[r], d0 + 1024 * r);
+                }
+                n_tot = 4 * tch;
+                n_p = pre;
+                n_n = nch;
+                n_head = (a0 + cur) & 3u;
+                n_tail = (4u - ((a0 + cur + len) & 3u)) & 3u;
+            } else if (have_part) {
+                const uint32_t nch = chunks(cur, cur + len);
+                n_tot = 4 * wave_sum_u32(nch);
             }
-            cur += len;
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            wave_sync();
+            if (have_part) cur += len;
             WSTAMP(4);
-            const uint32_t total = off;
-            if (surv_n + 64 > (uint32_t)kWaveSurv) wave_emit(S, X, P, m, L, sc_long, sc_short, surv_n, cand_n, tau);
-            const bool done = sketch && part_sketch(S, total, cmin, X.n_short, surv_n);
-            WSTAMP(5);
-            if (!done) part_exact(S, X, P, m, L, lo, total, cmin, sc_long, sc_short, surv_n, cand_n, tau, err);
-            WSTAMP(6);
+            // ---- count part i while part i+1 is in flight ----
+            if (cb >= 0 && !(P.dbg & 1u)) {  // dbg 1: stage only, no counting
+                uint32_t* st = S.stage + cb * kWaveCap;
+                if (surv_n + 64 > (uint32_t)kWaveSurv)
+                    wave_emit(S, X, P, m, L, sc_long, sc_short, surv_n, cand_n, tau);
+                const bool done = sketch && part_sketch(S, st, c_tot, cmin, X.n_short, X.n_terms, surv_n);
+                WSTAMP(5);
+                if (!done) part_exact(S, st, X, P, m, L, c_lo, c_tot, cmin, sc_long, sc_short, surv_n, cand_n, tau, err);
+                WSTAMP(6);
+            }
+            if (!have_part) break;
+            cb = (int)nb;
+            c_lo = lo;
+            c_tot = n_tot;
+            c_p = n_p;
+            c_n = n_n;
+            c_head = n_head;
+            c_tail = n_tail;
         }
     }
     WSTAMP(7);

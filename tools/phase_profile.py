@@ -34,7 +34,7 @@ def main():
         dt = time.time() - t
         L.release(h, res, sc)
         L.ngsPhaseStats(out, 32, 1)
-    wn = ["setup+short", "grams", "loop-top", "next_part", "issue", "sketch", "exact", "loop-exit", "emit",
+    wn = ["setup+short", "grams", "dma-wait", "next_part", "issue", "sketch", "exact", "loop-exit", "emit",
           "flush", "write"]
     wt = sum(out[16 + i] for i in range(len(wn)))
     print(f"k_wave: per-query wave time {wt/B:.0f} cycles")
