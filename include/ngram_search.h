@@ -99,7 +99,7 @@ NGS_API const char* ngsKey(uint32_t handle, uint32_t keyId);
  * min(limit ? limit : 2^31-1, ngsNumKeys). `stream` is a hipStream_t (NULL = the handle's
  * own stream); the call returns when the results are complete on that stream.
  * Returns 0, or a negative error (-1 bad handle, -2 un-built index, -3 bad argument,
- * -4 HIP failure). */
+ * -4 HIP failure, -5 internal error flagged by a kernel, e.g. an exhausted LDS table). */
 NGS_API int ngsSearchDevice(uint32_t handle, const uint8_t* dQueryBytes, const uint64_t* dQueryOffsets,
                             uint32_t nQueries, float threshold, uint32_t limit, uint32_t outStride,
                             uint32_t* dCounts, uint32_t* dKeys, float* dScores, void* stream);
@@ -109,7 +109,7 @@ typedef struct {
     uint64_t queries;          /* queries in the call */
     uint64_t fast_queries;     /* handled by the fused LDS kernel */
     uint64_t general_queries;  /* handled by the dense library-wide kernels */
-    uint64_t postings;         /* sum over fast queries of posting ids read (distinct grams) */
+    uint64_t postings;         /* posting ids read by the LDS kernels (k_wave: per gram occurrence) */
     uint64_t lists;            /* posting lists opened */
     uint64_t results;          /* results written by the fused kernel */
     uint64_t survivors;        /* terms whose match ratio passed the threshold (fused kernel) */
@@ -123,8 +123,8 @@ NGS_API int ngsLastStats(uint32_t handle, ngs_stats* out);
 /* Library build identification (e.g. "gfx950 ngram_search 0.1"). */
 NGS_API const char* ngsVersion(void);
 
-/* Diagnostics: per-phase block time of the fused kernel (100 MHz ticks, summed over blocks)
- * in the instrumented build libngram_search_prof.so; -1 in the regular build. */
+/* Diagnostics: per-phase time of the LDS kernels (s_memtime shader-clock ticks, summed over
+ * waves / blocks) in the instrumented build libngram_search_prof.so; -1 in the regular build. */
 NGS_API int ngsPhaseStats(uint64_t* out, int n, int reset);
 
 #ifdef __cplusplus

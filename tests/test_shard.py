@@ -1,0 +1,85 @@
+"""Multi-rank path of bench.py / shard.py on CPU: world size 2 over gloo.
+
+Each rank takes its contiguous query slice (shard_bounds) and scores it, with the CPU oracle
+standing in for the GPU searcher, since this container has no GPU. It writes the fixed-stride
+device layout that ngsSearchDevice produces, compacts it and gathers it to rank 0. Rank 0
+checks that the gathered per-rank results, concatenated, equal the whole batch scored in
+one piece.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle_py import OracleIndex
+from stringsearchlib_amd import shard, synth
+
+LIMIT = 20
+THR = 0.25
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _device_layout(oi, queries, stride):
+    """(counts[B], keys[B*stride], scores[B*stride]) as ngsSearchDevice writes them."""
+    B = len(queries)
+    counts = torch.zeros(B, dtype=torch.int32)
+    keys = torch.full((B * stride,), -1, dtype=torch.int32)
+    scores = torch.full((B * stride,), -1.0, dtype=torch.float32)
+    for i, q in enumerate(queries):
+        ids, sc = oi.score_ids(q, THR, LIMIT)
+        counts[i] = len(ids)
+        keys[i * stride:i * stride + len(ids)] = torch.tensor(ids, dtype=torch.int32)
+        scores[i * stride:i * stride + len(sc)] = torch.tensor(sc, dtype=torch.float32)
+    return counts, keys, scores
+
+
+def _worker(rank, world, port, result_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        words, wts, rng = synth.gen_corpus(3000, seed=7)
+        queries = synth.gen_queries(words, 1, 64, rng)
+        oi = OracleIndex(words, 1, wts)
+        lo, hi = shard.shard_bounds(rank, world, len(queries))
+        stride = LIMIT
+        c, k, s = shard.compact(*_device_layout(oi, queries[lo:hi], stride), stride)
+        got = shard.gather_to_root(c, k, s)
+        if rank == 0:
+            flat = []
+            for counts, keys, scores in got:
+                o = 0
+                for n in counts.tolist():
+                    flat.append((keys[o:o + n].tolist(), scores[o:o + n].tolist()))
+                    o += n
+            want = [tuple(map(list, oi.score_ids(q, THR, LIMIT))) for q in queries]
+            ok = len(flat) == len(want) and all(
+                a == list(b[0]) and torch.equal(torch.tensor(sa, dtype=torch.float32),
+                                                 torch.tensor(b[1], dtype=torch.float32))
+                for (a, sa), b in zip(flat, want))
+            with open(result_path, "w") as f:
+                f.write("ok" if ok else f"mismatch: {flat[:2]} vs {want[:2]}")
+        oi.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_gather_matches_single_batch(tmp_path):
+    out = tmp_path / "result.txt"
+    mp.spawn(_worker, args=(2, _free_port(), str(out)), nprocs=2, join=True)
+    assert out.read_text() == "ok"
+
+
+def test_shard_bounds_cover_batch():
+    for world in (1, 2, 3, 8):
+        spans = [shard.shard_bounds(r, world, 65536 + 5) for r in range(world)]
+        assert spans[0][0] == 0 and spans[-1][1] == 65541
+        assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
