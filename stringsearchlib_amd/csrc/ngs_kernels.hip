@@ -615,42 +615,25 @@ __global__ __launch_bounds__(kFastThreads) void k_fast(DevIndex X, SearchParams 
 
 // ---------------------------------------------------------------- wave kernel --------
 // Tier 1: ONE WAVE PER QUERY, wave-private LDS (no block barriers). A query's gram lists are
-// cut into term-id parts of <= kWaveCap postings (bucket skip table; a bucket above the cap is
-// split by lower_bound). Each part is DMA'd list-segment by list-segment straight into an LDS
-// stage (global_load_lds: uniform addressing, no per-posting index walk), then counted from
-// LDS with predication only. A repeated query gram is kept as a separate occurrence (its list
-// is read once per occurrence), which is the reference's multiplicity (hpp:289-298).
+// cut into term-id parts of <= kWaveChunks 16-byte chunks (bucket skip table; a bucket above
+// the cap is split by lower_bound). A part is loaded into registers, its lists' chunks packed
+// across the wave, while the previous part is counted against an LDS sketch / hash table
+// with predication only. A repeated query gram is kept as a separate occurrence (its list is
+// read once per occurrence), which is the reference's multiplicity (hpp:289-298).
 struct alignas(16) WaveSmem {
     uint32_t table[kWaveSlots];    // exact: (term - lo + 1) << 8 | count; sketch: 2 x u16 counters
-    uint32_t stage[2 * kWaveCap];  // two parts' postings (DMA double buffer); exact form: slot ids
     uint64_t cand[kWaveCand];      // (~enc) << 32 | key
+    uint4 segtab[64];              // staging: per list {first chunk - position, first entry, end entry, -}
+    uint32_t mark[kWaveChunks];    // staging: list index + 1 at the position of its first chunk
     uint32_t surv_t[kWaveSurv];    // survivor terms
+    uint32_t cbuf[64];             // sketch candidates (terms)
     uint8_t surv_c[kWaveSurv];     // hit count, | 0x80 for a Levenshtein (short search) match count
-    uint2 cbuf[64];                // sketch candidates (term, 1)
-    uint32_t mkey[128];            // their exact-count table (0xFFFFFFFF = empty)
-    uint32_t mcnt[128];
     uint8_t q[kWaveMaxGrams + 8];
     uint32_t surv_total;           // stats
 };
 
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
 
-// One LDS-DMA dword per active lane: LDS[lds_base + 4 * lane] = *g. Issued from asm so the
-// compiler's wait-count pass does not treat it as aliasing every later LDS access (it would
-// drain it before each ds_read); vmcnt is in-order, so the compiler's own waits only over-wait.
-// The caller makes the data visible with an explicit s_waitcnt vmcnt(0).
-__device__ __forceinline__ void dma_dword(const uint32_t* g, uint32_t lds_base) {
-    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(g), "s"(lds_base)
-                 : "memory", "m0");
-}
-// Same for 16 bytes per lane: LDS[lds_base + 16 * lane ..] = *g.
-__device__ __forceinline__ void dma_x4(const uint4* g, uint32_t lds_base) {
-    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(lds_base)
-                 : "memory", "m0");
-}
-__device__ __forceinline__ uint32_t lds_addr(const void* p) {
-    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
-}
 __device__ __forceinline__ unsigned long long lanes_below() { return (1ull << lane_id()) - 1ull; }
 
 // Ordering point for the wave-private LDS. A wave's LDS instructions execute in order, so
@@ -698,6 +681,17 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
     v += dpp_mov_rows<0x118, 0xf>(v);  // row_shr:8
     v += dpp_mov_rows<0x142, 0xa>(v);  // row_bcast:15 into rows 1 and 3
     v += dpp_mov_rows<0x143, 0xc>(v);  // row_bcast:31 into rows 2 and 3
+    return v;
+}
+
+// Inclusive prefix max across the wave, same DPP steps.
+__device__ __forceinline__ uint32_t wave_incl_max_scan(uint32_t v) {
+    v = max(v, dpp_mov_rows<0x111, 0xf>(v));
+    v = max(v, dpp_mov_rows<0x112, 0xf>(v));
+    v = max(v, dpp_mov_rows<0x114, 0xf>(v));
+    v = max(v, dpp_mov_rows<0x118, 0xf>(v));
+    v = max(v, dpp_mov_rows<0x142, 0xa>(v));
+    v = max(v, dpp_mov_rows<0x143, 0xc>(v));
     return v;
 }
 
@@ -821,63 +815,121 @@ __device__ __forceinline__ uint32_t wave_insert_slot(uint32_t* T, uint32_t rel, 
 
 __device__ __forceinline__ uint32_t sketch_cell(uint32_t t) { return (t * 0x9E3779B1u) >> (32 - kWaveSlotBits - 1); }
 
-// Exact count of the staged part: LDS hash table term -> count; each posting's slot replaces
-// it in the stage, and the extraction exchanges the slot with 0, so the first holder of a term
-// owns its count (no table scan; the table ends empty).
-__device__ void part_exact(WaveSmem& S, uint32_t* st, const DevIndex& X, const SearchParams& P, uint32_t m,
-                           uint32_t L, uint32_t lo, uint32_t total, uint32_t cmin, float sc_long, float sc_short,
-                           uint32_t& surv_n, uint32_t& cand_n, uint64_t& tau, unsigned* err) {
+// Loads one part into registers: lane g < ng contributes entries [cur, cur + len) of its list
+// (list base gbase, a0 = gbase % 4). The lists' 16-byte chunks are packed across the wave,
+// lane l holding chunks l, 64 + l, ... in v[0], v[1], ...: about one load instruction per
+// 256 postings, whatever the number of lists (MI355X issues scattered loads at a fixed
+// rate per instruction). A chunk finds its list through a marker per list
+// start and a max-scan; vmask bit 4r+e says whether entry e of v[r] belongs to the part
+// (chunk edges hold up to 3 entries of the neighbouring lists). Returns the chunk count.
+__device__ __forceinline__ uint32_t stage_part(WaveSmem& S, const uint4* __restrict__ post4, uint64_t gbase,
+                                               uint32_t a0, uint32_t cur, uint32_t len,
+                                               uint4 (&v)[kDmaRounds], uint32_t& vmask) {
     const uint32_t lane = lane_id();
-    for (uint32_t j = lane; j < total; j += 64) {
-        const uint32_t t = st[j];
-        st[j] = t != kStray ? wave_insert_slot(S.table, t - lo + 1u, err) : kStray;
+    const uint32_t head = (a0 + cur) & 3u;
+    const uint32_t nch = len ? (head + len + 3) >> 2 : 0u;
+    const uint32_t incl = wave_incl_scan(nch);
+    const uint32_t pre = incl - nch;
+    const uint32_t tch = __builtin_amdgcn_readlane(incl, 63);
+#pragma unroll
+    for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r)
+        if (64 * r < tch) S.mark[64 * r + lane] = 0;
+    wave_sync();
+    if (nch) {
+        S.mark[pre] = lane + 1;
+        const uint32_t first = (uint32_t)((gbase + cur) >> 2);
+        S.segtab[lane] = make_uint4(first - pre, 4 * pre + head, 4 * pre + head + len, 0);
     }
     wave_sync();
-    for (uint32_t j0 = 0; j0 < total; j0 += 64) {
+    uint32_t carry = 0;
+    vmask = 0;
+#pragma unroll
+    for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) {
+        if (64 * r < tch) {
+            const uint32_t c = 64 * r + lane;
+            const bool ok = c < tch;
+            const uint32_t sc = max(wave_incl_max_scan(ok ? S.mark[c] : 0u), carry);
+            carry = __builtin_amdgcn_readlane(sc, 63);
+            const uint4 seg = S.segtab[(sc - 1u) & 63u];
+            v[r] = post4[ok ? seg.x + c : 0u];
+            uint32_t bits = 0;
+#pragma unroll
+            for (uint32_t e = 0; e < 4; ++e) bits |= (ok && 4 * c + e >= seg.y && 4 * c + e < seg.z ? 1u : 0u) << e;
+            vmask |= bits << (4 * r);
+        }
+    }
+    return tch;
+}
+
+// Exact count of a part held in registers: LDS hash table term -> count. Each entry's slot
+// replaces its term in the registers; the extraction exchanges the slot with 0, so the first
+// holder of a term owns its count (no table scan; the table ends empty).
+__device__ __forceinline__ void part_exact(WaveSmem& S, uint4 (&v)[kDmaRounds], uint32_t vmask, uint32_t tch, const DevIndex& X,
+                           const SearchParams& P, uint32_t m, uint32_t L, uint32_t lo, uint32_t cmin, float sc_long,
+                           float sc_short, uint32_t& surv_n, uint32_t& cand_n, uint64_t& tau, unsigned* err) {
+#pragma unroll
+    for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) {
+        if (64 * r < tch) {
+#pragma unroll
+            for (uint32_t e = 0; e < 4; ++e) {
+                uint32_t& x = e == 0 ? v[r].x : e == 1 ? v[r].y : e == 2 ? v[r].z : v[r].w;
+                x = (vmask >> (4 * r + e)) & 1u ? wave_insert_slot(S.table, x - lo + 1u, err) : kStray;
+            }
+        }
+    }
+    wave_sync();
+    // one element slot per step (a single wave_emit call site keeps the registers out of scratch)
+    for (uint32_t k = 0; k < 4 * (uint32_t)kDmaRounds && 64 * (k >> 2) < tch; ++k) {
         if (surv_n + 64 > (uint32_t)kWaveSurv) wave_emit(S, X, P, m, L, sc_long, sc_short, surv_n, cand_n, tau);
-        const uint32_t j = j0 + lane;
-        const uint32_t sl = j < total ? st[j] : kStray;
-        const uint32_t v = sl != kStray ? atomicExch(&S.table[sl], 0u) : 0u;
-        const uint32_t cnt = v & 255u;  // s = cnt / n; s >= thr <=> cnt >= cmin (nGramSearch.hpp:300,315)
-        surv_append(S, v != 0 && cnt >= cmin, min(X.n_short + lo + (v >> 8) - 1u, X.n_terms - 1u), cnt, surv_n);
+        uint32_t sl = kStray;
+#pragma unroll
+        for (uint32_t j = 0; j < 4 * (uint32_t)kDmaRounds; ++j) {
+            const uint32_t x = (j & 3) == 0 ? v[j >> 2].x : (j & 3) == 1 ? v[j >> 2].y : (j & 3) == 2 ? v[j >> 2].z : v[j >> 2].w;
+            sl = j == k ? x : sl;
+        }
+        const uint32_t c = sl != kStray ? atomicExch(&S.table[sl], 0u) : 0u;
+        const uint32_t cnt = c & 255u;  // s = cnt / n; s >= thr <=> cnt >= cmin (nGramSearch.hpp:300,315)
+        surv_append(S, c != 0 && cnt >= cmin, min(X.n_short + lo + (c >> 8) - 1u, X.n_terms - 1u), cnt, surv_n);
     }
     wave_sync();
 }
 
-// Sketch count of the staged part (cmin >= 3): 2 x u16 counters per table word, never an
-// undercount; only postings whose cell reaches cmin are counted exactly (128-slot table).
-// Returns false when more than 64 postings pass (the caller then counts the part exactly).
-__device__ bool part_sketch(WaveSmem& S, const uint32_t* st, uint32_t total, uint32_t cmin, uint32_t n_short,
-                            uint32_t n_terms, uint32_t& surv_n) {
+// Sketch count of a part held in registers (cmin >= 3): 2 x u16 counters per table word,
+// never an undercount. Entries whose cell reaches cmin are candidates; their exact counts
+// come from comparing the <= 64 candidates with each other. Returns false when more than 64
+// entries pass (the caller then counts the part exactly; the table is clean again).
+__device__ __forceinline__ bool part_sketch(WaveSmem& S, const uint4 (&v)[kDmaRounds], uint32_t vmask, uint32_t tch,
+                            uint32_t cmin, uint32_t n_short, uint32_t n_terms, uint32_t& surv_n) {
     const uint32_t lane = lane_id();
-    const uint4* st4 = reinterpret_cast<const uint4*>(st);
-    const uint32_t rounds = (total + 255) >> 8;  // 4 postings per lane per round (b128 reads)
-    for (uint32_t r = 0; r < rounds; ++r) {
-        const uint4 v = st4[(r << 6) + lane];
-        const uint32_t j = (r << 8) + (lane << 2);
-        const uint32_t c0 = sketch_cell(v.x), c1 = sketch_cell(v.y), c2 = sketch_cell(v.z), c3 = sketch_cell(v.w);
-        atomicAdd(&S.table[c0 >> 1], (j + 0 < total && v.x != kStray ? 1u : 0u) << ((c0 & 1u) << 4));
-        atomicAdd(&S.table[c1 >> 1], (j + 1 < total && v.y != kStray ? 1u : 0u) << ((c1 & 1u) << 4));
-        atomicAdd(&S.table[c2 >> 1], (j + 2 < total && v.z != kStray ? 1u : 0u) << ((c2 & 1u) << 4));
-        atomicAdd(&S.table[c3 >> 1], (j + 3 < total && v.w != kStray ? 1u : 0u) << ((c3 & 1u) << 4));
+#pragma unroll
+    for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) {
+        if (64 * r < tch) {
+            const uint32_t t[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
+#pragma unroll
+            for (uint32_t e = 0; e < 4; ++e) {
+                const uint32_t c = sketch_cell(t[e]);
+                atomicAdd(&S.table[c >> 1], ((vmask >> (4 * r + e)) & 1u) << ((c & 1u) << 4));
+            }
+        }
     }
     wave_sync();
     uint32_t nc = 0;
-    for (uint32_t r = 0; r < rounds; ++r) {
-        const uint4 v = st4[(r << 6) + lane];
-        const uint32_t j = (r << 8) + (lane << 2);
-        const uint32_t t[4] = {v.x, v.y, v.z, v.w};
-        uint32_t w[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) w[e] = S.table[sketch_cell(t[e]) >> 1];
+    for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) {
+        if (64 * r < tch) {
+            const uint32_t t[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
+            uint32_t w[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const uint32_t c = sketch_cell(t[e]);
-            const bool pass = j + e < total && t[e] != kStray && ((w[e] >> ((c & 1u) << 4)) & 0xFFFFu) >= cmin;
-            const unsigned long long b = __ballot(pass);
-            const uint32_t idx = nc + __popcll(b & lanes_below());
-            if (pass && idx < 64) S.cbuf[idx] = make_uint2(t[e], 1u);
-            nc += __popcll(b);
+            for (uint32_t e = 0; e < 4; ++e) w[e] = S.table[sketch_cell(t[e]) >> 1];
+#pragma unroll
+            for (uint32_t e = 0; e < 4; ++e) {
+                const uint32_t c = sketch_cell(t[e]);
+                const bool pass = ((vmask >> (4 * r + e)) & 1u) && ((w[e] >> ((c & 1u) << 4)) & 0xFFFFu) >= cmin;
+                const unsigned long long b = __ballot(pass);
+                const uint32_t idx = nc + __popcll(b & lanes_below());
+                if (pass && idx < 64) S.cbuf[idx] = t[e];
+                nc += __popcll(b);
+            }
         }
     }
     wave_sync();
@@ -888,24 +940,18 @@ __device__ bool part_sketch(WaveSmem& S, const uint32_t* st, uint32_t total, uin
     wave_sync();
     if (nc > 64) return false;
     if (nc == 0) return true;
-    // exact counts of the <= 64 candidate postings; the lane that exchanges a slot's count
-    // with 0 first owns the term
-    const bool act = lane < nc;
-    const uint32_t key = act ? S.cbuf[lane].x : 0u;
-    uint32_t h = (key * 0x9E3779B1u) >> 25;
-    if (act) {
-        for (uint32_t probe = 0; probe < 128; ++probe, h = (h + 1) & 127u) {
-            const uint32_t prev = atomicCAS(&S.mkey[h], 0xFFFFFFFFu, key);
-            if (prev == 0xFFFFFFFFu || prev == key) break;
-        }
-        atomicAdd(&S.mcnt[h], 1u);
+    // lane l < nc holds candidate l; its term's exact count is the number of candidates with
+    // that term (every entry of a term lands in the same cell), owned by the first of them
+    const uint32_t t = lane < nc ? S.cbuf[lane] : kStray;
+    uint32_t cnt = 0;
+    bool first = true;
+    for (uint32_t j = 0; j < nc; ++j) {
+        const uint32_t tj = __builtin_amdgcn_readlane(t, j);
+        const bool eq = t == tj;
+        cnt += eq;
+        first &= !(eq && j < lane);
     }
-    wave_sync();
-    const uint32_t acc = act ? atomicExch(&S.mcnt[h], 0u) : 0u;
-    wave_sync();
-    if (act) S.mkey[h] = 0xFFFFFFFFu;
-    wave_sync();
-    surv_append(S, acc != 0 && acc >= cmin, min(n_short + key, n_terms - 1u), acc, surv_n);
+    surv_append(S, lane < nc && first && cnt >= cmin, min(n_short + t, n_terms - 1u), cnt, surv_n);
     return true;
 }
 
@@ -945,10 +991,6 @@ __global__ __launch_bounds__(64) void k_wave(DevIndex X, SearchParams P, const u
     const uint8_t* qg = qnorm + qoff[q];
     for (uint32_t i = lane; i < m; i += 64) S.q[i] = qg[i];
     if (lane == 0) S.surv_total = 0;
-    S.mkey[lane] = 0xFFFFFFFFu;
-    S.mkey[lane + 64] = 0xFFFFFFFFu;
-    S.mcnt[lane] = 0;
-    S.mcnt[lane + 64] = 0;
     {
         uint4* T4 = reinterpret_cast<uint4*>(S.table);
         for (uint32_t i = lane; i < (uint32_t)kWaveSlots / 4; i += 64) T4[i] = make_uint4(0, 0, 0, 0);
@@ -1026,31 +1068,27 @@ __global__ __launch_bounds__(64) void k_wave(DevIndex X, SearchParams P, const u
         const uint32_t a0 = (uint32_t)gbase & 3u;  // list start within its 16-byte chunk
         // entries [s, e) of this lane's list cover 16-byte chunks [(a0 + s) / 4, (a0 + e + 3) / 4)
         auto chunks = [a0](uint32_t s, uint32_t e) -> uint32_t { return e > s ? ((a0 + e + 3) >> 2) - ((a0 + s) >> 2) : 0u; };
-        // part iterator: buckets [bnext, bnext + w) unless they exceed the stage, then term-id sub-parts
+        // part iterator: buckets [bnext, bnext + w) unless they exceed kWaveChunks, then term-id sub-parts
         uint32_t cur = 0, bnext = 0;
         uint32_t e_pre = sk[min(K, w)];  // end of the next bucket part (row 0 for idle lanes)
         bool in_sub = false;
         uint32_t sub_lo = 0, hi_lim = 0, sub_end = 0, sub_bnext = 0, step = 1;
-        // software pipeline over two stage buffers: wait for part i, DMA part i+1, count part i
-        int cb = -1;  // stage buffer holding the part to count (-1: none yet)
-        uint32_t c_lo = 0, c_tot = 0;                  // its term-id base and staged entries (4 per chunk)
-        uint32_t c_p = 0, c_n = 0, c_head = 0, c_tail = 0;  // this lane's segment: first chunk, chunks, strays
+        // software pipeline in registers: part i+1's loads are in flight while part i is counted
+        uint4 pv[kDmaRounds];
+        uint32_t p_vm = 0, p_tch = 0, p_lo = 0;
+        bool have_p = false;
+#pragma unroll
+        for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) pv[r] = make_uint4(0, 0, 0, 0);
         for (uint32_t guard = 0;;) {
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // part cb has landed
-            wave_sync();
-            if (cb >= 0 && c_n) {  // the chunk edges hold up to 3 entries of neighbouring lists
-                uint32_t* st = S.stage + cb * kWaveCap;
-                for (uint32_t j = 0; j < 3; ++j) {
-                    if (j < c_head) st[4 * c_p + j] = kStray;
-                    if (j < c_tail) st[4 * (c_p + c_n) - 1 - j] = kStray;
-                }
-            }
-            wave_sync();
+            uint4 cv[kDmaRounds];
+#pragma unroll
+            for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) cv[r] = pv[r];
+            const uint32_t c_vm = p_vm, c_tch = p_tch, c_lo = p_lo;
+            const bool have_c = have_p;
             WSTAMP(2);
-            const uint32_t nb = cb == 0 ? 1u : 0u;
             // ---- next part: [lo, ...) with per-lane segments [gbase + cur, gbase + cur + len) ----
             uint32_t lo = 0, len = 0;
-            bool have_part = false;
+            have_p = false;
             for (;;) {
                 if (++guard > 8u * K + 4096u) {
                     if (lane == 0) atomicOr(err, 4u);
@@ -1065,7 +1103,7 @@ __global__ __launch_bounds__(64) void k_wave(DevIndex X, SearchParams P, const u
                         len = e - cur;
                         bnext = bhi;
                         e_pre = sk[min(K, bnext + w)];
-                        if (tot) { have_part = true; break; }
+                        if (tot) { have_p = true; break; }
                         continue;
                     }
                     in_sub = true;
@@ -1097,60 +1135,28 @@ __global__ __launch_bounds__(64) void k_wave(DevIndex X, SearchParams P, const u
                     bnext = sub_bnext;
                     e_pre = sk[min(K, bnext + w)];
                 }
-                if (t2) { have_part = true; break; }
+                if (t2) { have_p = true; break; }
                 cur = a;
             }
             WSTAMP(3);
-            // ---- stage part i+1: its lists' 16-byte chunks packed across the wave, <= kDmaRounds DMAs ----
-            uint32_t n_tot = 0, n_p = 0, n_n = 0, n_head = 0, n_tail = 0;
-            if (have_part && (!(P.dbg & 2u) || cb < 0)) {  // dbg 2: stage only the first part
-                const uint32_t nch = chunks(cur, cur + len);
-                const uint32_t incl = wave_incl_scan(nch);
-                const uint32_t pre = incl - nch;
-                const uint32_t tch = __builtin_amdgcn_readlane(incl, 63);
-                const uint32_t cs = (uint32_t)((gbase + cur) >> 2) - pre;  // chunk c of the part <- cs + c
-                uint32_t src[kDmaRounds] = {};
-                for (uint32_t g = 0; g < ng; ++g) {  // the last non-empty segment starting at or before c
-                    if (__builtin_amdgcn_readlane(nch, g) == 0) continue;
-                    const uint32_t sp = __builtin_amdgcn_readlane(pre, g), sb = __builtin_amdgcn_readlane(cs, g);
-#pragma unroll
-                    for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r)
-                        if (64 * r + lane >= sp) src[r] = sb + 64 * r + lane;
-                }
-                const uint32_t d0 = lds_addr(S.stage + nb * kWaveCap);
-#pragma unroll
-                for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) {
-                    if (64 * r < tch && 64 * r + lane < tch) dma_x4(post4 + src[r], d0 + 1024 * r);
-                }
-                n_tot = 4 * tch;
-                n_p = pre;
-                n_n = nch;
-                n_head = (a0 + cur) & 3u;
-                n_tail = (4u - ((a0 + cur + len) & 3u)) & 3u;
-            } else if (have_part) {
-                const uint32_t nch = chunks(cur, cur + len);
-                n_tot = 4 * wave_sum_u32(nch);
+            // ---- part i+1: issue its loads ----
+            if (have_p) {
+                p_tch = stage_part(S, post4, gbase, a0, cur, len, pv, p_vm);
+                p_lo = lo;
+                cur += len;
             }
-            if (have_part) cur += len;
             WSTAMP(4);
             // ---- count part i while part i+1 is in flight ----
-            if (cb >= 0 && !(P.dbg & 1u)) {  // dbg 1: stage only, no counting
-                uint32_t* st = S.stage + cb * kWaveCap;
+            if (have_c && !(P.dbg & 1u)) {  // dbg 1: load only, no counting
                 if (surv_n + 64 > (uint32_t)kWaveSurv)
                     wave_emit(S, X, P, m, L, sc_long, sc_short, surv_n, cand_n, tau);
-                const bool done = sketch && part_sketch(S, st, c_tot, cmin, X.n_short, X.n_terms, surv_n);
+                const bool done = sketch && part_sketch(S, cv, c_vm, c_tch, cmin, X.n_short, X.n_terms, surv_n);
                 WSTAMP(5);
-                if (!done) part_exact(S, st, X, P, m, L, c_lo, c_tot, cmin, sc_long, sc_short, surv_n, cand_n, tau, err);
+                if (!done)
+                    part_exact(S, cv, c_vm, c_tch, X, P, m, L, c_lo, cmin, sc_long, sc_short, surv_n, cand_n, tau, err);
                 WSTAMP(6);
             }
-            if (!have_part) break;
-            cb = (int)nb;
-            c_lo = lo;
-            c_tot = n_tot;
-            c_p = n_p;
-            c_n = n_n;
-            c_head = n_head;
-            c_tail = n_tail;
+            if (!have_p) break;
         }
     }
     WSTAMP(7);
