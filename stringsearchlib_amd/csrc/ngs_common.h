@@ -53,10 +53,11 @@ constexpr int kWaveCap = kWaveSlots / 2;        // postings per part (<= 50 % lo
 constexpr int kWaveCand = 256;                  // candidate buffer per query
 constexpr uint32_t kWaveMaxLimit = kWaveCand / 2;
 constexpr int kWaveChunks = kWaveCap / 4;       // 16-byte chunks per stage buffer
-constexpr int kDmaRounds = kWaveChunks / 64;    // dwordx4 LDS-DMAs to fill one
+constexpr int kDmaRounds = kWaveChunks / 64;    // dwordx4 loads per lane for one part
+constexpr int kWaveWavesPerSimd = 4;            // occupancy target: <= 128 VGPRs
 constexpr int kWaveTarget = kWaveCap * 5 / 8;   // postings per part the bucket grouping aims at
 constexpr uint32_t kStray = 0xFFFFFFFFu;        // staged entry outside its list segment
-constexpr int kWaveSurv = 320;                  // survivor list (term, count) before calcScore
+constexpr int kWaveSurv = 128;                  // survivor list (term, count) before calcScore
 constexpr uint32_t kWaveMaxGrams = 63;          // counts <= 63: one lane per count value
 
 struct DevIndex {  // passed by value to kernels; all pointers are device pointers

@@ -624,7 +624,7 @@ struct alignas(16) WaveSmem {
     uint32_t table[kWaveSlots];    // exact: (term - lo + 1) << 8 | count; sketch: 2 x u16 counters
     uint64_t cand[kWaveCand];      // (~enc) << 32 | key
     uint4 segtab[64];              // staging: per list {first chunk - position, first entry, end entry, -}
-    uint32_t mark[kWaveChunks];    // staging: list index + 1 at the position of its first chunk
+    uint8_t mark[kWaveChunks];     // staging: list index + 1 at the position of its first chunk
     uint32_t surv_t[kWaveSurv];    // survivor terms
     uint32_t cbuf[64];             // sketch candidates (terms)
     uint8_t surv_c[kWaveSurv];     // hit count, | 0x80 for a Levenshtein (short search) match count
@@ -955,7 +955,7 @@ __device__ __forceinline__ bool part_sketch(WaveSmem& S, const uint4 (&v)[kDmaRo
     return true;
 }
 
-__global__ __launch_bounds__(64) void k_wave(DevIndex X, SearchParams P, const uint8_t* __restrict__ qnorm,
+__global__ __launch_bounds__(64, kWaveWavesPerSimd) void k_wave(DevIndex X, SearchParams P, const uint8_t* __restrict__ qnorm,
                                              const uint64_t* __restrict__ qoff, const uint32_t* __restrict__ qm,
                                              uint32_t* __restrict__ out_n, uint32_t* __restrict__ out_k,
                                              float* __restrict__ out_s, uint32_t* __restrict__ list2,
