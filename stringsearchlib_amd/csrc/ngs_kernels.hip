@@ -33,7 +33,9 @@ __device__ unsigned long long g_phase[32];
         wacc_[i] += t_ - wt_;                                             \
         wt_ = t_;                                                         \
     }
+#define WCOUNT(i, v) wacc_[i] += (v)
 #else
+#define WCOUNT(i, v)
 #define STAMP(i)
 #define WSTAMP(i)
 #endif
@@ -635,6 +637,10 @@ struct alignas(16) WaveSmem {
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
 
 __device__ __forceinline__ unsigned long long lanes_below() { return (1ull << lane_id()) - 1ull; }
+// popcount of the ballot bits of the lanes below this one (v_mbcnt_lo/hi)
+__device__ __forceinline__ uint32_t rank_below(unsigned long long b) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+}
 
 // Ordering point for the wave-private LDS. A wave's LDS instructions execute in order, so
 // no barrier and no wait is needed: only keep the compiler from moving LDS accesses across.
@@ -772,7 +778,7 @@ __device__ void wave_emit(WaveSmem& S, const DevIndex& X, const SearchParams& P,
             if (cand_n + 64 > (uint32_t)kWaveCand) wave_flush(S, cand_n, tau, L);
             const bool want = rec < tau;
             const unsigned long long b = __ballot(want);
-            if (want) S.cand[cand_n + __popcll(b & lanes_below())] = rec;
+            if (want) S.cand[cand_n + rank_below(b)] = rec;
             cand_n += __popcll(b);
         }
     }
@@ -783,7 +789,7 @@ __device__ void wave_emit(WaveSmem& S, const DevIndex& X, const SearchParams& P,
 __device__ __forceinline__ void surv_append(WaveSmem& S, bool pass, uint32_t t, uint32_t code, uint32_t& surv_n) {
     const unsigned long long b = __ballot(pass);
     if (pass) {
-        const uint32_t i = surv_n + __popcll(b & lanes_below());
+        const uint32_t i = surv_n + rank_below(b);
         S.surv_t[i] = t;
         S.surv_c[i] = (uint8_t)code;
     }
@@ -813,7 +819,9 @@ __device__ __forceinline__ uint32_t wave_insert_slot(uint32_t* T, uint32_t rel, 
     }
 }
 
-__device__ __forceinline__ uint32_t sketch_cell(uint32_t t) { return (t * 0x9E3779B1u) >> (32 - kWaveSlotBits - 1); }
+// sketch cell of a term: full-rate shift/xor (v_mul_lo_u32 is quarter rate). Term ids of a part
+// are spread over a range much wider than the table, and consecutive ids get distinct cells.
+__device__ __forceinline__ uint32_t sketch_cell(uint32_t t) { return (t ^ (t >> (kWaveSlotBits + 1))) & (2u * kWaveSlots - 1u); }
 
 // Loads one part into registers: lane g < ng contributes entries [cur, cur + len) of its list
 // (list base gbase, a0 = gbase % 4). The lists' 16-byte chunks are packed across the wave,
@@ -852,10 +860,11 @@ __device__ __forceinline__ uint32_t stage_part(WaveSmem& S, const uint4* __restr
             carry = __builtin_amdgcn_readlane(sc, 63);
             const uint4 seg = S.segtab[(sc - 1u) & 63u];
             v[r] = post4[ok ? seg.x + c : 0u];
-            uint32_t bits = 0;
-#pragma unroll
-            for (uint32_t e = 0; e < 4; ++e) bits |= (ok && 4 * c + e >= seg.y && 4 * c + e < seg.z ? 1u : 0u) << e;
-            vmask |= bits << (4 * r);
+            // entries [lo_e, hi_e) of this chunk are in the list segment [seg.y, seg.z)
+            const uint32_t lo_e = (uint32_t)min(max((int)seg.y - (int)(4 * c), 0), 4);
+            const uint32_t hi_e = (uint32_t)min(max((int)seg.z - (int)(4 * c), 0), 4);
+            const uint32_t bits = ((1u << hi_e) - 1u) & ~((1u << lo_e) - 1u);
+            vmask |= (ok ? bits : 0u) << (4 * r);
         }
     }
     return tch;
@@ -896,9 +905,9 @@ __device__ __forceinline__ void part_exact(WaveSmem& S, uint4 (&v)[kDmaRounds], 
 
 // Sketch count of a part held in registers (cmin >= 3): 2 x u16 counters per table word,
 // never an undercount. Entries whose cell reaches cmin are candidates; their exact counts
-// come from comparing the <= 64 candidates with each other. Returns false when more than 64
-// entries pass (the caller then counts the part exactly; the table is clean again).
-__device__ __forceinline__ bool part_sketch(WaveSmem& S, const uint4 (&v)[kDmaRounds], uint32_t vmask, uint32_t tch,
+// come from comparing the <= 64 candidates with each other. Returns the number of candidate
+// entries; above 64 the caller counts the part exactly (the table is clean again).
+__device__ __forceinline__ uint32_t part_sketch(WaveSmem& S, const uint4 (&v)[kDmaRounds], uint32_t vmask, uint32_t tch,
                             uint32_t cmin, uint32_t n_short, uint32_t n_terms, uint32_t& surv_n) {
     const uint32_t lane = lane_id();
 #pragma unroll
@@ -913,7 +922,9 @@ __device__ __forceinline__ bool part_sketch(WaveSmem& S, const uint4 (&v)[kDmaRo
         }
     }
     wave_sync();
-    uint32_t nc = 0;
+    // candidates are rare (~10 of ~600 entries): flag them in a per-lane mask, then write them
+    // at offsets from one prefix sum instead of compacting every entry slot by ballot
+    uint32_t cm = 0;
 #pragma unroll
     for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) {
         if (64 * r < tch) {
@@ -924,11 +935,23 @@ __device__ __forceinline__ bool part_sketch(WaveSmem& S, const uint4 (&v)[kDmaRo
 #pragma unroll
             for (uint32_t e = 0; e < 4; ++e) {
                 const uint32_t c = sketch_cell(t[e]);
-                const bool pass = ((vmask >> (4 * r + e)) & 1u) && ((w[e] >> ((c & 1u) << 4)) & 0xFFFFu) >= cmin;
-                const unsigned long long b = __ballot(pass);
-                const uint32_t idx = nc + __popcll(b & lanes_below());
-                if (pass && idx < 64) S.cbuf[idx] = t[e];
-                nc += __popcll(b);
+                cm |= (((w[e] >> ((c & 1u) << 4)) & 0xFFFFu) >= cmin ? 1u : 0u) << (4 * r + e);
+            }
+        }
+    }
+    cm &= vmask;
+    const uint32_t mine = __popc(cm);
+    const uint32_t incl = wave_incl_scan(mine);
+    const uint32_t nc = __builtin_amdgcn_readlane(incl, 63);
+    if (nc <= 64 && __ballot(cm != 0)) {
+        uint32_t pos = incl - mine;
+#pragma unroll
+        for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) {
+            if (64 * r < tch) {
+                const uint32_t t[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
+#pragma unroll
+                for (uint32_t e = 0; e < 4; ++e)
+                    if ((cm >> (4 * r + e)) & 1u) S.cbuf[pos++] = t[e];
             }
         }
     }
@@ -938,8 +961,7 @@ __device__ __forceinline__ bool part_sketch(WaveSmem& S, const uint4 (&v)[kDmaRo
         for (uint32_t i = lane; i < (uint32_t)kWaveSlots / 4; i += 64) T4[i] = make_uint4(0, 0, 0, 0);
     }
     wave_sync();
-    if (nc > 64) return false;
-    if (nc == 0) return true;
+    if (nc > 64 || nc == 0) return nc;
     // lane l < nc holds candidate l; its term's exact count is the number of candidates with
     // that term (every entry of a term lands in the same cell), owned by the first of them
     const uint32_t t = lane < nc ? S.cbuf[lane] : kStray;
@@ -952,7 +974,7 @@ __device__ __forceinline__ bool part_sketch(WaveSmem& S, const uint4 (&v)[kDmaRo
         first &= !(eq && j < lane);
     }
     surv_append(S, lane < nc && first && cnt >= cmin, min(n_short + t, n_terms - 1u), cnt, surv_n);
-    return true;
+    return nc;
 }
 
 __global__ __launch_bounds__(64, kWaveWavesPerSimd) void k_wave(DevIndex X, SearchParams P, const uint8_t* __restrict__ qnorm,
@@ -986,7 +1008,7 @@ __global__ __launch_bounds__(64, kWaveWavesPerSimd) void k_wave(DevIndex X, Sear
     const uint32_t n_long = X.n_terms - X.n_short;
 #ifdef NGS_PHASE_STAMPS
     unsigned long long wt_ = __builtin_amdgcn_s_memtime();
-    unsigned long long wacc_[11] = {};
+    unsigned long long wacc_[16] = {};
 #endif
     const uint8_t* qg = qnorm + qoff[q];
     for (uint32_t i = lane; i < m; i += 64) S.q[i] = qg[i];
@@ -1150,7 +1172,12 @@ __global__ __launch_bounds__(64, kWaveWavesPerSimd) void k_wave(DevIndex X, Sear
             if (have_c && !(P.dbg & 1u)) {  // dbg 1: load only, no counting
                 if (surv_n + 64 > (uint32_t)kWaveSurv)
                     wave_emit(S, X, P, m, L, sc_long, sc_short, surv_n, cand_n, tau);
-                const bool done = sketch && part_sketch(S, cv, c_vm, c_tch, cmin, X.n_short, X.n_terms, surv_n);
+                const uint32_t nc = sketch ? part_sketch(S, cv, c_vm, c_tch, cmin, X.n_short, X.n_terms, surv_n) : 65u;
+                const bool done = nc <= 64;
+                WCOUNT(11, 1);
+                WCOUNT(12, done ? 0 : 1);
+                WCOUNT(13, sketch ? nc : 0);
+                WCOUNT(14, c_tch);
                 WSTAMP(5);
                 if (!done)
                     part_exact(S, cv, c_vm, c_tch, X, P, m, L, c_lo, cmin, sc_long, sc_short, surv_n, cand_n, tau, err);
@@ -1181,7 +1208,7 @@ __global__ __launch_bounds__(64, kWaveWavesPerSimd) void k_wave(DevIndex X, Sear
     WSTAMP(10);
 #ifdef NGS_PHASE_STAMPS
     if (lane == 0)
-        for (int i = 0; i < 11; ++i) atomicAdd(&g_phase[16 + i], wacc_[i]);
+        for (int i = 0; i < 16; ++i) atomicAdd(&g_phase[16 + i], wacc_[i]);
 #endif
 }
 

@@ -40,6 +40,8 @@ def main():
     print(f"k_wave: per-query wave time {wt/B:.0f} cycles")
     for i, nm in enumerate(wn):
         print(f"  {nm:10s} {out[16+i]/B:9.0f} cyc/query  {100*out[16+i]/max(wt,1):5.1f} %")
+    print(f"  parts/query {out[27]/B:.1f}  exact parts/query {out[28]/B:.2f}  sketch candidates/part "
+          f"{out[29]/max(1, out[27]):.1f}  chunks/part {out[30]/max(1, out[27]):.1f}")
     tot = sum(out[i] for i in range(12))
     print(f"rows={rows} B={B} thr={thr} wall={dt*1e3:.1f} ms; per-query block time {tot/B/100:.2f} us")
     for i, nm in enumerate(NAMES):
