@@ -261,6 +261,12 @@ int device_search(Library& L, Context& c, const uint8_t* d_raw, const uint64_t* 
         return e ? (uint32_t)std::strtoul(e, nullptr, 0) : 0u;
     }();
     P.dbg = dbg;
+    static const uint32_t waves = [] {  // experiment override of the tier-1 waves per query
+        const char* e = std::getenv("NGS_WAVES");
+        const uint32_t w = e ? (uint32_t)std::strtoul(e, nullptr, 0) : kDefaultWaves;
+        return w == 1 || w == 2 || w == 4 ? w : kDefaultWaves;
+    }();
+    P.waves = waves;
     {
         std::lock_guard<std::mutex> g(L.valid_mu);
         std::memcpy(P.valid, L.valid, sizeof(P.valid));

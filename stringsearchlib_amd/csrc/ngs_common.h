@@ -55,6 +55,7 @@ constexpr uint32_t kWaveMaxLimit = kWaveCand / 2;
 constexpr int kWaveChunks = kWaveCap / 4;       // 16-byte chunks per stage buffer
 constexpr int kDmaRounds = kWaveChunks / 64;    // dwordx4 loads per lane for one part
 constexpr int kWaveWavesPerSimd = 4;            // occupancy target: <= 128 VGPRs
+constexpr uint32_t kDefaultWaves = 1;           // waves per query in the tier-1 kernel
 constexpr int kWaveTarget = kWaveCap * 5 / 8;   // postings per part the bucket grouping aims at
 constexpr uint32_t kStray = 0xFFFFFFFFu;        // staged entry outside its list segment
 constexpr int kWaveSurv = 128;                  // survivor list (term, count) before calcScore
@@ -84,6 +85,7 @@ struct SearchParams {
     uint32_t n_queries;
     uint32_t valid[8];   // 256-bit validChar mask (h:307-313 / setValidChar)
     uint32_t dbg;        // ablation switches for performance experiments (NGS_DEBUG); 0 in production
+    uint32_t waves;      // waves per query in the tier-1 kernel: 1, 2 or 4 (kDefaultWaves; NGS_WAVES)
 };
 
 // per-query normalised length sentinels written by the prep kernel

@@ -616,22 +616,29 @@ __global__ __launch_bounds__(kFastThreads) void k_fast(DevIndex X, SearchParams 
 }
 
 // ---------------------------------------------------------------- wave kernel --------
-// Tier 1: ONE WAVE PER QUERY, wave-private LDS (no block barriers). A query's gram lists are
-// cut into term-id parts of <= kWaveChunks 16-byte chunks (bucket skip table; a bucket above
-// the cap is split by lower_bound). A part is loaded into registers, its lists' chunks packed
-// across the wave, while the previous part is counted against an LDS sketch / hash table
-// with predication only. A repeated query gram is kept as a separate occurrence (its list is
-// read once per occurrence), which is the reference's multiplicity (hpp:289-298).
+// Tier 1: W WAVES PER QUERY (W = 1, 2 or 4) sharing one LDS table of W x 8 KB. A query's gram
+// lists are cut into term-id parts of <= W x kWaveChunks 16-byte chunks (bucket skip table; a
+// bucket above the cap is split by lower_bound). Every wave plans the same parts (redundantly,
+// no synchronisation); wave w loads chunks [w, w+1) x kWaveChunks of each part into registers,
+// the lists' chunks packed across the wave, while the previous part is counted against the
+// shared LDS sketch / hash table with predication only. Block barriers wait for LDS only, so
+// the next part's loads stay in flight. Candidate resolution, survivors and the top-L run on
+// wave 0. A repeated query gram is kept as a separate occurrence (its list is read once per
+// occurrence), which is the reference's multiplicity (hpp:289-298).
+template <int W>
 struct alignas(16) WaveSmem {
-    uint32_t table[kWaveSlots];    // exact: (term - lo + 1) << 8 | count; sketch: 2 x u16 counters
-    uint64_t cand[kWaveCand];      // (~enc) << 32 | key
-    uint4 segtab[64];              // staging: per list {first chunk - position, first entry, end entry, -}
-    uint8_t mark[kWaveChunks];     // staging: list index + 1 at the position of its first chunk
-    uint32_t surv_t[kWaveSurv];    // survivor terms
-    uint32_t cbuf[64];             // sketch candidates (terms)
-    uint8_t surv_c[kWaveSurv];     // hit count, | 0x80 for a Levenshtein (short search) match count
+    uint32_t table[kWaveSlots * W];  // exact: (term - lo + 1) << 8 | count; sketch: 2 x u16 counters
+    uint64_t cand[kWaveCand];        // (~enc) << 32 | key
+    uint2 segtab[W][64];             // staging, per wave: per list {first chunk - position, first | end entry << 16}
+    uint8_t mark[W][kWaveChunks];    // staging, per wave: list index + 1 at the (wave-local) position of its first chunk
+    uint32_t surv_t[kWaveSurv];      // survivor terms
+    uint32_t cbuf[64];               // sketch candidates (terms)
+    uint8_t surv_c[kWaveSurv];       // hit count, | 0x80 for a Levenshtein (short search) match count
     uint8_t q[kWaveMaxGrams + 8];
-    uint32_t surv_total;           // stats
+    uint32_t surv_total;             // stats
+    uint32_t ncand;                  // sketch candidates of the part, all waves
+    uint32_t x_surv_n, x_cand_n;     // wave 0's emit state, handed round in exact-path turns
+    uint64_t x_tau;
 };
 
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
@@ -648,6 +655,18 @@ __device__ __forceinline__ uint32_t rank_below(unsigned long long b) {
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
+}
+
+// Ordering point for LDS shared by the block's W waves: this wave's LDS operations complete,
+// then a raw s_barrier. Global loads in flight are NOT drained (no vmcnt wait), unlike
+// __syncthreads().
+template <int W>
+__device__ __forceinline__ void grp_sync() {
+    if constexpr (W == 1) {
+        wave_sync();
+    } else {
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
 }
 
 template <class T>
@@ -702,7 +721,8 @@ __device__ __forceinline__ uint32_t wave_incl_max_scan(uint32_t v) {
 }
 
 // Wave-local running top-L over the candidate buffer (same algorithm as flush()).
-__device__ void wave_flush(WaveSmem& S, uint32_t& cand_n, uint64_t& tau, uint32_t L) {
+template <int W>
+__device__ void wave_flush(WaveSmem<W>& S, uint32_t& cand_n, uint64_t& tau, uint32_t L) {
     const uint32_t lane = lane_id();
     const uint32_t n = min(cand_n, (uint32_t)kWaveCand);
     const uint32_t P2 = next_pow2(max(n, 2u));
@@ -751,7 +771,8 @@ __device__ void wave_flush(WaveSmem& S, uint32_t& cand_n, uint64_t& tau, uint32_
 
 // calcScore (nGramSearch.hpp:310-341) over the survivor list: term -> (key, weight) pairs,
 // max(w*s, 0), exact-match promotion, into the running top-L.
-__device__ void wave_emit(WaveSmem& S, const DevIndex& X, const SearchParams& P, uint32_t m, uint32_t L,
+template <int W>
+__device__ void wave_emit(WaveSmem<W>& S, const DevIndex& X, const SearchParams& P, uint32_t m, uint32_t L,
                           float sc_long, float sc_short, uint32_t& surv_n, uint32_t& cand_n, uint64_t& tau) {
     const uint32_t lane = lane_id();
     S.surv_total += surv_n;
@@ -786,7 +807,8 @@ __device__ void wave_emit(WaveSmem& S, const DevIndex& X, const SearchParams& P,
     wave_sync();
 }
 
-__device__ __forceinline__ void surv_append(WaveSmem& S, bool pass, uint32_t t, uint32_t code, uint32_t& surv_n) {
+template <int W>
+__device__ __forceinline__ void surv_append(WaveSmem<W>& S, bool pass, uint32_t t, uint32_t code, uint32_t& surv_n) {
     const unsigned long long b = __ballot(pass);
     if (pass) {
         const uint32_t i = surv_n + rank_below(b);
@@ -796,9 +818,11 @@ __device__ __forceinline__ void surv_append(WaveSmem& S, bool pass, uint32_t t, 
     surv_n += __popcll(b);
 }
 
+template <int W>
 __device__ __forceinline__ uint32_t wave_insert_slot(uint32_t* T, uint32_t rel, unsigned* err) {
+    constexpr uint32_t kSlots = kWaveSlots * W;
     uint32_t probes = 0;
-    uint32_t h = (rel * 0x9E3779B1u) >> (32 - kWaveSlotBits);
+    uint32_t h = (rel * 0x9E3779B1u) >> (32 - kWaveSlotBits - (W == 4 ? 2 : W == 2 ? 1 : 0));
     const uint32_t want = rel << 8;
     for (;;) {
         uint32_t cur = T[h];
@@ -811,8 +835,8 @@ __device__ __forceinline__ uint32_t wave_insert_slot(uint32_t* T, uint32_t rel, 
             atomicAdd(&T[h], 1u);
             return h;
         }
-        h = (h + 1) & (kWaveSlots - 1);
-        if (++probes > (uint32_t)kWaveSlots) {
+        h = (h + 1) & (kSlots - 1);
+        if (++probes > kSlots) {
             atomicOr(err, 1u);
             return h;
         }
@@ -821,120 +845,181 @@ __device__ __forceinline__ uint32_t wave_insert_slot(uint32_t* T, uint32_t rel, 
 
 // sketch cell of a term: full-rate shift/xor (v_mul_lo_u32 is quarter rate). Term ids of a part
 // are spread over a range much wider than the table, and consecutive ids get distinct cells.
-__device__ __forceinline__ uint32_t sketch_cell(uint32_t t) { return (t ^ (t >> (kWaveSlotBits + 1))) & (2u * kWaveSlots - 1u); }
+template <int W>
+__device__ __forceinline__ uint32_t sketch_cell(uint32_t t) {
+    constexpr uint32_t kBits = kWaveSlotBits + 1 + (W == 4 ? 2 : W == 2 ? 1 : 0);
+    return (t ^ (t >> kBits)) & ((1u << kBits) - 1u);
+}
 
-// Loads one part into registers: lane g < ng contributes entries [cur, cur + len) of its list
-// (list base gbase, a0 = gbase % 4). The lists' 16-byte chunks are packed across the wave,
-// lane l holding chunks l, 64 + l, ... in v[0], v[1], ...: about one load instruction per
-// 256 postings, whatever the number of lists (MI355X issues scattered loads at a fixed
-// rate per instruction). A chunk finds its list through a marker per list
-// start and a max-scan; vmask bit 4r+e says whether entry e of v[r] belongs to the part
-// (chunk edges hold up to 3 entries of the neighbouring lists). Returns the chunk count.
-__device__ __forceinline__ uint32_t stage_part(WaveSmem& S, const uint4* __restrict__ post4, uint64_t gbase,
+// Loads this wave's share of one part into registers. Lane g < ng contributes entries
+// [cur, cur + len) of its list (list base gbase, a0 = gbase % 4); the part's 16-byte chunks are
+// numbered across all lists (DPP prefix sum) and wave w takes chunks [w, w+1) x kWaveChunks,
+// lane l holding chunks l, 64 + l, ... of that range in v[0], v[1], ...: about one load
+// instruction per 256 postings whatever the number of lists (MI355X issues scattered loads at
+// a fixed rate per instruction). A chunk finds its list through a marker per list
+// start plus a max-scan; vmask bit 4r+e says whether entry e of v[r] belongs to the part (chunk
+// edges hold up to 3 entries of neighbouring lists). Returns this wave's chunk count; *tch_all
+// receives the part's.
+template <int W>
+__device__ __forceinline__ uint32_t stage_part(WaveSmem<W>& S, const uint4* __restrict__ post4, uint64_t gbase,
                                                uint32_t a0, uint32_t cur, uint32_t len,
                                                uint4 (&v)[kDmaRounds], uint32_t& vmask) {
-    const uint32_t lane = lane_id();
+    const uint32_t lane = lane_id(), wid = W == 1 ? 0u : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t head = (a0 + cur) & 3u;
     const uint32_t nch = len ? (head + len + 3) >> 2 : 0u;
     const uint32_t incl = wave_incl_scan(nch);
     const uint32_t pre = incl - nch;
     const uint32_t tch = __builtin_amdgcn_readlane(incl, 63);
+    const uint32_t c0 = wid * kWaveChunks;  // this wave's first chunk of the part
+    const uint32_t mt = __builtin_amdgcn_readfirstlane(tch > c0 ? min(tch - c0, (uint32_t)kWaveChunks) : 0u);
+    uint8_t* mk = S.mark[wid];
 #pragma unroll
     for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r)
-        if (64 * r < tch) S.mark[64 * r + lane] = 0;
+        if (64 * r < mt) mk[64 * r + lane] = 0;
     wave_sync();
     if (nch) {
-        S.mark[pre] = lane + 1;
+        if (pre >= c0 && pre < c0 + kWaveChunks) mk[pre - c0] = (uint8_t)(lane + 1);
         const uint32_t first = (uint32_t)((gbase + cur) >> 2);
-        S.segtab[lane] = make_uint4(first - pre, 4 * pre + head, 4 * pre + head + len, 0);
+        S.segtab[wid][lane] = make_uint2(first - pre, (4 * pre + head) | ((4 * pre + head + len) << 16));
     }
     wave_sync();
-    uint32_t carry = 0;
+    // the list holding this wave's first chunk may start in an earlier wave's range
+    const unsigned long long before = __ballot(nch != 0 && pre < c0);
+    uint32_t carry = before ? 64u - (uint32_t)__clzll(before) : 0u;
     vmask = 0;
 #pragma unroll
     for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) {
-        if (64 * r < tch) {
-            const uint32_t c = 64 * r + lane;
-            const bool ok = c < tch;
-            const uint32_t sc = max(wave_incl_max_scan(ok ? S.mark[c] : 0u), carry);
+        if (64 * r < mt) {
+            const uint32_t lc = 64 * r + lane, c = c0 + lc;
+            const bool ok = lc < mt;
+            const uint32_t sc = max(wave_incl_max_scan(ok ? (uint32_t)mk[lc] : 0u), carry);
             carry = __builtin_amdgcn_readlane(sc, 63);
-            const uint4 seg = S.segtab[(sc - 1u) & 63u];
+            const uint2 seg = S.segtab[wid][(sc - 1u) & 63u];
             v[r] = post4[ok ? seg.x + c : 0u];
-            // entries [lo_e, hi_e) of this chunk are in the list segment [seg.y, seg.z)
-            const uint32_t lo_e = (uint32_t)min(max((int)seg.y - (int)(4 * c), 0), 4);
-            const uint32_t hi_e = (uint32_t)min(max((int)seg.z - (int)(4 * c), 0), 4);
+            // entries [lo_e, hi_e) of this chunk are in the list segment [y, z)
+            const int y = (int)(seg.y & 0xFFFFu), z = (int)(seg.y >> 16);
+            const uint32_t lo_e = (uint32_t)min(max(y - (int)(4 * c), 0), 4);
+            const uint32_t hi_e = (uint32_t)min(max(z - (int)(4 * c), 0), 4);
             const uint32_t bits = ((1u << hi_e) - 1u) & ~((1u << lo_e) - 1u);
             vmask |= (ok ? bits : 0u) << (4 * r);
         }
     }
-    return tch;
+    return mt;
 }
 
-// Exact count of a part held in registers: LDS hash table term -> count. Each entry's slot
-// replaces its term in the registers; the extraction exchanges the slot with 0, so the first
-// holder of a term owns its count (no table scan; the table ends empty).
-__device__ __forceinline__ void part_exact(WaveSmem& S, uint4 (&v)[kDmaRounds], uint32_t vmask, uint32_t tch, const DevIndex& X,
-                           const SearchParams& P, uint32_t m, uint32_t L, uint32_t lo, uint32_t cmin, float sc_long,
-                           float sc_short, uint32_t& surv_n, uint32_t& cand_n, uint64_t& tau, unsigned* err) {
+// Exact count of a part held in registers (all waves): shared LDS hash table term -> count.
+// Each entry's slot replaces its term in the registers; the extraction exchanges the slot with
+// 0, so the first holder of a term owns its count (no table scan; the table ends empty). With
+// W > 1 the waves extract in turns, handing wave 0's survivor / top-L state round in LDS.
+template <int W>
+__device__ __forceinline__ void part_exact(WaveSmem<W>& S, uint4 (&v)[kDmaRounds], uint32_t vmask, uint32_t mt,
+                                           const DevIndex& X, const SearchParams& P, uint32_t m, uint32_t L,
+                                           uint32_t lo, uint32_t cmin, float sc_long, float sc_short,
+                                           uint32_t& surv_n, uint32_t& cand_n, uint64_t& tau, unsigned* err) {
+    const uint32_t lane = lane_id(), wid = W == 1 ? 0u : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    mt = __builtin_amdgcn_readfirstlane(mt);
 #pragma unroll
     for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) {
-        if (64 * r < tch) {
+        if (64 * r < mt) {
 #pragma unroll
             for (uint32_t e = 0; e < 4; ++e) {
                 uint32_t& x = e == 0 ? v[r].x : e == 1 ? v[r].y : e == 2 ? v[r].z : v[r].w;
-                x = (vmask >> (4 * r + e)) & 1u ? wave_insert_slot(S.table, x - lo + 1u, err) : kStray;
+                x = (vmask >> (4 * r + e)) & 1u ? wave_insert_slot<W>(S.table, x - lo + 1u, err) : kStray;
             }
         }
     }
-    wave_sync();
-    // one element slot per step (a single wave_emit call site keeps the registers out of scratch)
-    for (uint32_t k = 0; k < 4 * (uint32_t)kDmaRounds && 64 * (k >> 2) < tch; ++k) {
-        if (surv_n + 64 > (uint32_t)kWaveSurv) wave_emit(S, X, P, m, L, sc_long, sc_short, surv_n, cand_n, tau);
-        uint32_t sl = kStray;
-#pragma unroll
-        for (uint32_t j = 0; j < 4 * (uint32_t)kDmaRounds; ++j) {
-            const uint32_t x = (j & 3) == 0 ? v[j >> 2].x : (j & 3) == 1 ? v[j >> 2].y : (j & 3) == 2 ? v[j >> 2].z : v[j >> 2].w;
-            sl = j == k ? x : sl;
+    grp_sync<W>();
+    if constexpr (W > 1) {
+        if (wid == 0 && lane == 0) {
+            S.x_surv_n = surv_n;
+            S.x_cand_n = cand_n;
+            S.x_tau = tau;
         }
-        const uint32_t c = sl != kStray ? atomicExch(&S.table[sl], 0u) : 0u;
-        const uint32_t cnt = c & 255u;  // s = cnt / n; s >= thr <=> cnt >= cmin (nGramSearch.hpp:300,315)
-        surv_append(S, c != 0 && cnt >= cmin, min(X.n_short + lo + (c >> 8) - 1u, X.n_terms - 1u), cnt, surv_n);
+        grp_sync<W>();
     }
-    wave_sync();
+    for (uint32_t turn = 0; turn < (uint32_t)W; ++turn) {
+        if (wid == turn) {
+            uint32_t sn = W == 1 ? surv_n : S.x_surv_n, cn = W == 1 ? cand_n : S.x_cand_n;
+            uint64_t ta = W == 1 ? tau : S.x_tau;
+            // one element slot per step (a single wave_emit call site keeps the registers out of scratch)
+            for (uint32_t k = 0; k < 4 * (uint32_t)kDmaRounds && 64 * (k >> 2) < mt; ++k) {
+                if (sn + 64 > (uint32_t)kWaveSurv) wave_emit(S, X, P, m, L, sc_long, sc_short, sn, cn, ta);
+                uint32_t sl = kStray;
+#pragma unroll
+                for (uint32_t j = 0; j < 4 * (uint32_t)kDmaRounds; ++j) {
+                    const uint32_t x = (j & 3) == 0 ? v[j >> 2].x : (j & 3) == 1 ? v[j >> 2].y : (j & 3) == 2 ? v[j >> 2].z : v[j >> 2].w;
+                    sl = j == k ? x : sl;
+                }
+                const uint32_t c = sl != kStray ? atomicExch(&S.table[sl], 0u) : 0u;
+                const uint32_t cnt = c & 255u;  // s = cnt / n; s >= thr <=> cnt >= cmin (nGramSearch.hpp:300,315)
+                surv_append(S, c != 0 && cnt >= cmin, min(X.n_short + lo + (c >> 8) - 1u, X.n_terms - 1u), cnt, sn);
+            }
+            if constexpr (W == 1) {
+                surv_n = sn;
+                cand_n = cn;
+                tau = ta;
+            } else {
+                wave_sync();
+                if (lane == 0) {
+                    S.x_surv_n = sn;
+                    S.x_cand_n = cn;
+                    S.x_tau = ta;
+                }
+            }
+        }
+        grp_sync<W>();
+    }
+    if constexpr (W > 1) {
+        if (wid == 0) {  // only wave 0 keeps survivor / top-L state
+            surv_n = S.x_surv_n;
+            cand_n = S.x_cand_n;
+            tau = S.x_tau;
+        }
+        grp_sync<W>();
+    }
 }
 
-// Sketch count of a part held in registers (cmin >= 3): 2 x u16 counters per table word,
-// never an undercount. Entries whose cell reaches cmin are candidates; their exact counts
-// come from comparing the <= 64 candidates with each other. Returns the number of candidate
-// entries; above 64 the caller counts the part exactly (the table is clean again).
-__device__ __forceinline__ uint32_t part_sketch(WaveSmem& S, const uint4 (&v)[kDmaRounds], uint32_t vmask, uint32_t tch,
-                            uint32_t cmin, uint32_t n_short, uint32_t n_terms, uint32_t& surv_n) {
-    const uint32_t lane = lane_id();
+// Sketch count of a part held in registers (cmin >= 3; all waves): 2 x u16 counters per shared
+// table word, never an undercount. Entries whose cell reaches cmin are candidates; wave 0 gets
+// their exact counts by comparing the <= 64 candidates with each other. Returns the number of
+// candidate entries; above 64 the caller counts the part exactly (the table is clean again).
+template <int W>
+__device__ __forceinline__ uint32_t part_sketch(WaveSmem<W>& S, const uint4 (&v)[kDmaRounds], uint32_t vmask,
+                                                uint32_t mt, uint32_t cmin, uint32_t n_short, uint32_t n_terms,
+                                                uint32_t& surv_n, uint32_t dbg) {
+    const uint32_t lane = lane_id(), wid = W == 1 ? 0u : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    mt = __builtin_amdgcn_readfirstlane(mt);
 #pragma unroll
     for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) {
-        if (64 * r < tch) {
+        if (64 * r < mt) {
             const uint32_t t[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
 #pragma unroll
             for (uint32_t e = 0; e < 4; ++e) {
-                const uint32_t c = sketch_cell(t[e]);
+                const uint32_t c = sketch_cell<W>(t[e]);
                 atomicAdd(&S.table[c >> 1], ((vmask >> (4 * r + e)) & 1u) << ((c & 1u) << 4));
             }
         }
     }
-    wave_sync();
+    grp_sync<W>();
+    if (dbg & 2u) {  // ablation: add pass only (table cleared, no candidates)
+        uint4* T4 = reinterpret_cast<uint4*>(S.table) + wid * (kWaveSlots / 4);
+        for (uint32_t i = lane; i < (uint32_t)kWaveSlots / 4; i += 64) T4[i] = make_uint4(0, 0, 0, 0);
+        grp_sync<W>();
+        return 0;
+    }
     // candidates are rare (~10 of ~600 entries): flag them in a per-lane mask, then write them
     // at offsets from one prefix sum instead of compacting every entry slot by ballot
     uint32_t cm = 0;
 #pragma unroll
     for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) {
-        if (64 * r < tch) {
+        if (64 * r < mt) {
             const uint32_t t[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
             uint32_t w[4];
 #pragma unroll
-            for (uint32_t e = 0; e < 4; ++e) w[e] = S.table[sketch_cell(t[e]) >> 1];
+            for (uint32_t e = 0; e < 4; ++e) w[e] = S.table[sketch_cell<W>(t[e]) >> 1];
 #pragma unroll
             for (uint32_t e = 0; e < 4; ++e) {
-                const uint32_t c = sketch_cell(t[e]);
+                const uint32_t c = sketch_cell<W>(t[e]);
                 cm |= (((w[e] >> ((c & 1u) << 4)) & 0xFFFFu) >= cmin ? 1u : 0u) << (4 * r + e);
             }
         }
@@ -942,12 +1027,18 @@ __device__ __forceinline__ uint32_t part_sketch(WaveSmem& S, const uint4 (&v)[kD
     cm &= vmask;
     const uint32_t mine = __popc(cm);
     const uint32_t incl = wave_incl_scan(mine);
-    const uint32_t nc = __builtin_amdgcn_readlane(incl, 63);
-    if (nc <= 64 && __ballot(cm != 0)) {
-        uint32_t pos = incl - mine;
+    const uint32_t wnc = __builtin_amdgcn_readlane(incl, 63);
+    uint32_t base = 0;
+    if constexpr (W > 1) {
+        uint32_t b0 = 0;
+        if (lane == 0 && wnc) b0 = atomicAdd(&S.ncand, wnc);
+        base = __builtin_amdgcn_readlane(b0, 0);
+    }
+    if (base + wnc <= 64 && __ballot(cm != 0)) {
+        uint32_t pos = base + incl - mine;
 #pragma unroll
         for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) {
-            if (64 * r < tch) {
+            if (64 * r < mt) {
                 const uint32_t t[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
 #pragma unroll
                 for (uint32_t e = 0; e < 4; ++e)
@@ -955,53 +1046,65 @@ __device__ __forceinline__ uint32_t part_sketch(WaveSmem& S, const uint4 (&v)[kD
             }
         }
     }
-    wave_sync();
+    grp_sync<W>();
+    const uint32_t nc = __builtin_amdgcn_readfirstlane(W == 1 ? wnc : S.ncand);
     {
-        uint4* T4 = reinterpret_cast<uint4*>(S.table);
+        uint4* T4 = reinterpret_cast<uint4*>(S.table) + wid * (kWaveSlots / 4);
         for (uint32_t i = lane; i < (uint32_t)kWaveSlots / 4; i += 64) T4[i] = make_uint4(0, 0, 0, 0);
     }
-    wave_sync();
-    if (nc > 64 || nc == 0) return nc;
-    // lane l < nc holds candidate l; its term's exact count is the number of candidates with
-    // that term (every entry of a term lands in the same cell), owned by the first of them
-    const uint32_t t = lane < nc ? S.cbuf[lane] : kStray;
-    uint32_t cnt = 0;
-    bool first = true;
-    for (uint32_t j = 0; j < nc; ++j) {
-        const uint32_t tj = __builtin_amdgcn_readlane(t, j);
-        const bool eq = t == tj;
-        cnt += eq;
-        first &= !(eq && j < lane);
+    if (wid == 0 && nc && nc <= 64 && !(dbg & 4u)) {
+        // lane l < nc holds candidate l; its term's exact count is the number of candidates with
+        // that term (every entry of a term lands in the same cell), owned by the first of them
+        const uint32_t t = lane < nc ? S.cbuf[lane] : kStray;
+        uint32_t cnt = 0;
+        bool first = true;
+        for (uint32_t j = 0; j < nc; ++j) {
+            const uint32_t tj = __builtin_amdgcn_readlane(t, j);
+            const bool eq = t == tj;
+            cnt += eq;
+            first &= !(eq && j < lane);
+        }
+        surv_append(S, lane < nc && first && cnt >= cmin, min(n_short + t, n_terms - 1u), cnt, surv_n);
     }
-    surv_append(S, lane < nc && first && cnt >= cmin, min(n_short + t, n_terms - 1u), cnt, surv_n);
+    grp_sync<W>();
+    if constexpr (W > 1) {
+        if (wid == 0 && lane == 0) S.ncand = 0;  // every wave has read it; the next writes come after a barrier
+    }
     return nc;
 }
 
-__global__ __launch_bounds__(64, kWaveWavesPerSimd) void k_wave(DevIndex X, SearchParams P, const uint8_t* __restrict__ qnorm,
-                                             const uint64_t* __restrict__ qoff, const uint32_t* __restrict__ qm,
-                                             uint32_t* __restrict__ out_n, uint32_t* __restrict__ out_k,
-                                             float* __restrict__ out_s, uint32_t* __restrict__ list2,
-                                             uint32_t* __restrict__ count2, DevStats* __restrict__ stats) {
-    __shared__ WaveSmem S;
-    const uint32_t q = blockIdx.x, lane = lane_id();
+template <int W>
+__global__ __launch_bounds__(64 * W, kWaveWavesPerSimd) void k_wave(DevIndex X, SearchParams P,
+                                                                   const uint8_t* __restrict__ qnorm,
+                                                                   const uint64_t* __restrict__ qoff,
+                                                                   const uint32_t* __restrict__ qm,
+                                                                   uint32_t* __restrict__ out_n,
+                                                                   uint32_t* __restrict__ out_k,
+                                                                   float* __restrict__ out_s,
+                                                                   uint32_t* __restrict__ list2,
+                                                                   uint32_t* __restrict__ count2,
+                                                                   DevStats* __restrict__ stats) {
+    __shared__ WaveSmem<W> S;
+    const uint32_t q = blockIdx.x, lane = lane_id(), tid = threadIdx.x;
+    const uint32_t wid = W == 1 ? 0u : __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t m = qm[q];
     const uint32_t L = P.limit;
     const size_t ob = (size_t)q * P.out_stride;
     if (m == kQueryWildcard) {  // nGramSearch.hpp:356-369, answer precomputed at index time
         const uint32_t n = min(L, X.n_keys);
-        for (uint32_t i = lane; i < n; i += 64) {
+        for (uint32_t i = tid; i < n; i += 64 * W) {
             out_k[ob + i] = X.wild_key[i];
             out_s[ob + i] = X.wild_score[i];
         }
-        if (lane == 0) out_n[q] = n;
+        if (tid == 0) out_n[q] = n;
         return;
     }
     if (m == 0) {  // nothing left after normalisation, nGramSearch.hpp:374-375
-        if (lane == 0) out_n[q] = 0;
+        if (tid == 0) out_n[q] = 0;
         return;
     }
     if (m <= kFullScanQueryLen || m - 2 > kWaveMaxGrams || L > kWaveMaxLimit) {
-        if (lane == 0) list2[atomicAdd(count2, 1u)] = q;  // tier 2 / library-wide path
+        if (tid == 0) list2[atomicAdd(count2, 1u)] = q;  // tier 2 / library-wide path
         return;
     }
     const uint32_t n = m - 2;
@@ -1011,13 +1114,16 @@ __global__ __launch_bounds__(64, kWaveWavesPerSimd) void k_wave(DevIndex X, Sear
     unsigned long long wacc_[16] = {};
 #endif
     const uint8_t* qg = qnorm + qoff[q];
-    for (uint32_t i = lane; i < m; i += 64) S.q[i] = qg[i];
-    if (lane == 0) S.surv_total = 0;
+    for (uint32_t i = tid; i < m; i += 64 * W) S.q[i] = qg[i];
+    if (tid == 0) {
+        S.surv_total = 0;
+        S.ncand = 0;
+    }
     {
         uint4* T4 = reinterpret_cast<uint4*>(S.table);
-        for (uint32_t i = lane; i < (uint32_t)kWaveSlots / 4; i += 64) T4[i] = make_uint4(0, 0, 0, 0);
+        for (uint32_t i = tid; i < (uint32_t)kWaveSlots * W / 4; i += 64 * W) T4[i] = make_uint4(0, 0, 0, 0);
     }
-    wave_sync();
+    grp_sync<W>();
     uint32_t cand_n = 0, surv_n = 0;
     uint64_t tau = kNoCand;
     unsigned* err = &stats->errors;
@@ -1025,8 +1131,8 @@ __global__ __launch_bounds__(64, kWaveWavesPerSimd) void k_wave(DevIndex X, Sear
     const float sc_long = lane <= n ? (float)lane / (float)n : 0.0f;
     const float sc_short = lane <= m ? (float)lane / (float)m : 0.0f;
 
-    // ---- searchShort over shortLib (nGramSearch.hpp:262-270), 4 <= m < 9 ----
-    if (m < kShortQueryLen && X.n_short) {
+    // ---- searchShort over shortLib (nGramSearch.hpp:262-270), 4 <= m < 9, wave 0 ----
+    if (wid == 0 && m < kShortQueryLen && X.n_short) {
         uint8_t qc[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) qc[i] = (uint32_t)i < m ? S.q[i] : 0;
@@ -1047,7 +1153,8 @@ __global__ __launch_bounds__(64, kWaveWavesPerSimd) void k_wave(DevIndex X, Sear
 
     // ---- searchLong (nGramSearch.hpp:278-301) ----
     // lane i: occurrence i of a query gram; lanes 0..ng-1 then own the occurrences whose gram
-    // has postings (a gram repeated k times owns k lanes: count with multiplicity)
+    // has postings (a gram repeated k times owns k lanes: count with multiplicity). Every wave
+    // computes the same plan.
     uint64_t gbase = 0;
     uint32_t glen = 0, grow = 0;
     bool have = false;
@@ -1080,24 +1187,25 @@ __global__ __launch_bounds__(64, kWaveWavesPerSimd) void k_wave(DevIndex X, Sear
     const unsigned long long pm = __ballot(lane <= n && lane > 0 && !(sc_long < P.thr));  // hpp:315
     const uint32_t cmin = pm ? (uint32_t)(__ffsll((long long)pm) - 1) : 1000u;
     const bool sketch = cmin >= 3;
+    constexpr uint32_t kChunks = kWaveChunks * W;  // part cap
     WSTAMP(1);
     if (p_total && cmin <= n) {
         const uint32_t K = X.n_buckets, span = X.bucket_span;
         const uint32_t wmax = (uint32_t)max64(1, min64(K, kMaxPartSpan / max(span, 1u)));
-        const uint32_t w = (uint32_t)max64(1, min64(wmax, (uint64_t)K * kWaveTarget / p_total));
+        const uint32_t w = (uint32_t)max64(1, min64(wmax, (uint64_t)K * kWaveTarget * W / p_total));
         const uint32_t* sk = X.skip + (size_t)grow * (K + 1);
         const uint4* post4 = reinterpret_cast<const uint4*>(X.post);
         const uint32_t a0 = (uint32_t)gbase & 3u;  // list start within its 16-byte chunk
         // entries [s, e) of this lane's list cover 16-byte chunks [(a0 + s) / 4, (a0 + e + 3) / 4)
         auto chunks = [a0](uint32_t s, uint32_t e) -> uint32_t { return e > s ? ((a0 + e + 3) >> 2) - ((a0 + s) >> 2) : 0u; };
-        // part iterator: buckets [bnext, bnext + w) unless they exceed kWaveChunks, then term-id sub-parts
+        // part iterator: buckets [bnext, bnext + w) unless they exceed kChunks, then term-id sub-parts
         uint32_t cur = 0, bnext = 0;
         uint32_t e_pre = sk[min(K, w)];  // end of the next bucket part (row 0 for idle lanes)
-        bool in_sub = false;
+        uint32_t in_sub = 0;
         uint32_t sub_lo = 0, hi_lim = 0, sub_end = 0, sub_bnext = 0, step = 1;
         // software pipeline in registers: part i+1's loads are in flight while part i is counted
         uint4 pv[kDmaRounds];
-        uint32_t p_vm = 0, p_tch = 0, p_lo = 0;
+        uint32_t p_vm = 0, p_mt = 0, p_lo = 0;
         bool have_p = false;
 #pragma unroll
         for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) pv[r] = make_uint4(0, 0, 0, 0);
@@ -1105,22 +1213,44 @@ __global__ __launch_bounds__(64, kWaveWavesPerSimd) void k_wave(DevIndex X, Sear
             uint4 cv[kDmaRounds];
 #pragma unroll
             for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) cv[r] = pv[r];
-            const uint32_t c_vm = p_vm, c_tch = p_tch, c_lo = p_lo;
+            const uint32_t c_vm = p_vm, c_mt = p_mt, c_lo = p_lo;
             const bool have_c = have_p;
             WSTAMP(2);
             // ---- next part: [lo, ...) with per-lane segments [gbase + cur, gbase + cur + len) ----
             uint32_t lo = 0, len = 0;
             have_p = false;
-            for (;;) {
+            in_sub = __builtin_amdgcn_readfirstlane(in_sub);
+            bnext = __builtin_amdgcn_readfirstlane(bnext);
+            // common case, straight-line: the next group of w buckets is non-empty and fits
+            // (span * w <= kMaxPartSpan holds by the choice of w)
+            bool fast = false;
+            if (!in_sub && bnext < K) {
+                const uint32_t e = lane < ng ? e_pre : cur;
+                const uint32_t tot = wave_sum_u32(chunks(cur, e));
+                if (tot && tot <= kChunks) {
+                    lo = bnext * span;
+                    len = e - cur;
+                    bnext = min(K, bnext + w);
+                    e_pre = sk[min(K, bnext + w)];
+                    have_p = true;
+                    fast = true;
+                }
+            }
+            for (; !fast;) {
+                // loop-carried part state is wave-uniform: keep it in SGPRs
+                guard = __builtin_amdgcn_readfirstlane(guard);
+                bnext = __builtin_amdgcn_readfirstlane(bnext);
+                sub_lo = __builtin_amdgcn_readfirstlane(sub_lo);
+                step = __builtin_amdgcn_readfirstlane(step);
                 if (++guard > 8u * K + 4096u) {
-                    if (lane == 0) atomicOr(err, 4u);
+                    atomicOr(err, 4u);  // every lane (idempotent): a lane-0 branch would make the loop divergent
                     break;
                 }
                 if (!in_sub) {
                     if (bnext >= K) break;
                     const uint32_t bhi = min(K, bnext + w), e = lane < ng ? e_pre : cur;
                     const uint32_t tot = wave_sum_u32(chunks(cur, e));
-                    if (tot <= (uint32_t)kWaveChunks && (uint64_t)span * (bhi - bnext) <= kMaxPartSpan) {
+                    if (tot <= kChunks) {
                         lo = bnext * span;
                         len = e - cur;
                         bnext = bhi;
@@ -1128,32 +1258,36 @@ __global__ __launch_bounds__(64, kWaveWavesPerSimd) void k_wave(DevIndex X, Sear
                         if (tot) { have_p = true; break; }
                         continue;
                     }
-                    in_sub = true;
+                    in_sub = 1;
                     sub_lo = bnext * span;
                     hi_lim = (uint32_t)min64((uint64_t)bhi * span, n_long);
                     sub_end = e;
                     sub_bnext = bhi;
-                    step = (uint32_t)max64(1, min64((uint64_t)(hi_lim - sub_lo) * (kWaveChunks * 3 / 4) / max(tot, 1u),
+                    step = (uint32_t)max64(1, min64((uint64_t)(hi_lim - sub_lo) * (kChunks * 3 / 4) / max(tot, 1u),
                                                     kMaxPartSpan));
                 }
                 const uint32_t hi = (uint32_t)min64(hi_lim, (uint64_t)sub_lo + step);
-                uint32_t a = cur, b = sub_end;
-                if (lane < ng) {
-                    while (a < b) {  // lower_bound(list, hi)
-                        const uint32_t mid = (a + b) >> 1;
-                        if (X.post[gbase + mid] < hi) a = mid + 1; else b = mid;
-                    }
+                // lower_bound(list, hi) per lane, as a ballot-controlled (uniform) loop: a divergent
+                // loop here would make the whole part iterator divergent for the compiler
+                uint32_t a = cur, b = lane < ng ? sub_end : cur;
+                while (__ballot(a < b)) {
+                    const bool act = a < b;
+                    const uint32_t mid = (a + b) >> 1;
+                    const uint32_t pv = X.post[gbase + (act ? mid : 0u)];
+                    const bool below = pv < hi;
+                    a = act && below ? mid + 1 : a;
+                    b = act && !below ? mid : b;
                 }
                 const uint32_t t2 = wave_sum_u32(lane < ng ? chunks(cur, a) : 0u);
-                if (t2 > (uint32_t)kWaveChunks && hi - sub_lo > 1) {
-                    step = max(1u, (uint32_t)((uint64_t)(hi - sub_lo) * (kWaveChunks * 3 / 4) / t2));
+                if (t2 > kChunks && hi - sub_lo > 1) {
+                    step = max(1u, (uint32_t)((uint64_t)(hi - sub_lo) * (kChunks * 3 / 4) / t2));
                     continue;
                 }
                 lo = sub_lo;
                 len = lane < ng ? a - cur : 0u;
                 sub_lo = hi;
                 if (sub_lo >= hi_lim) {
-                    in_sub = false;
+                    in_sub = 0;
                     bnext = sub_bnext;
                     e_pre = sk[min(K, bnext + w)];
                 }
@@ -1161,32 +1295,33 @@ __global__ __launch_bounds__(64, kWaveWavesPerSimd) void k_wave(DevIndex X, Sear
                 cur = a;
             }
             WSTAMP(3);
-            // ---- part i+1: issue its loads ----
+            // ---- part i+1: issue this wave's loads ----
             if (have_p) {
-                p_tch = stage_part(S, post4, gbase, a0, cur, len, pv, p_vm);
+                p_mt = stage_part(S, post4, gbase, a0, cur, len, pv, p_vm);
                 p_lo = lo;
                 cur += len;
             }
             WSTAMP(4);
             // ---- count part i while part i+1 is in flight ----
             if (have_c && !(P.dbg & 1u)) {  // dbg 1: load only, no counting
-                if (surv_n + 64 > (uint32_t)kWaveSurv)
+                if (wid == 0 && surv_n + 64 > (uint32_t)kWaveSurv)
                     wave_emit(S, X, P, m, L, sc_long, sc_short, surv_n, cand_n, tau);
-                const uint32_t nc = sketch ? part_sketch(S, cv, c_vm, c_tch, cmin, X.n_short, X.n_terms, surv_n) : 65u;
+                const uint32_t nc = sketch ? part_sketch(S, cv, c_vm, c_mt, cmin, X.n_short, X.n_terms, surv_n, P.dbg) : 65u;
                 const bool done = nc <= 64;
                 WCOUNT(11, 1);
                 WCOUNT(12, done ? 0 : 1);
                 WCOUNT(13, sketch ? nc : 0);
-                WCOUNT(14, c_tch);
+                WCOUNT(14, c_mt);
                 WSTAMP(5);
                 if (!done)
-                    part_exact(S, cv, c_vm, c_tch, X, P, m, L, c_lo, cmin, sc_long, sc_short, surv_n, cand_n, tau, err);
+                    part_exact(S, cv, c_vm, c_mt, X, P, m, L, c_lo, cmin, sc_long, sc_short, surv_n, cand_n, tau, err);
                 WSTAMP(6);
             }
             if (!have_p) break;
         }
     }
     WSTAMP(7);
+    if (wid != 0) return;
     if (surv_n) wave_emit(S, X, P, m, L, sc_long, sc_short, surv_n, cand_n, tau);
     WSTAMP(8);
     wave_flush(S, cand_n, tau, L);
@@ -1372,8 +1507,20 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
                        const uint32_t* qm, uint32_t* out_n, uint32_t* out_k, float* out_s, uint32_t* list2,
                        uint32_t* count2, uint32_t* glist, uint32_t* gcount, DevStats* stats, hipStream_t s) {
     if (!P.n_queries) return hipSuccess;
-    hipLaunchKernelGGL(k_wave, dim3(P.n_queries), dim3(64), 0, s, X, P, qnorm, off, qm, out_n, out_k, out_s, list2,
-                       count2, stats);
+    switch (P.waves) {  // waves per query (SearchParams.waves, NGS_WAVES)
+        case 1:
+            hipLaunchKernelGGL(k_wave<1>, dim3(P.n_queries), dim3(64), 0, s, X, P, qnorm, off, qm, out_n, out_k,
+                               out_s, list2, count2, stats);
+            break;
+        case 2:
+            hipLaunchKernelGGL(k_wave<2>, dim3(P.n_queries), dim3(128), 0, s, X, P, qnorm, off, qm, out_n, out_k,
+                               out_s, list2, count2, stats);
+            break;
+        default:
+            hipLaunchKernelGGL(k_wave<4>, dim3(P.n_queries), dim3(256), 0, s, X, P, qnorm, off, qm, out_n, out_k,
+                               out_s, list2, count2, stats);
+            break;
+    }
     const uint32_t grid2 = std::min<uint32_t>(P.n_queries, 1024);
     hipLaunchKernelGGL(k_fast, dim3(grid2), dim3(kFastThreads), 0, s, X, P, qnorm, off, qm, out_n, out_k, out_s,
                        (const uint32_t*)list2, (const uint32_t*)count2, glist, gcount, stats);
