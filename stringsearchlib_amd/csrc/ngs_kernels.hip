@@ -1034,17 +1034,20 @@ __device__ __forceinline__ uint32_t part_sketch(WaveSmem<W>& S, const uint4 (&v)
         if (lane == 0 && wnc) b0 = atomicAdd(&S.ncand, wnc);
         base = __builtin_amdgcn_readlane(b0, 0);
     }
-    if (base + wnc <= 64 && __ballot(cm != 0)) {
+    if (base + wnc <= 64 && cm) {  // the few lanes holding candidates walk their set bits
         uint32_t pos = base + incl - mine;
+        uint32_t bits = cm;
+        do {
+            const uint32_t k = __ffs(bits) - 1u;
+            bits &= bits - 1u;
+            uint32_t t = 0;
 #pragma unroll
-        for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) {
-            if (64 * r < mt) {
-                const uint32_t t[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
-#pragma unroll
-                for (uint32_t e = 0; e < 4; ++e)
-                    if ((cm >> (4 * r + e)) & 1u) S.cbuf[pos++] = t[e];
+            for (uint32_t j = 0; j < 4 * (uint32_t)kDmaRounds; ++j) {
+                const uint32_t x = (j & 3) == 0 ? v[j >> 2].x : (j & 3) == 1 ? v[j >> 2].y : (j & 3) == 2 ? v[j >> 2].z : v[j >> 2].w;
+                t = j == k ? x : t;
             }
-        }
+            S.cbuf[pos++] = t;
+        } while (bits);
     }
     grp_sync<W>();
     const uint32_t nc = __builtin_amdgcn_readfirstlane(W == 1 ? wnc : S.ncand);
