@@ -1298,6 +1298,7 @@ __global__ __launch_bounds__(64 * W, kWaveWavesPerSimd) void k_wave(DevIndex X, 
                 cur = a;
             }
             WSTAMP(3);
+            have_p = __builtin_amdgcn_readfirstlane(have_p ? 1u : 0u) != 0;  // uniform: scalar loop exit
             // ---- part i+1: issue this wave's loads ----
             if (have_p) {
                 p_mt = stage_part(S, post4, gbase, a0, cur, len, pv, p_vm);
