@@ -49,14 +49,17 @@ constexpr uint32_t kMinBucketTerms = 4096;
 // ---- wave kernel geometry (tier 1: one wave per query) ----
 constexpr int kWaveSlotBits = 11;
 constexpr int kWaveSlots = 1 << kWaveSlotBits;  // wave-private LDS hash table
-constexpr int kWaveCap = kWaveSlots / 2;        // postings per part (<= 50 % load)
+constexpr int kWaveCap = kWaveSlots / 2;        // entries per exact-count pass (<= 50 % table load)
+constexpr int kSketchCap = kWaveCap;            // entries per sketch part (u8 counters, 4 per word: 8 cells per entry)
 constexpr int kWaveCand = 256;                  // candidate buffer per query
 constexpr uint32_t kWaveMaxLimit = kWaveCand / 2;
-constexpr int kWaveChunks = kWaveCap / 4;       // 16-byte chunks per stage buffer
+constexpr int kWaveChunks = kSketchCap / 4;     // 16-byte chunks per part and wave (sketch parts)
+constexpr int kExactChunks = kWaveCap / 4;      // ... for parts counted exactly (cmin <= 2)
 constexpr int kDmaRounds = kWaveChunks / 64;    // dwordx4 loads per lane for one part
 constexpr int kWaveWavesPerSimd = 4;            // occupancy target: <= 128 VGPRs
 constexpr uint32_t kDefaultWaves = 1;           // waves per query in the tier-1 kernel
-constexpr int kWaveTarget = kWaveCap * 5 / 8;   // postings per part the bucket grouping aims at
+constexpr int kWaveTarget = kWaveCap * 5 / 8;   // postings per exact part the bucket grouping aims at
+constexpr int kSketchTarget = kSketchCap * 5 / 8;  // ... per sketch part
 constexpr uint32_t kStray = 0xFFFFFFFFu;        // staged entry outside its list segment
 constexpr int kWaveSurv = 128;                  // survivor list (term, count) before calcScore
 constexpr uint32_t kWaveMaxGrams = 63;          // counts <= 63: one lane per count value

@@ -638,6 +638,7 @@ struct alignas(16) WaveSmem {
     uint32_t surv_total;             // stats
     uint32_t ncand;                  // sketch candidates of the part, all waves
     uint32_t x_surv_n, x_cand_n;     // wave 0's emit state, handed round in exact-path turns
+    uint32_t xcnt;                   // exact-pass range sizing: max entries in range over the waves
     uint64_t x_tau;
 };
 
@@ -846,8 +847,8 @@ __device__ __forceinline__ uint32_t wave_insert_slot(uint32_t* T, uint32_t rel, 
 // sketch cell of a term: full-rate shift/xor (v_mul_lo_u32 is quarter rate). Term ids of a part
 // are spread over a range much wider than the table, and consecutive ids get distinct cells.
 template <int W>
-__device__ __forceinline__ uint32_t sketch_cell(uint32_t t) {
-    constexpr uint32_t kBits = kWaveSlotBits + 1 + (W == 4 ? 2 : W == 2 ? 1 : 0);
+__device__ __forceinline__ uint32_t sketch_cell(uint32_t t) {  // u8 counter index: 4 per table word
+    constexpr uint32_t kBits = kWaveSlotBits + 2 + (W == 4 ? 2 : W == 2 ? 1 : 0);
     return (t ^ (t >> kBits)) & ((1u << kBits) - 1u);
 }
 
@@ -886,16 +887,30 @@ __device__ __forceinline__ uint32_t stage_part(WaveSmem<W>& S, const uint4* __re
     // the list holding this wave's first chunk may start in an earlier wave's range
     const unsigned long long before = __ballot(nch != 0 && pre < c0);
     uint32_t carry = before ? 64u - (uint32_t)__clzll(before) : 0u;
+    // all rounds' max-scans are independent; the carries chain only through their lane-63
+    // values, so the LDS reads and loads of the rounds can be in flight together
+    uint32_t scn[kDmaRounds];
+#pragma unroll
+    for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) {
+        const uint32_t lc = 64 * r + lane;
+        scn[r] = 64 * r < mt ? wave_incl_max_scan(lc < mt ? (uint32_t)mk[lc] : 0u) : 0u;
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) {
+        const uint32_t top = __builtin_amdgcn_readlane(scn[r], 63);
+        scn[r] = max(scn[r], carry);
+        carry = max(carry, top);
+    }
     vmask = 0;
 #pragma unroll
     for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) {
         if (64 * r < mt) {
             const uint32_t lc = 64 * r + lane, c = c0 + lc;
             const bool ok = lc < mt;
-            const uint32_t sc = max(wave_incl_max_scan(ok ? (uint32_t)mk[lc] : 0u), carry);
-            carry = __builtin_amdgcn_readlane(sc, 63);
-            const uint2 seg = S.segtab[wid][(sc - 1u) & 63u];
-            v[r] = post4[ok ? seg.x + c : 0u];
+            const uint2 seg = S.segtab[wid][(scn[r] - 1u) & 63u];
+            // inactive lanes must not load: a shared fallback address would be read by every wave
+            // of the GPU and serialise on one L2 channel
+            if (ok) v[r] = post4[seg.x + c];
             // entries [lo_e, hi_e) of this chunk are in the list segment [y, z)
             const int y = (int)(seg.y & 0xFFFFu), z = (int)(seg.y >> 16);
             const uint32_t lo_e = (uint32_t)min(max(y - (int)(4 * c), 0), 4);
@@ -907,24 +922,29 @@ __device__ __forceinline__ uint32_t stage_part(WaveSmem<W>& S, const uint4* __re
     return mt;
 }
 
-// Exact count of a part held in registers (all waves): shared LDS hash table term -> count.
-// Each entry's slot replaces its term in the registers; the extraction exchanges the slot with
-// 0, so the first holder of a term owns its count (no table scan; the table ends empty). With
+// Exact count of the part's entries with term ids in [ta, tb) (all waves; at most kWaveCap x W
+// of them): shared LDS hash table term -> count. Each such entry's register is replaced by
+// its slot, tagged with the pass number (bit 31 | pass << 16 | slot; term ids stay below 2^31),
+// so later passes over other term ranges skip it; the extraction exchanges the slot with 0,
+// so the first holder of a term owns its count (no table scan; the table ends empty). With
 // W > 1 the waves extract in turns, handing wave 0's survivor / top-L state round in LDS.
 template <int W>
 __device__ __forceinline__ void part_exact(WaveSmem<W>& S, uint4 (&v)[kDmaRounds], uint32_t vmask, uint32_t mt,
-                                           const DevIndex& X, const SearchParams& P, uint32_t m, uint32_t L,
-                                           uint32_t lo, uint32_t cmin, float sc_long, float sc_short,
-                                           uint32_t& surv_n, uint32_t& cand_n, uint64_t& tau, unsigned* err) {
+                                           uint32_t ta, uint32_t tb, uint32_t pass, const DevIndex& X,
+                                           const SearchParams& P, uint32_t m, uint32_t L, uint32_t cmin,
+                                           float sc_long, float sc_short, uint32_t& surv_n, uint32_t& cand_n,
+                                           uint64_t& tau, unsigned* err) {
     const uint32_t lane = lane_id(), wid = W == 1 ? 0u : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     mt = __builtin_amdgcn_readfirstlane(mt);
+    const uint32_t tag = 0x80000000u | (pass << 16);
 #pragma unroll
     for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) {
         if (64 * r < mt) {
 #pragma unroll
             for (uint32_t e = 0; e < 4; ++e) {
                 uint32_t& x = e == 0 ? v[r].x : e == 1 ? v[r].y : e == 2 ? v[r].z : v[r].w;
-                x = (vmask >> (4 * r + e)) & 1u ? wave_insert_slot<W>(S.table, x - lo + 1u, err) : kStray;
+                if (((vmask >> (4 * r + e)) & 1u) && x - ta < tb - ta)
+                    x = tag | wave_insert_slot<W>(S.table, x - ta + 1u, err);
             }
         }
     }
@@ -940,30 +960,39 @@ __device__ __forceinline__ void part_exact(WaveSmem<W>& S, uint4 (&v)[kDmaRounds
     for (uint32_t turn = 0; turn < (uint32_t)W; ++turn) {
         if (wid == turn) {
             uint32_t sn = W == 1 ? surv_n : S.x_surv_n, cn = W == 1 ? cand_n : S.x_cand_n;
-            uint64_t ta = W == 1 ? tau : S.x_tau;
+            uint64_t ta2 = W == 1 ? tau : S.x_tau;
             // one element slot per step (a single wave_emit call site keeps the registers out of scratch)
             for (uint32_t k = 0; k < 4 * (uint32_t)kDmaRounds && 64 * (k >> 2) < mt; ++k) {
-                if (sn + 64 > (uint32_t)kWaveSurv) wave_emit(S, X, P, m, L, sc_long, sc_short, sn, cn, ta);
-                uint32_t sl = kStray;
+                if (sn + 64 > (uint32_t)kWaveSurv) wave_emit(S, X, P, m, L, sc_long, sc_short, sn, cn, ta2);
+                uint32_t x = kStray;
+                if (k < 16) {  // 16-way selects (k is uniform)
 #pragma unroll
-                for (uint32_t j = 0; j < 4 * (uint32_t)kDmaRounds; ++j) {
-                    const uint32_t x = (j & 3) == 0 ? v[j >> 2].x : (j & 3) == 1 ? v[j >> 2].y : (j & 3) == 2 ? v[j >> 2].z : v[j >> 2].w;
-                    sl = j == k ? x : sl;
+                    for (uint32_t j = 0; j < 16; ++j) {
+                        const uint32_t y = (j & 3) == 0 ? v[j >> 2].x : (j & 3) == 1 ? v[j >> 2].y : (j & 3) == 2 ? v[j >> 2].z : v[j >> 2].w;
+                        x = j == k ? y : x;
+                    }
+                } else {
+#pragma unroll
+                    for (uint32_t j = 16; j < 4 * (uint32_t)kDmaRounds; ++j) {
+                        const uint32_t y = (j & 3) == 0 ? v[j >> 2].x : (j & 3) == 1 ? v[j >> 2].y : (j & 3) == 2 ? v[j >> 2].z : v[j >> 2].w;
+                        x = j == k ? y : x;
+                    }
                 }
-                const uint32_t c = sl != kStray ? atomicExch(&S.table[sl], 0u) : 0u;
+                const bool mine = (x >> 16) == (tag >> 16);
+                const uint32_t c = mine ? atomicExch(&S.table[x & 0xFFFFu], 0u) : 0u;
                 const uint32_t cnt = c & 255u;  // s = cnt / n; s >= thr <=> cnt >= cmin (nGramSearch.hpp:300,315)
-                surv_append(S, c != 0 && cnt >= cmin, min(X.n_short + lo + (c >> 8) - 1u, X.n_terms - 1u), cnt, sn);
+                surv_append(S, c != 0 && cnt >= cmin, min(X.n_short + ta + (c >> 8) - 1u, X.n_terms - 1u), cnt, sn);
             }
             if constexpr (W == 1) {
                 surv_n = sn;
                 cand_n = cn;
-                tau = ta;
+                tau = ta2;
             } else {
                 wave_sync();
                 if (lane == 0) {
                     S.x_surv_n = sn;
                     S.x_cand_n = cn;
-                    S.x_tau = ta;
+                    S.x_tau = ta2;
                 }
             }
         }
@@ -979,8 +1008,9 @@ __device__ __forceinline__ void part_exact(WaveSmem<W>& S, uint4 (&v)[kDmaRounds
     }
 }
 
-// Sketch count of a part held in registers (cmin >= 3; all waves): 2 x u16 counters per shared
-// table word, never an undercount. Entries whose cell reaches cmin are candidates; wave 0 gets
+// Sketch count of a part held in registers (cmin >= 3; all waves): 4 x u8 counters per shared
+// table word, never an undercount (an increment that wraps a counter past 255 is seen in the
+// value the atomic returns and sends the part to exact counting). Entries whose cell reaches cmin are candidates; wave 0 gets
 // their exact counts by comparing the <= 64 candidates with each other. Returns the number of
 // candidate entries; above 64 the caller counts the part exactly (the table is clean again).
 template <int W>
@@ -989,6 +1019,7 @@ __device__ __forceinline__ uint32_t part_sketch(WaveSmem<W>& S, const uint4 (&v)
                                                 uint32_t& surv_n, uint32_t dbg) {
     const uint32_t lane = lane_id(), wid = W == 1 ? 0u : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     mt = __builtin_amdgcn_readfirstlane(mt);
+    bool ovf = false;
 #pragma unroll
     for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) {
         if (64 * r < mt) {
@@ -996,7 +1027,9 @@ __device__ __forceinline__ uint32_t part_sketch(WaveSmem<W>& S, const uint4 (&v)
 #pragma unroll
             for (uint32_t e = 0; e < 4; ++e) {
                 const uint32_t c = sketch_cell<W>(t[e]);
-                atomicAdd(&S.table[c >> 1], ((vmask >> (4 * r + e)) & 1u) << ((c & 1u) << 4));
+                const uint32_t sh = (c & 3u) << 3;
+                const uint32_t old = atomicAdd(&S.table[c >> 2], ((vmask >> (4 * r + e)) & 1u) << sh);
+                ovf |= ((old >> sh) & 0xFFu) == 0xFFu;
             }
         }
     }
@@ -1016,18 +1049,19 @@ __device__ __forceinline__ uint32_t part_sketch(WaveSmem<W>& S, const uint4 (&v)
             const uint32_t t[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
             uint32_t w[4];
 #pragma unroll
-            for (uint32_t e = 0; e < 4; ++e) w[e] = S.table[sketch_cell<W>(t[e]) >> 1];
+            for (uint32_t e = 0; e < 4; ++e) w[e] = S.table[sketch_cell<W>(t[e]) >> 2];
 #pragma unroll
             for (uint32_t e = 0; e < 4; ++e) {
                 const uint32_t c = sketch_cell<W>(t[e]);
-                cm |= (((w[e] >> ((c & 1u) << 4)) & 0xFFFFu) >= cmin ? 1u : 0u) << (4 * r + e);
+                cm |= (((w[e] >> ((c & 3u) << 3)) & 0xFFu) >= cmin ? 1u : 0u) << (4 * r + e);
             }
         }
     }
     cm &= vmask;
+    const uint32_t ov = __ballot(ovf) ? 65u : 0u;  // a wrapped counter forces exact counting
     const uint32_t mine = __popc(cm);
     const uint32_t incl = wave_incl_scan(mine);
-    const uint32_t wnc = __builtin_amdgcn_readlane(incl, 63);
+    const uint32_t wnc = __builtin_amdgcn_readlane(incl, 63) + ov;
     uint32_t base = 0;
     if constexpr (W > 1) {
         uint32_t b0 = 0;
@@ -1050,7 +1084,7 @@ __device__ __forceinline__ uint32_t part_sketch(WaveSmem<W>& S, const uint4 (&v)
         } while (bits);
     }
     grp_sync<W>();
-    const uint32_t nc = __builtin_amdgcn_readfirstlane(W == 1 ? wnc : S.ncand);
+    uint32_t nc = __builtin_amdgcn_readfirstlane(W == 1 ? wnc : S.ncand);
     {
         uint4* T4 = reinterpret_cast<uint4*>(S.table) + wid * (kWaveSlots / 4);
         for (uint32_t i = lane; i < (uint32_t)kWaveSlots / 4; i += 64) T4[i] = make_uint4(0, 0, 0, 0);
@@ -1121,6 +1155,7 @@ __global__ __launch_bounds__(64 * W, kWaveWavesPerSimd) void k_wave(DevIndex X, 
     if (tid == 0) {
         S.surv_total = 0;
         S.ncand = 0;
+        S.xcnt = 0;
     }
     {
         uint4* T4 = reinterpret_cast<uint4*>(S.table);
@@ -1190,12 +1225,13 @@ __global__ __launch_bounds__(64 * W, kWaveWavesPerSimd) void k_wave(DevIndex X, 
     const unsigned long long pm = __ballot(lane <= n && lane > 0 && !(sc_long < P.thr));  // hpp:315
     const uint32_t cmin = pm ? (uint32_t)(__ffsll((long long)pm) - 1) : 1000u;
     const bool sketch = cmin >= 3;
-    constexpr uint32_t kChunks = kWaveChunks * W;  // part cap
+    // part cap: a sketch part holds twice the entries of an exact pass (u8 vs u32 cells)
+    const uint32_t kChunks = (sketch ? (uint32_t)kWaveChunks : (uint32_t)kExactChunks) * W;
     WSTAMP(1);
     if (p_total && cmin <= n) {
         const uint32_t K = X.n_buckets, span = X.bucket_span;
         const uint32_t wmax = (uint32_t)max64(1, min64(K, kMaxPartSpan / max(span, 1u)));
-        const uint32_t w = (uint32_t)max64(1, min64(wmax, (uint64_t)K * kWaveTarget * W / p_total));
+        const uint32_t w = (uint32_t)max64(1, min64(wmax, (uint64_t)K * (sketch ? kSketchTarget : kWaveTarget) * W / p_total));
         const uint32_t* sk = X.skip + (size_t)grow * (K + 1);
         const uint4* post4 = reinterpret_cast<const uint4*>(X.post);
         const uint32_t a0 = (uint32_t)gbase & 3u;  // list start within its 16-byte chunk
@@ -1203,12 +1239,14 @@ __global__ __launch_bounds__(64 * W, kWaveWavesPerSimd) void k_wave(DevIndex X, 
         auto chunks = [a0](uint32_t s, uint32_t e) -> uint32_t { return e > s ? ((a0 + e + 3) >> 2) - ((a0 + s) >> 2) : 0u; };
         // part iterator: buckets [bnext, bnext + w) unless they exceed kChunks, then term-id sub-parts
         uint32_t cur = 0, bnext = 0;
-        uint32_t e_pre = sk[min(K, w)];  // end of the next bucket part (row 0 for idle lanes)
+        // end of the next bucket part; idle lanes load nothing (a shared row would be a hot spot)
+        uint32_t e_pre = 0;
+        if (lane < ng) e_pre = sk[min(K, w)];
         uint32_t in_sub = 0;
         uint32_t sub_lo = 0, hi_lim = 0, sub_end = 0, sub_bnext = 0, step = 1;
         // software pipeline in registers: part i+1's loads are in flight while part i is counted
         uint4 pv[kDmaRounds];
-        uint32_t p_vm = 0, p_mt = 0, p_lo = 0;
+        uint32_t p_vm = 0, p_mt = 0, p_lo = 0, p_hi = 0;
         bool have_p = false;
 #pragma unroll
         for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) pv[r] = make_uint4(0, 0, 0, 0);
@@ -1216,11 +1254,11 @@ __global__ __launch_bounds__(64 * W, kWaveWavesPerSimd) void k_wave(DevIndex X, 
             uint4 cv[kDmaRounds];
 #pragma unroll
             for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) cv[r] = pv[r];
-            const uint32_t c_vm = p_vm, c_mt = p_mt, c_lo = p_lo;
+            const uint32_t c_vm = p_vm, c_mt = p_mt, c_lo = p_lo, c_hi = p_hi;
             const bool have_c = have_p;
             WSTAMP(2);
             // ---- next part: [lo, ...) with per-lane segments [gbase + cur, gbase + cur + len) ----
-            uint32_t lo = 0, len = 0;
+            uint32_t lo = 0, hi_t = 0, len = 0;  // part: term ids [lo, hi_t)
             have_p = false;
             in_sub = __builtin_amdgcn_readfirstlane(in_sub);
             bnext = __builtin_amdgcn_readfirstlane(bnext);
@@ -1234,7 +1272,8 @@ __global__ __launch_bounds__(64 * W, kWaveWavesPerSimd) void k_wave(DevIndex X, 
                     lo = bnext * span;
                     len = e - cur;
                     bnext = min(K, bnext + w);
-                    e_pre = sk[min(K, bnext + w)];
+                    hi_t = (uint32_t)min64((uint64_t)bnext * span, n_long);
+                    if (lane < ng) e_pre = sk[min(K, bnext + w)];
                     have_p = true;
                     fast = true;
                 }
@@ -1257,7 +1296,8 @@ __global__ __launch_bounds__(64 * W, kWaveWavesPerSimd) void k_wave(DevIndex X, 
                         lo = bnext * span;
                         len = e - cur;
                         bnext = bhi;
-                        e_pre = sk[min(K, bnext + w)];
+                        hi_t = (uint32_t)min64((uint64_t)bhi * span, n_long);
+                        if (lane < ng) e_pre = sk[min(K, bnext + w)];
                         if (tot) { have_p = true; break; }
                         continue;
                     }
@@ -1276,7 +1316,8 @@ __global__ __launch_bounds__(64 * W, kWaveWavesPerSimd) void k_wave(DevIndex X, 
                 while (__ballot(a < b)) {
                     const bool act = a < b;
                     const uint32_t mid = (a + b) >> 1;
-                    const uint32_t pv = X.post[gbase + (act ? mid : 0u)];
+                    uint32_t pv = 0;
+                    if (act) pv = X.post[gbase + mid];
                     const bool below = pv < hi;
                     a = act && below ? mid + 1 : a;
                     b = act && !below ? mid : b;
@@ -1287,12 +1328,13 @@ __global__ __launch_bounds__(64 * W, kWaveWavesPerSimd) void k_wave(DevIndex X, 
                     continue;
                 }
                 lo = sub_lo;
+                hi_t = hi;
                 len = lane < ng ? a - cur : 0u;
                 sub_lo = hi;
                 if (sub_lo >= hi_lim) {
                     in_sub = 0;
                     bnext = sub_bnext;
-                    e_pre = sk[min(K, bnext + w)];
+                    if (lane < ng) e_pre = sk[min(K, bnext + w)];
                 }
                 if (t2) { have_p = true; break; }
                 cur = a;
@@ -1303,6 +1345,7 @@ __global__ __launch_bounds__(64 * W, kWaveWavesPerSimd) void k_wave(DevIndex X, 
             if (have_p) {
                 p_mt = stage_part(S, post4, gbase, a0, cur, len, pv, p_vm);
                 p_lo = lo;
+                p_hi = hi_t;
                 cur += len;
             }
             WSTAMP(4);
@@ -1317,8 +1360,40 @@ __global__ __launch_bounds__(64 * W, kWaveWavesPerSimd) void k_wave(DevIndex X, 
                 WCOUNT(13, sketch ? nc : 0);
                 WCOUNT(14, c_mt);
                 WSTAMP(5);
-                if (!done)
-                    part_exact(S, cv, c_vm, c_mt, X, P, m, L, c_lo, cmin, sc_long, sc_short, surv_n, cand_n, tau, err);
+                if (!done) {
+                    // exact count in term-id ranges of <= kWaveCap entries per wave (one range unless a
+                    // sketch part overflowed)
+                    const uint32_t mtu = __builtin_amdgcn_readfirstlane(c_mt);
+                    uint32_t ta = c_lo, pass = 0;
+                    while (ta < c_hi) {
+                        uint32_t tb = c_hi;
+                        for (;;) {
+                            uint32_t cnt = 0;
+#pragma unroll
+                            for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) {
+                                if (64 * r < mtu) {
+                                    const uint32_t t4[4] = {cv[r].x, cv[r].y, cv[r].z, cv[r].w};
+#pragma unroll
+                                    for (uint32_t e = 0; e < 4; ++e)
+                                        cnt += ((c_vm >> (4 * r + e)) & 1u) && t4[e] - ta < tb - ta ? 1u : 0u;
+                                }
+                            }
+                            cnt = wave_sum_u32(cnt);
+                            if constexpr (W > 1) {  // the largest share over the waves decides
+                                if (lane == 0) atomicMax(&S.xcnt, cnt);
+                                grp_sync<W>();
+                                cnt = __builtin_amdgcn_readfirstlane(S.xcnt);
+                                grp_sync<W>();
+                                if (wid == 0 && lane == 0) S.xcnt = 0;
+                            }
+                            if (cnt <= (uint32_t)kWaveCap || tb - ta <= 1) break;
+                            tb = ta + (tb - ta) / 2;
+                        }
+                        part_exact(S, cv, c_vm, c_mt, ta, tb, pass++, X, P, m, L, cmin, sc_long, sc_short, surv_n,
+                                   cand_n, tau, err);
+                        ta = tb;
+                    }
+                }
                 WSTAMP(6);
             }
             if (!have_p) break;

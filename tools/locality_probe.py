@@ -56,7 +56,8 @@ def main():
     raw, offs = corpus.queries(B)
     qs = [raw[offs[i]:offs[i + 1]] for i in range(B)]
     for name, batch in [("bench", qs), ("sorted", sorted(qs)), ("hot4096", [qs[i % 4096] for i in range(B)]),
-                        ("hot256", [qs[i % 256] for i in range(B)])]:
+                        ("hot256", [qs[i % 256] for i in range(B)]), ("hot32", [qs[i % 32] for i in range(B)]),
+                        ("hot1", [qs[0]] * B)]:
         t = time.time()
         ms, ppq = run(L, h, batch)
         print(f"{name:8s} kernel {ms:7.3f} ms  {B / ms / 1e3:6.2f} Mq/s  postings/query {ppq:8.0f}  "

@@ -12,7 +12,7 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
 }
 
-template <int MODE, int M, int ACTIVE>
+template <int MODE, int M, int ACTIVE, uint64_t WIN = (1ull << 22)>
 __global__ __launch_bounds__(64) void k_dma(const uint32_t* __restrict__ src, uint64_t n_words, int iters,
                                             uint32_t* __restrict__ sink) {
     __shared__ __attribute__((aligned(16))) uint32_t st[M * 256];
@@ -42,6 +42,14 @@ __global__ __launch_bounds__(64) void k_dma(const uint32_t* __restrict__ src, ui
                     const uint32_t* g = src + base % (1u << 24) + lane * 4;
                     asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g),
                                  "s"(lds_addr(st + m * 256)) : "memory", "m0");
+                } else if (MODE == 6) {  // register dwordx4, 5-segment gather inside a small window
+                    const uint32_t seg = lane / 13;
+                    const uint64_t sb = (((h >> (8 + 4 * seg)) * 2654435761u) % (WIN / 64)) * 16 + 4 * (seg * 7 % 5);
+                    const uint4 v = *reinterpret_cast<const uint4*>(src + sb + (lane % 13) * 4);
+                    acc += v.x ^ v.y ^ v.z ^ v.w;
+                } else if (MODE == 7) {  // register dwordx4, contiguous, inside a small window
+                    const uint4 v = *reinterpret_cast<const uint4*>(src + (base % WIN) + lane * 4);
+                    acc += v.x ^ v.y ^ v.z ^ v.w;
                 } else if (MODE == 2) {  // register dword
                     acc += __builtin_nontemporal_load(src + base + lane);
                 } else {  // register dwordx4
@@ -52,18 +60,18 @@ __global__ __launch_bounds__(64) void k_dma(const uint32_t* __restrict__ src, ui
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    if (MODE >= 2) { if (acc == 0x12345678u) sink[0] = acc; }
+    if (MODE >= 2 && MODE != 4 && MODE != 5) { if (acc == 0x12345678u) sink[0] = acc; }
     else if (st[lane] == 0x12345678u) sink[1] = lane;
 }
 
-template <int MODE, int M, int ACTIVE>
+template <int MODE, int M, int ACTIVE, uint64_t WIN = (1ull << 22)>
 int run(const char* name, const uint32_t* d, uint64_t n, uint32_t* sink, int waves_per_cu) {
     const int blocks = 256 * waves_per_cu, iters = 200;
     hipEvent_t a, b;
     hipEventCreate(&a); hipEventCreate(&b);
-    k_dma<MODE, M, ACTIVE><<<blocks, 64>>>(d, n, 4, sink);
+    k_dma<MODE, M, ACTIVE, WIN><<<blocks, 64>>>(d, n, 4, sink);
     hipEventRecord(a);
-    k_dma<MODE, M, ACTIVE><<<blocks, 64>>>(d, n, iters, sink);
+    k_dma<MODE, M, ACTIVE, WIN><<<blocks, 64>>>(d, n, iters, sink);
     hipEventRecord(b);
     hipEventSynchronize(b);
     float ms = 0; hipEventElapsedTime(&ms, a, b);
@@ -82,12 +90,12 @@ int main() {
     CHECK(hipMalloc(&d, n * 4));
     CHECK(hipMalloc(&sink, 64));
     CHECK(hipMemset(d, 1, n * 4));
-    for (int w : {4, 8, 12}) {
-        run<1, 16, 64>("lds-dma dwordx4", d, n, sink, w);
-        run<4, 16, 64>("lds-dma dwordx4 5-seg gather", d, n, sink, w);
-        run<5, 16, 64>("lds-dma dwordx4 64MiB window", d, n, sink, w);
-        run<1, 4, 64>("lds-dma dwordx4 M=4", d, n, sink, w);
-        run<0, 4, 64>("lds-dma dword M=4", d, n, sink, w);
+    for (int w : {4, 8, 13, 16}) {
+        run<3, 4, 64>("vgpr dwordx4 1GiB M=4", d, n, sink, w);
+        run<7, 4, 64, (1ull << 20)>("vgpr dwordx4 4MiB win M=4", d, n, sink, w);
+        run<6, 4, 64, (1ull << 20)>("vgpr x4 5-seg 4MiB win M=4", d, n, sink, w);
+        run<6, 4, 64, (1ull << 14)>("vgpr x4 5-seg 64KiB win M=4", d, n, sink, w);
+        run<6, 16, 64, (1ull << 20)>("vgpr x4 5-seg 4MiB win M=16", d, n, sink, w);
     }
     return 0;
 }
