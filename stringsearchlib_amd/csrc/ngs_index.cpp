@@ -2,11 +2,26 @@
 #include "ngs_index.h"
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 
 namespace ngs {
 namespace {
+
+// NGS_BUILD_TIMING=1 prints the host build phases to stderr
+struct PhaseTimer {
+    bool on = std::getenv("NGS_BUILD_TIMING") != nullptr;
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    void mark(const char* what) {
+        if (!on) return;
+        const auto n = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[ngs build] %-22s %8.3f s\n", what, std::chrono::duration<double>(n - t).count());
+        t = n;
+    }
+};
 
 // nGramSearch.h:307-313
 constexpr char kDefaultValid[] = ".%$ @0123456789abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ";
@@ -111,6 +126,7 @@ void build_index(HostIndex& ix, char* const* words, uint64_t size, uint16_t rowS
 
     bool valid[256] = {};
     for (const char* c = kDefaultValid; *c; ++c) valid[(uint8_t)*c] = true;
+    PhaseTimer pt;
 
     Interner terms, keys;
     std::vector<Pair> pairs;
@@ -141,6 +157,7 @@ void build_index(HostIndex& ix, char* const* words, uint64_t size, uint16_t rowS
         }
     }
 
+    pt.mark("parse+intern");
     // (term, key) -> weight, last write wins (tempWeightMap[term][key] = w)
     {
         size_t hs = 16;
@@ -163,6 +180,7 @@ void build_index(HostIndex& ix, char* const* words, uint64_t size, uint16_t rowS
         pairs.resize(nu);
     }
 
+    pt.mark("pair dedup");
     // key ranks: stable counting sort by length keeps first appearance within a length
     ix.n_keys = keys.size();
     std::vector<uint32_t> krank(ix.n_keys);
@@ -214,6 +232,7 @@ void build_index(HostIndex& ix, char* const* words, uint64_t size, uint16_t rowS
         ix.term_off[ix.n_terms] = o;
     }
 
+    pt.mark("keys+terms layout");
     // term -> (key rank, weight) CSR; wildcard weight per key (max of its pairs)
     ix.tk_off.assign((size_t)ix.n_terms + 1, 0);
     for (const Pair& p : pairs) ix.tk_off[tmap[p.term] + 1]++;
@@ -234,6 +253,7 @@ void build_index(HostIndex& ix, char* const* words, uint64_t size, uint16_t rowS
     }
     std::vector<Pair>().swap(pairs);
 
+    pt.mark("term->key CSR");
     // gram CSR over longLib, two passes, term-range parallel (postings stay sorted by term id)
     const uint32_t n_long = ix.n_terms - ix.n_short;
     if (!threads) threads = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
@@ -290,6 +310,7 @@ void build_index(HostIndex& ix, char* const* words, uint64_t size, uint16_t rowS
     });
     counts.clear();
 
+    pt.mark("gram CSR");
     // bucket skip table: for every non-empty list, the offset of its first posting in each of
     // K equal term-id buckets. Lets a query cut its lists into term-id parts with one load per
     // (gram, bucket) instead of a binary search (DESIGN.md §Index layout).
@@ -320,6 +341,7 @@ void build_index(HostIndex& ix, char* const* words, uint64_t size, uint16_t rowS
             out[K] = len;
         }
     });
+    pt.mark("skip table");
     ix.indexed = true;                                                    // hpp:45
 }
 
