@@ -20,6 +20,7 @@
 
 #include <stddef.h>
 #include <stdint.h>
+#include <wchar.h>
 
 #ifdef __cplusplus
 extern "C" {
@@ -79,6 +80,39 @@ NGS_API uint32_t searchBatch(uint32_t handle, const char* const* queries, uint32
                              float threshold, uint32_t limit, uint32_t* counts, char*** results);
 
 /* ------------------------------------------------------------------------------------
+ * Gram-size and wide-string extensions (BASELINE config 4; Readme.md:47,91,135,170,190,208
+ * documents indexW/searchW/releaseW/disposeW/getSizeW/getLibSizeW with a gSize parameter,
+ * but the reference code has neither — parity self-consistent only).
+ * Handles are shared with the narrow API; wchar_t is 4 bytes (UTF-32) on Linux.
+ * Every threshold of the reference scales with g: terms of length >= 2g are gram-indexed,
+ * queries shorter than 3g also run the edit-distance search, queries of <= g characters
+ * scan the whole library, a query of m characters has m - g + 1 grams.
+ * Wide normalisation: code points < 128 follow the byte rules (validChar, toupper);
+ * code points >= 128 are kept as they are; values > 0x10FFFF become spaces.
+ * ------------------------------------------------------------------------------------ */
+
+/* indexN with grams of gSize (1..3) bytes; gSize 3 is indexN. Returns 0 for other gSize. */
+NGS_API uint32_t indexG(char** words, uint64_t size, uint16_t rowSize, float* weight, uint16_t gSize);
+/* Wide index (Readme.md:91): words are NUL-terminated UTF-32 strings; gSize 1..3. */
+NGS_API uint32_t indexW(wchar_t** words, uint64_t size, uint16_t rowSize, float* weight, uint16_t gSize);
+/* Wide search/score (Readme.md:135) on an indexW handle; result strings are index-owned
+ * wchar_t keys. Return 0 on a narrow handle (and the narrow calls return 0 on a wide one). */
+NGS_API uint32_t searchW(uint32_t handle, const wchar_t* query, wchar_t*** results, float threshold,
+                         uint32_t limit);
+NGS_API uint32_t scoreW(uint32_t handle, const wchar_t* query, wchar_t*** results, float** scores,
+                        float threshold, uint32_t limit);
+NGS_API uint32_t scoreBatchW(uint32_t handle, const wchar_t* const* queries, uint32_t nQueries,
+                             float threshold, uint32_t limit, uint32_t* counts, wchar_t*** results,
+                             float** scores);
+NGS_API uint32_t searchBatchW(uint32_t handle, const wchar_t* const* queries, uint32_t nQueries,
+                              float threshold, uint32_t limit, uint32_t* counts, wchar_t*** results);
+/* Readme.md:170,190,208,226 — same meaning as release/dispose/getSize/getLibSize. */
+NGS_API void releaseW(uint32_t handle, wchar_t** results, float* scores);
+NGS_API void disposeW(uint32_t handle);
+NGS_API uint64_t getSizeW(uint32_t handle);
+NGS_API uint64_t getLibSizeW(uint32_t handle);
+
+/* ------------------------------------------------------------------------------------
  * Device-level extensions: inputs and outputs stay in HBM (bench, multi-GPU sharding,
  * host frameworks that already hold device buffers). Not in the reference.
  * ------------------------------------------------------------------------------------ */
@@ -90,11 +124,17 @@ NGS_API int ngsDeviceCount(void);
 
 /* Number of master keys; key ids used by ngsSearchDevice are 0..n-1. */
 NGS_API uint32_t ngsNumKeys(uint32_t handle);
-/* NUL-terminated, index-owned string of key `keyId` (NULL if out of range). */
+/* NUL-terminated, index-owned string of key `keyId` (NULL if out of range or if the
+ * index's character width differs: ngsKey for narrow indexes, ngsKeyW for indexW). */
 NGS_API const char* ngsKey(uint32_t handle, uint32_t keyId);
+NGS_API const wchar_t* ngsKeyW(uint32_t handle, uint32_t keyId);
+/* Character width in bytes (1 or 4) and gram size of the index; 0 for an unknown handle. */
+NGS_API uint32_t ngsCharSize(uint32_t handle);
+NGS_API uint32_t ngsGramSize(uint32_t handle);
 
 /* Scores nQueries queries held on the handle's device: query i is the raw bytes
- * dQueryBytes[dQueryOffsets[i] .. dQueryOffsets[i+1]) (no NUL needed). Writes, for query i,
+ * dQueryBytes[dQueryOffsets[i] .. dQueryOffsets[i+1]) (no NUL needed; for an indexW handle
+ * the bytes are UTF-32 characters and the offsets multiples of 4). Writes, for query i,
  * dCounts[i] results to dKeys/dScores[i*outStride ...]; outStride must be >=
  * min(limit ? limit : 2^31-1, ngsNumKeys). `stream` is a hipStream_t (NULL = the handle's
  * own stream); the call returns when the results are complete on that stream.

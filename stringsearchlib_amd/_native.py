@@ -68,6 +68,36 @@ def lib():
                              C.POINTER(C.POINTER(f32))]
     L.searchBatch.restype = u32
     L.searchBatch.argtypes = [u32, C.POINTER(cp), u32, f32, u32, C.POINTER(u32), C.POINTER(PP)]
+    # wide / gram-size extensions: wchar_t is 4 bytes on Linux, bound as uint32 units
+    W = C.POINTER(C.c_uint32)
+    PW = C.POINTER(W)
+    L.indexG.restype = u32
+    L.indexG.argtypes = [C.POINTER(cp), u64, C.c_uint16, C.POINTER(f32), C.c_uint16]
+    L.indexW.restype = u32
+    L.indexW.argtypes = [C.POINTER(W), u64, C.c_uint16, C.POINTER(f32), C.c_uint16]
+    L.searchW.restype = u32
+    L.searchW.argtypes = [u32, W, C.POINTER(PW), f32, u32]
+    L.scoreW.restype = u32
+    L.scoreW.argtypes = [u32, W, C.POINTER(PW), C.POINTER(C.POINTER(f32)), f32, u32]
+    L.scoreBatchW.restype = u32
+    L.scoreBatchW.argtypes = [u32, C.POINTER(W), u32, f32, u32, C.POINTER(u32), C.POINTER(PW),
+                              C.POINTER(C.POINTER(f32))]
+    L.searchBatchW.restype = u32
+    L.searchBatchW.argtypes = [u32, C.POINTER(W), u32, f32, u32, C.POINTER(u32), C.POINTER(PW)]
+    L.releaseW.restype = None
+    L.releaseW.argtypes = [u32, PW, C.POINTER(f32)]
+    L.disposeW.restype = None
+    L.disposeW.argtypes = [u32]
+    L.getSizeW.restype = u64
+    L.getSizeW.argtypes = [u32]
+    L.getLibSizeW.restype = u64
+    L.getLibSizeW.argtypes = [u32]
+    L.ngsKeyW.restype = C.c_void_p
+    L.ngsKeyW.argtypes = [u32, u32]
+    L.ngsCharSize.restype = u32
+    L.ngsCharSize.argtypes = [u32]
+    L.ngsGramSize.restype = u32
+    L.ngsGramSize.argtypes = [u32]
     L.ngsSetDevice.restype = C.c_int
     L.ngsSetDevice.argtypes = [C.c_int]
     L.ngsDeviceCount.restype = C.c_int

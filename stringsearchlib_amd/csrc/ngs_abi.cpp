@@ -162,6 +162,18 @@ bool upload(Library& L) {
               dev_upload(&wild_w, H.wild_w, L.owned) && dev_upload(&gram_row, H.gram_row, L.owned) &&
               dev_upload(&skip, H.skip, L.owned);
     if (!ok) return false;
+    uint64_t* ghash_key = nullptr;
+    uint32_t* ghash_val = nullptr;
+    if (H.gram_mode == 1 && !(dev_upload(&ghash_key, H.ghash_key, L.owned) && dev_upload(&ghash_val, H.ghash_val, L.owned)))
+        return false;
+    X.gsz = H.gsz;
+    X.csize = H.csize;
+    X.gram_mode = H.gram_mode;
+    X.short_query_len = H.short_query_len;
+    X.full_scan_len = H.full_scan_len;
+    X.ghash_bits = H.ghash_bits;
+    X.ghash_key = ghash_key;
+    X.ghash_val = ghash_val;
     if (!dev_alloc(&wild_key, H.n_keys)) return false;
     L.owned.push_back(wild_key);
     if (!dev_alloc(&wild_score, H.n_keys)) return false;
@@ -191,6 +203,8 @@ bool upload(Library& L) {
     std::vector<uint32_t>().swap(H.tk_off);
     std::vector<uint2>().swap(H.tk);
     std::vector<float>().swap(H.wild_w);
+    std::vector<uint64_t>().swap(H.ghash_key);
+    std::vector<uint32_t>().swap(H.ghash_val);
     return true;
 }
 
@@ -277,7 +291,7 @@ int device_search(Library& L, Context& c, const uint8_t* d_raw, const uint64_t* 
     st.queries = B;
     if (!HIP_CHECK(hipMemsetAsync(c.d_stats, 0, sizeof(DevStats), s))) return -4;
     if (timing) HIP_CHECK(hipEventRecord(c.ev[0], s));
-    if (!HIP_CHECK(launch_prep(d_raw, d_off, B, P, c.d_norm, c.d_qm, s))) return -4;
+    if (!HIP_CHECK(launch_prep(d_raw, d_off, B, P, c.d_norm, c.d_qm, L.dev.csize, s))) return -4;
     if (timing) HIP_CHECK(hipEventRecord(c.ev[1], s));
     if (!HIP_CHECK(hipMemsetAsync(c.d_gcount, 0, 2 * sizeof(uint32_t), s))) return -4;
     if (timing) HIP_CHECK(hipEventRecord(c.ev[2], s));
@@ -337,9 +351,19 @@ uint32_t effective_limit(const Library& L, uint32_t limit) {
     return std::min<uint32_t>(limit, L.host.n_keys);
 }
 
-// Host entry: scores n queries; fills counts and flat (key, score) vectors.
-bool host_search(Library& L, const char* const* queries, uint32_t nq, float thr, uint32_t limit,
+template <typename CharT>
+size_t str_len(const CharT* p) {
+    size_t n = 0;
+    while (p[n]) ++n;
+    return n;
+}
+
+// Host entry: scores n queries (characters of the index's width); fills counts and flat
+// (key, score) vectors.
+template <typename CharT>
+bool host_search(Library& L, const CharT* const* queries, uint32_t nq, float thr, uint32_t limit,
                  std::vector<uint32_t>& counts, std::vector<uint32_t>& keys, std::vector<float>& scores) {
+    constexpr size_t cs = sizeof(CharT);
     counts.assign(nq, 0);
     keys.clear();
     scores.clear();
@@ -357,7 +381,7 @@ bool host_search(Library& L, const char* const* queries, uint32_t nq, float thr,
         const uint32_t B = (uint32_t)std::min<size_t>(max_chunk, nq - q0);
         c->h_off.resize(B + 1);
         c->h_off[0] = 0;
-        for (uint32_t i = 0; i < B; ++i) c->h_off[i + 1] = c->h_off[i] + (queries[q0 + i] ? std::strlen(queries[q0 + i]) : 0);
+        for (uint32_t i = 0; i < B; ++i) c->h_off[i + 1] = c->h_off[i] + (queries[q0 + i] ? str_len(queries[q0 + i]) * cs : 0);
         c->h_raw.resize(std::max<uint64_t>(c->h_off[B], 1));
         for (uint32_t i = 0; i < B; ++i)
             if (queries[q0 + i]) std::memcpy(c->h_raw.data() + c->h_off[i], queries[q0 + i], c->h_off[i + 1] - c->h_off[i]);
@@ -397,34 +421,41 @@ void set_valid(Library& L, const char* chars, int n) {
     std::memcpy(L.valid, v, sizeof(v));
 }
 
-uint32_t marshal(const Library& L, const std::vector<uint32_t>& keys, const std::vector<float>& sc, char*** results,
-                 float** scores) {
+// result strings point into the index's own key storage (valid until dispose, hpp:443-447)
+template <typename CharT>
+uint32_t marshal(const Library& L, const std::vector<uint32_t>& keys, const std::vector<float>& sc,
+                 CharT*** results, float** scores) {
     const size_t n = keys.size();
     if (scores) *scores = new float[n];
-    *results = new char*[n];
+    *results = new CharT*[n];
     for (size_t i = 0; i < n; ++i) {
-        (*results)[i] = const_cast<char*>(L.host.key_bytes.data() + L.host.key_off[keys[i]]);
+        (*results)[i] = reinterpret_cast<CharT*>(const_cast<char*>(L.host.key_bytes.data()) +
+                                                 L.host.key_off[keys[i]] * sizeof(CharT));
         if (scores) (*scores)[i] = sc[i];
     }
     return (uint32_t)n;
 }
 
-uint32_t one_query(uint32_t handle, const char* query, char*** results, float** scores, float thr, uint32_t limit) {
+// A narrow call on a wide index (or the reverse) is answered like an unknown handle.
+template <typename CharT>
+uint32_t one_query(uint32_t handle, const CharT* query, CharT*** results, float** scores, float thr,
+                   uint32_t limit) {
     std::shared_lock<std::shared_mutex> lk(g_lock);
     Library* L = find_lib(handle);
-    if (!L || !L->host.indexed || !query) return 0;  // dllmain.cpp:69, nGramSearch.hpp:417-418
+    if (!L || !L->host.indexed || !query || L->host.csize != sizeof(CharT)) return 0;  // dllmain.cpp:69, hpp:417-418
     std::vector<uint32_t> counts, keys;
     std::vector<float> sc;
     if (!host_search(*L, &query, 1, thr, limit, counts, keys, sc)) return 0;
     return marshal(*L, keys, sc, results, scores);
 }
 
-uint32_t batch_query(uint32_t handle, const char* const* queries, uint32_t nq, float thr, uint32_t limit,
-                     uint32_t* counts, char*** results, float** scores) {
+template <typename CharT>
+uint32_t batch_query(uint32_t handle, const CharT* const* queries, uint32_t nq, float thr, uint32_t limit,
+                     uint32_t* counts, CharT*** results, float** scores) {
     if (counts) std::fill(counts, counts + nq, 0u);
     std::shared_lock<std::shared_mutex> lk(g_lock);
     Library* L = find_lib(handle);
-    if (!L || !L->host.indexed || !queries || !counts) return 0;
+    if (!L || !L->host.indexed || !queries || !counts || L->host.csize != sizeof(CharT)) return 0;
     std::vector<uint32_t> cnt, keys;
     std::vector<float> sc;
     if (!host_search(*L, queries, nq, thr, limit, cnt, keys, sc)) return 0;
@@ -439,7 +470,13 @@ using namespace ngs;
 
 extern "C" {
 
-NGS_API uint32_t indexN(char** words, uint64_t size, uint16_t rowSize, float* weight) {
+}  // extern "C"
+
+namespace ngs {
+namespace {
+// dllmain.cpp:37-59 for every index flavour: smallest free handle, build, upload.
+template <class Build>
+uint32_t new_library(Build&& build) {
     std::unique_lock<std::shared_mutex> lk(g_lock);  // dllmain.cpp:39
     uint32_t handle = 1;                             // dllmain.cpp:41-46
     const uint32_t maxVal = std::numeric_limits<uint32_t>::max();
@@ -447,7 +484,7 @@ NGS_API uint32_t indexN(char** words, uint64_t size, uint16_t rowSize, float* we
     if (handle == maxVal) return 0;
     auto L = std::make_unique<Library>();
     set_valid(*L, kDefaultValid, (int)std::strlen(kDefaultValid));
-    build_index(L->host, words, size, rowSize, weight);
+    build(L->host);
     if (L->host.indexed && !upload(*L)) {
         std::fprintf(stderr, "ngram_search: indexN could not place the index on a GPU\n");
         return 0;
@@ -459,6 +496,27 @@ NGS_API uint32_t indexN(char** words, uint64_t size, uint16_t rowSize, float* we
     }
     g_libs.emplace(handle, std::move(L));
     return handle;
+}
+}  // namespace
+}  // namespace ngs
+
+extern "C" {
+
+NGS_API uint32_t indexN(char** words, uint64_t size, uint16_t rowSize, float* weight) {
+    return new_library([&](HostIndex& H) { build_index(H, words, size, rowSize, weight); });
+}
+
+NGS_API uint32_t indexG(char** words, uint64_t size, uint16_t rowSize, float* weight, uint16_t gSize) {
+    if (gSize < 1 || gSize > kMaxGramSize) return 0;
+    return new_library([&](HostIndex& H) { build_index_g(H, words, size, rowSize, weight, gSize); });
+}
+
+NGS_API uint32_t indexW(wchar_t** words, uint64_t size, uint16_t rowSize, float* weight, uint16_t gSize) {
+    static_assert(sizeof(wchar_t) == 4, "wide strings are UTF-32");
+    if (gSize < 1 || gSize > kMaxGramSize) return 0;
+    return new_library([&](HostIndex& H) {
+        build_index_w(H, reinterpret_cast<const uint32_t* const*>(words), size, rowSize, weight, gSize);
+    });
 }
 
 NGS_API uint32_t search(uint32_t handle, const char* query, char*** results, float threshold, uint32_t limit) {
@@ -510,6 +568,43 @@ NGS_API uint32_t searchBatch(uint32_t handle, const char* const* queries, uint32
     return batch_query(handle, queries, nQueries, threshold, limit, counts, results, nullptr);
 }
 
+// ---- wide (UTF-32 wchar_t) API: Readme.md:91,135,170,190,208,226, keyed by handle like the
+// narrow exports (dllmain.cpp). Valid only on indexW handles; narrow calls on a wide handle
+// and wide calls on a narrow handle return 0 / nothing.
+
+NGS_API uint32_t searchW(uint32_t handle, const wchar_t* query, wchar_t*** results, float threshold,
+                         uint32_t limit) {
+    return one_query(handle, query, results, nullptr, threshold, limit);
+}
+
+NGS_API uint32_t scoreW(uint32_t handle, const wchar_t* query, wchar_t*** results, float** scores,
+                        float threshold, uint32_t limit) {
+    return one_query(handle, query, results, scores, threshold, limit);
+}
+
+NGS_API uint32_t scoreBatchW(uint32_t handle, const wchar_t* const* queries, uint32_t nQueries, float threshold,
+                             uint32_t limit, uint32_t* counts, wchar_t*** results, float** scores) {
+    return batch_query(handle, queries, nQueries, threshold, limit, counts, results, scores);
+}
+
+NGS_API uint32_t searchBatchW(uint32_t handle, const wchar_t* const* queries, uint32_t nQueries, float threshold,
+                              uint32_t limit, uint32_t* counts, wchar_t*** results) {
+    return batch_query(handle, queries, nQueries, threshold, limit, counts, results, nullptr);
+}
+
+NGS_API void releaseW(uint32_t handle, wchar_t** results, float* scores) {
+    std::shared_lock<std::shared_mutex> lk(g_lock);
+    if (!find_lib(handle)) return;
+    delete[] results;
+    delete[] scores;
+}
+
+NGS_API void disposeW(uint32_t handle) { dispose(handle); }
+
+NGS_API uint64_t getSizeW(uint32_t handle) { return getSize(handle); }
+
+NGS_API uint64_t getLibSizeW(uint32_t handle) { return getLibSize(handle); }
+
 NGS_API int ngsSetDevice(int device) {
     int n = 0;
     hipError_t e = hipGetDeviceCount(&n);
@@ -533,8 +628,27 @@ NGS_API uint32_t ngsNumKeys(uint32_t handle) {
 NGS_API const char* ngsKey(uint32_t handle, uint32_t keyId) {
     std::shared_lock<std::shared_mutex> lk(g_lock);
     Library* L = find_lib(handle);
-    if (!L || keyId >= L->host.n_keys) return nullptr;
+    if (!L || keyId >= L->host.n_keys || L->host.csize != 1) return nullptr;
     return L->host.key_bytes.data() + L->host.key_off[keyId];
+}
+
+NGS_API const wchar_t* ngsKeyW(uint32_t handle, uint32_t keyId) {
+    std::shared_lock<std::shared_mutex> lk(g_lock);
+    Library* L = find_lib(handle);
+    if (!L || keyId >= L->host.n_keys || L->host.csize != sizeof(wchar_t)) return nullptr;
+    return reinterpret_cast<const wchar_t*>(L->host.key_bytes.data() + L->host.key_off[keyId] * sizeof(wchar_t));
+}
+
+NGS_API uint32_t ngsCharSize(uint32_t handle) {
+    std::shared_lock<std::shared_mutex> lk(g_lock);
+    Library* L = find_lib(handle);
+    return L ? L->host.csize : 0;
+}
+
+NGS_API uint32_t ngsGramSize(uint32_t handle) {
+    std::shared_lock<std::shared_mutex> lk(g_lock);
+    Library* L = find_lib(handle);
+    return L ? L->host.gsz : 0;
 }
 
 NGS_API int ngsSearchDevice(uint32_t handle, const uint8_t* dQueryBytes, const uint64_t* dQueryOffsets,

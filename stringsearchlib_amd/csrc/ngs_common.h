@@ -23,6 +23,9 @@ constexpr uint32_t kFullScanQueryLen = 3;
 // match. The 21-bit code (c0<<14 | c1<<7 | c2) is therefore a lossless direct index.
 constexpr uint32_t kGramBits = 21;
 constexpr uint32_t kGramSpace = 1u << kGramBits;
+// indexG / indexW: gram sizes 1..3 (a gram of g <= 3 code points packs into 63 bits, the
+// key of the gram dictionary; grams of any other shape than narrow g=3 go through it).
+constexpr uint32_t kMaxGramSize = 3;
 
 // Score encoding shared by every stage: enc = bits(max(w*s, +0.0f)) + 1 for finite
 // non-negative scores (fp32 bits of non-negative floats order like the floats), 0 = "key
@@ -79,7 +82,15 @@ struct DevIndex {  // passed by value to kernels; all pointers are device pointe
     const uint32_t* wild_key;   // wildcard answer, pre-sorted (hpp:356-369)
     const float* wild_score;
     uint32_t n_terms, n_short, n_keys, pad;
+    // gram size and character width (indexG / indexW extensions; 3 and 1 for indexN)
+    uint32_t gsz, csize, gram_mode;         // gram_mode 1: grams via the dictionary below
+    uint32_t short_query_len, full_scan_len; // 3g and g (nGramSearch.hpp:381, :247)
+    uint32_t ghash_bits;
+    const uint64_t* ghash_key;  // dictionary mode: open addressing on packed code points, ~0 = empty
+    const uint32_t* ghash_val;  // -> gram id (row of gram_off / gram_row)
 };
+
+constexpr uint64_t kGramEmpty = ~0ull;
 
 struct SearchParams {
     float thr;

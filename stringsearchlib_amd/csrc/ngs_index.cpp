@@ -91,15 +91,6 @@ private:
 
 struct Pair { uint32_t term, key; float w; };
 
-// escapeBlank (h:93-98) -> trim (h:243-247) -> toUpper (h:72-76); returns the length.
-inline uint32_t normalise_term(const bool* valid, const uint8_t* p, uint32_t n, uint8_t* out) {
-    uint32_t a = 0, b = n;
-    while (a < b && is_space(valid[p[a]] ? p[a] : ' ')) ++a;
-    while (b > a && is_space(valid[p[b - 1]] ? p[b - 1] : ' ')) --b;
-    for (uint32_t i = a; i < b; ++i) out[i - a] = (uint8_t)to_upper(valid[p[i]] ? p[i] : ' ');
-    return b - a;
-}
-
 inline uint32_t gram_code(const uint8_t* s) { return ((uint32_t)s[0] << 14) | ((uint32_t)s[1] << 7) | s[2]; }
 
 // Distinct grams of one term (ngrams[h].insert(id) deduplicates per term, hpp:13-21).
@@ -111,11 +102,99 @@ inline uint32_t term_grams(const uint8_t* s, uint32_t L, uint32_t* g) {
     return (uint32_t)(std::unique(g, g + n) - g);
 }
 
+// ---- character-generic helpers (narrow bytes / wide UTF-32 code points) ----------------
+// Wide strings (indexW) normalise code points below 128 exactly as narrow bytes; code points
+// from 128 are kept as they are (no escaping, no case mapping), except values above 0x10FFFF,
+// which are not code points and become spaces.
+template <typename CharT>
+inline uint32_t str_len(const CharT* p) {
+    uint32_t n = 0;
+    while (p[n]) ++n;
+    return n;
+}
+template <typename CharT>
+inline uint32_t esc_char(const bool* valid, uint32_t c) {
+    if (sizeof(CharT) == 1 || c < 128) return valid[c] ? c : ' ';
+    return c > 0x10FFFFu ? ' ' : c;
+}
+template <typename CharT>
+inline bool space_char(uint32_t c) { return c < 128 && is_space(c); }
+
+// escapeBlank (h:93-98) -> trim (h:243-247) -> toUpper (h:72-76); returns the length.
+template <typename CharT>
+inline uint32_t normalise_t(const bool* valid, const CharT* p, uint32_t n, CharT* out) {
+    uint32_t a = 0, b = n;
+    while (a < b && space_char<CharT>(esc_char<CharT>(valid, p[a]))) ++a;
+    while (b > a && space_char<CharT>(esc_char<CharT>(valid, p[b - 1]))) --b;
+    for (uint32_t i = a; i < b; ++i) {
+        const uint32_t c = esc_char<CharT>(valid, p[i]);
+        out[i - a] = (CharT)(c < 128 ? to_upper(c) : c);
+    }
+    return b - a;
+}
+
+// dictionary-mode gram key: g code points (< 2^21 after normalisation), 21 bits each
+template <typename CharT>
+inline uint64_t gram_key(const CharT* s, uint32_t g) {
+    uint64_t k = 0;
+    for (uint32_t j = 0; j < g; ++j) k = (k << 21) | (uint64_t)(uint32_t)s[j];
+    return k;
+}
+
+// open-addressing set / map of u64 keys (~0 = empty)
+struct U64Map {
+    std::vector<uint64_t> key;
+    std::vector<uint32_t> val;
+    uint32_t bits = 0;
+    size_t n = 0;
+    void init(size_t cap) {
+        bits = 4;
+        while ((size_t(1) << bits) < cap * 2) ++bits;
+        key.assign(size_t(1) << bits, ~0ull);
+        val.assign(size_t(1) << bits, 0);
+        n = 0;
+    }
+    size_t slot(uint64_t k) const { return (size_t)((k * 0x9E3779B97F4A7C15ull) >> (64 - bits)); }
+    bool insert(uint64_t k) {  // true if new
+        if ((n + 1) * 2 > key.size()) grow();
+        size_t i = slot(k), mask = key.size() - 1;
+        while (key[i] != ~0ull) {
+            if (key[i] == k) return false;
+            i = (i + 1) & mask;
+        }
+        key[i] = k;
+        ++n;
+        return true;
+    }
+    uint32_t find(uint64_t k) const {
+        size_t i = slot(k), mask = key.size() - 1;
+        while (key[i] != ~0ull) {
+            if (key[i] == k) return val[i];
+            i = (i + 1) & mask;
+        }
+        return UINT32_MAX;
+    }
+    void grow() {
+        std::vector<uint64_t> old;
+        old.swap(key);
+        init(n * 2 + 16);
+        for (uint64_t k : old)
+            if (k != ~0ull) insert(k);
+    }
+};
+
 }  // namespace
 
-void build_index(HostIndex& ix, char* const* words, uint64_t size, uint16_t rowSize, const float* weight,
-                 unsigned threads) {
+template <typename CharT>
+static void build_impl(HostIndex& ix, const CharT* const* words, uint64_t size, uint16_t rowSize,
+                       const float* weight, uint32_t g, unsigned threads) {
     ix = HostIndex();
+    ix.csize = sizeof(CharT);
+    ix.gsz = g;
+    ix.gram_mode = (sizeof(CharT) == 1 && g == 3) ? 0u : 1u;
+    ix.short_term_len = 2 * g;   // nGramSearch.hpp:82 (6 = 2 x 3)
+    ix.short_query_len = 3 * g;  // hpp:381 (9 = 3 x 3)
+    ix.full_scan_len = g;        // hpp:235,247,266 (3)
     ix.gram_off.assign((size_t)kGramSpace + 1, 0);
     ix.term_off.assign(1, 0);
     ix.tk_off.assign(1, 0);
@@ -128,32 +207,33 @@ void build_index(HostIndex& ix, char* const* words, uint64_t size, uint16_t rowS
     for (const char* c = kDefaultValid; *c; ++c) valid[(uint8_t)*c] = true;
     PhaseTimer pt;
 
-    Interner terms, keys;
+    constexpr uint32_t cs = sizeof(CharT);
+    Interner terms, keys;  // interned as raw bytes (cs per character)
     std::vector<Pair> pairs;
     pairs.reserve(size);
-    std::vector<uint8_t> scratch(256);
+    std::vector<CharT> scratch(256);
     for (uint64_t i = 0; i < size; i += rowSize) {                        // hpp:126
         if (!words[i]) continue;                                          // hpp:129
-        const uint8_t* raw = (const uint8_t*)words[i];
-        uint32_t n = (uint32_t)std::strlen(words[i]), a = 0, b = n;
-        while (a < b && is_space(raw[a])) ++a;                            // trim(strKey), hpp:132
-        while (b > a && is_space(raw[b - 1])) --b;
+        const CharT* raw = words[i];
+        uint32_t n = str_len(raw), a = 0, b = n;
+        while (a < b && space_char<CharT>(raw[a])) ++a;                   // trim(strKey), hpp:132
+        while (b > a && space_char<CharT>(raw[b - 1])) --b;
         if (a == b) continue;                                             // hpp:134
-        const uint8_t* key = raw + a;
+        const CharT* key = raw + a;
         const uint32_t klen = b - a;
         uint32_t kid = UINT32_MAX;
         const uint64_t row_end = std::min<uint64_t>(i + rowSize, size);   // hpp:150 (clamped)
         for (uint64_t j = i; j < row_end; ++j) {
             if (!words[j]) continue;
-            const uint8_t* src = j == i ? key : (const uint8_t*)words[j];
-            uint32_t sl = j == i ? klen : (uint32_t)std::strlen(words[j]);
+            const CharT* src = j == i ? key : words[j];
+            uint32_t sl = j == i ? klen : str_len(words[j]);
             if (sl > scratch.size()) scratch.resize(sl * 2);
-            uint32_t tl = normalise_term(valid, src, sl, scratch.data()); // hpp:136-139, :153-156
+            uint32_t tl = normalise_t<CharT>(valid, src, sl, scratch.data());  // hpp:136-139, :153-156
             if (j != i && tl == 0) continue;                              // hpp:157; a key's own term may be ""
             float w = weight ? weight[j] : 1.0f;                          // hpp:141-143, :159-161
             if (w == 0.0f) continue;                                      // hpp:144, :162
-            if (kid == UINT32_MAX) kid = keys.intern(key, klen);
-            pairs.push_back({terms.intern(scratch.data(), tl), kid, w});  // hpp:146-147, :164-165
+            if (kid == UINT32_MAX) kid = keys.intern((const uint8_t*)key, klen * cs);
+            pairs.push_back({terms.intern((const uint8_t*)scratch.data(), tl * cs), kid, w});  // hpp:146-147, :164-165
         }
     }
 
@@ -195,15 +275,17 @@ void build_index(HostIndex& ix, char* const* words, uint64_t size, uint16_t rowS
             krank[k] = cnt[keys.len(k)]++;
             order[krank[k]] = k;
         }
+        // offsets in characters; each key ends with one NUL character
         ix.key_off.resize((size_t)ix.n_keys + 1);
-        ix.key_bytes.resize(keys.bytes() + ix.n_keys);
+        ix.key_bytes.resize(keys.bytes() + (size_t)ix.n_keys * cs);
         uint64_t o = 0;
         for (uint32_t r = 0; r < ix.n_keys; ++r) {
             uint32_t k = order[r];
             ix.key_off[r] = o;
-            std::memcpy(ix.key_bytes.data() + o, keys.str(k), keys.len(k));
-            o += keys.len(k);
-            ix.key_bytes[o++] = 0;
+            std::memcpy(ix.key_bytes.data() + o * cs, keys.str(k), keys.len(k));
+            o += keys.len(k) / cs;
+            std::memset(ix.key_bytes.data() + o * cs, 0, cs);
+            ++o;
         }
         ix.key_off[ix.n_keys] = o;
     }
@@ -214,20 +296,20 @@ void build_index(HostIndex& ix, char* const* words, uint64_t size, uint16_t rowS
     {
         uint32_t s = 0;
         for (uint32_t t = 0; t < ix.n_terms; ++t)
-            if (terms.len(t) < kShortTermLen) tmap[t] = s++;
+            if (terms.len(t) / cs < ix.short_term_len) tmap[t] = s++;
         ix.n_short = s;
         for (uint32_t t = 0; t < ix.n_terms; ++t)
-            if (terms.len(t) >= kShortTermLen) tmap[t] = s++;
+            if (terms.len(t) / cs >= ix.short_term_len) tmap[t] = s++;
         std::vector<uint32_t> inv(ix.n_terms);
         for (uint32_t t = 0; t < ix.n_terms; ++t) inv[tmap[t]] = t;
         ix.term_off.resize((size_t)ix.n_terms + 1);
         ix.term_bytes.resize(terms.bytes());
         uint64_t o = 0;
-        for (uint32_t r = 0; r < ix.n_terms; ++r) {
+        for (uint32_t r = 0; r < ix.n_terms; ++r) {  // offsets in characters
             uint32_t t = inv[r];
             ix.term_off[r] = o;
-            std::memcpy(ix.term_bytes.data() + o, terms.str(t), terms.len(t));
-            o += terms.len(t);
+            std::memcpy(ix.term_bytes.data() + o * cs, terms.str(t), terms.len(t));
+            o += terms.len(t) / cs;
         }
         ix.term_off[ix.n_terms] = o;
     }
@@ -258,7 +340,6 @@ void build_index(HostIndex& ix, char* const* words, uint64_t size, uint16_t rowS
     const uint32_t n_long = ix.n_terms - ix.n_short;
     if (!threads) threads = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     threads = std::max(1u, std::min<unsigned>(threads, n_long / 4096 + 1));
-    std::vector<std::vector<uint32_t>> counts(threads, std::vector<uint32_t>(kGramSpace, 0));
     auto range = [&](unsigned t, uint32_t& b, uint32_t& e) {
         b = ix.n_short + (uint32_t)((uint64_t)n_long * t / threads);
         e = ix.n_short + (uint32_t)((uint64_t)n_long * (t + 1) / threads);
@@ -268,48 +349,90 @@ void build_index(HostIndex& ix, char* const* words, uint64_t size, uint16_t rowS
         for (unsigned t = 0; t < threads; ++t) th.emplace_back(body, t);
         for (auto& x : th) x.join();
     };
+    const CharT* tchars = reinterpret_cast<const CharT*>(ix.term_bytes.data());
+    // dictionary mode: distinct gram keys -> ids in key order; the device looks them up in an
+    // open-addressing table (ghash)
+    U64Map dict;
+    uint32_t nspace = kGramSpace;
+    if (ix.gram_mode == 1) {
+        std::vector<U64Map> sets(threads);
+        run([&](unsigned t) {
+            uint32_t b, e;
+            range(t, b, e);
+            sets[t].init(1024);
+            for (uint32_t id = b; id < e; ++id) {
+                const uint32_t L = (uint32_t)(ix.term_off[id + 1] - ix.term_off[id]);
+                const CharT* p = tchars + ix.term_off[id];
+                for (uint32_t i = 0; i + g <= L; ++i) sets[t].insert(gram_key(p + i, g));
+            }
+        });
+        std::vector<uint64_t> all;
+        for (auto& st : sets)
+            for (uint64_t k : st.key)
+                if (k != ~0ull) all.push_back(k);
+        sets.clear();
+        std::sort(all.begin(), all.end());
+        all.erase(std::unique(all.begin(), all.end()), all.end());
+        dict.init(all.size() + 1);
+        for (uint32_t i = 0; i < all.size(); ++i) dict.insert(all[i]);
+        for (size_t i = 0; i < dict.key.size(); ++i)
+            if (dict.key[i] != ~0ull)
+                dict.val[i] = (uint32_t)(std::lower_bound(all.begin(), all.end(), dict.key[i]) - all.begin());
+        nspace = (uint32_t)all.size();
+        ix.ghash_key = dict.key;
+        ix.ghash_val = dict.val;
+        ix.ghash_bits = dict.bits;
+    }
+    // distinct grams of one long term (ngrams[h].insert(id) deduplicates per term, hpp:13-21)
+    auto grams_of = [&](uint32_t id, std::vector<uint32_t>& gv) -> uint32_t {
+        const uint32_t L = (uint32_t)(ix.term_off[id + 1] - ix.term_off[id]);
+        if (L > gv.size()) gv.resize(L);
+        if (ix.gram_mode == 0) return term_grams(ix.term_bytes.data() + ix.term_off[id], L, gv.data());
+        const CharT* p = tchars + ix.term_off[id];
+        uint32_t n = 0;
+        for (uint32_t i = 0; i + g <= L; ++i) gv[n++] = dict.find(gram_key(p + i, g));
+        std::sort(gv.begin(), gv.begin() + n);
+        return (uint32_t)(std::unique(gv.begin(), gv.begin() + n) - gv.begin());
+    };
+    ix.gram_off.assign((size_t)nspace + 1, 0);
+    std::vector<std::vector<uint32_t>> counts(threads, std::vector<uint32_t>(nspace, 0));
     run([&](unsigned t) {
         uint32_t b, e;
         range(t, b, e);
-        std::vector<uint32_t> g(64);
+        std::vector<uint32_t> gv(64);
         uint32_t* c = counts[t].data();
         for (uint32_t id = b; id < e; ++id) {
-            uint32_t L = (uint32_t)(ix.term_off[id + 1] - ix.term_off[id]);
-            if (L > g.size()) g.resize(L);
-            uint32_t n = term_grams(ix.term_bytes.data() + ix.term_off[id], L, g.data());
-            for (uint32_t i = 0; i < n; ++i) c[g[i]]++;
+            uint32_t n = grams_of(id, gv);
+            for (uint32_t i = 0; i < n; ++i) c[gv[i]]++;
         }
     });
     {
         uint64_t o = 0;
-        for (uint32_t g = 0; g < kGramSpace; ++g) {
-            ix.gram_off[g] = o;
+        for (uint32_t gi = 0; gi < nspace; ++gi) {
+            ix.gram_off[gi] = o;
             uint64_t tot = 0;
             for (unsigned t = 0; t < threads; ++t) {
-                uint32_t c = counts[t][g];
-                counts[t][g] = (uint32_t)(o + tot);  // becomes this thread's write cursor
+                uint32_t c = counts[t][gi];
+                counts[t][gi] = (uint32_t)(o + tot);  // becomes this thread's write cursor
                 tot += c;
             }
             ix.n_grams += tot != 0;
             o += tot;
         }
-        ix.gram_off[kGramSpace] = o;
+        ix.gram_off[nspace] = o;
         ix.post.resize(o);
     }
     run([&](unsigned t) {
         uint32_t b, e;
         range(t, b, e);
-        std::vector<uint32_t> g(64);
+        std::vector<uint32_t> gv(64);
         uint32_t* cur = counts[t].data();
         for (uint32_t id = b; id < e; ++id) {
-            uint32_t L = (uint32_t)(ix.term_off[id + 1] - ix.term_off[id]);
-            if (L > g.size()) g.resize(L);
-            uint32_t n = term_grams(ix.term_bytes.data() + ix.term_off[id], L, g.data());
-            for (uint32_t i = 0; i < n; ++i) ix.post[cur[g[i]]++] = id - ix.n_short;
+            uint32_t n = grams_of(id, gv);
+            for (uint32_t i = 0; i < n; ++i) ix.post[cur[gv[i]]++] = id - ix.n_short;
         }
     });
     counts.clear();
-
     pt.mark("gram CSR");
     // bucket skip table: for every non-empty list, the offset of its first posting in each of
     // K equal term-id buckets. Lets a query cut its lists into term-id parts with one load per
@@ -317,20 +440,20 @@ void build_index(HostIndex& ix, char* const* words, uint64_t size, uint16_t rowS
     ix.n_buckets = 1;
     while (ix.n_buckets < kMaxBuckets && (uint64_t)ix.n_buckets * kMinBucketTerms < n_long) ix.n_buckets <<= 1;
     ix.bucket_span = n_long ? (n_long + ix.n_buckets - 1) / ix.n_buckets : 1;
-    ix.gram_row.assign(kGramSpace, UINT32_MAX);
+    ix.gram_row.assign(nspace, UINT32_MAX);
     std::vector<uint32_t> rows;
-    for (uint32_t g = 0; g < kGramSpace; ++g)
-        if (ix.gram_off[g + 1] > ix.gram_off[g]) {
-            ix.gram_row[g] = (uint32_t)rows.size();
-            rows.push_back(g);
+    for (uint32_t gi = 0; gi < nspace; ++gi)
+        if (ix.gram_off[gi + 1] > ix.gram_off[gi]) {
+            ix.gram_row[gi] = (uint32_t)rows.size();
+            rows.push_back(gi);
         }
     const uint32_t K = ix.n_buckets;
     ix.skip.assign((size_t)rows.size() * (K + 1), 0);
     run([&](unsigned t) {
         for (size_t r = t; r < rows.size(); r += threads) {
-            const uint32_t g = rows[r];
-            const uint32_t* p = ix.post.data() + ix.gram_off[g];
-            const uint32_t len = (uint32_t)(ix.gram_off[g + 1] - ix.gram_off[g]);
+            const uint32_t gi = rows[r];
+            const uint32_t* p = ix.post.data() + ix.gram_off[gi];
+            const uint32_t len = (uint32_t)(ix.gram_off[gi + 1] - ix.gram_off[gi]);
             uint32_t* out = ix.skip.data() + r * (K + 1);
             uint32_t i = 0;
             for (uint32_t b = 0; b <= K; ++b) {
@@ -343,6 +466,21 @@ void build_index(HostIndex& ix, char* const* words, uint64_t size, uint16_t rowS
     });
     pt.mark("skip table");
     ix.indexed = true;                                                    // hpp:45
+}
+
+void build_index(HostIndex& ix, char* const* words, uint64_t size, uint16_t rowSize, const float* weight,
+                 unsigned threads) {
+    build_impl<uint8_t>(ix, reinterpret_cast<const uint8_t* const*>(words), size, rowSize, weight, 3, threads);
+}
+
+void build_index_g(HostIndex& ix, char* const* words, uint64_t size, uint16_t rowSize, const float* weight,
+                   uint32_t gsz, unsigned threads) {
+    build_impl<uint8_t>(ix, reinterpret_cast<const uint8_t* const*>(words), size, rowSize, weight, gsz, threads);
+}
+
+void build_index_w(HostIndex& ix, const uint32_t* const* words, uint64_t size, uint16_t rowSize,
+                   const float* weight, uint32_t gsz, unsigned threads) {
+    build_impl<uint32_t>(ix, words, size, rowSize, weight, gsz, threads);
 }
 
 void wildcard_order(const HostIndex& ix, std::vector<uint32_t>& keys, std::vector<float>& scores) {

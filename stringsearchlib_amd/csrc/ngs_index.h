@@ -20,9 +20,17 @@ namespace ngs {
 
 struct HostIndex {
     bool indexed = false;                   // nGramSearch.h:301
+    // characters: 1 byte (indexN / indexG) or 4 (indexW, UTF-32); offsets below count characters
+    uint32_t csize = 1, gsz = 3;
+    // 0: gram = 21-bit code of 3 ASCII bytes, direct-indexed; 1: gram dictionary (ghash)
+    uint32_t gram_mode = 0;
+    uint32_t short_term_len = 6, short_query_len = 9, full_scan_len = 3;  // 2g, 3g, g
+    std::vector<uint64_t> ghash_key;        // dictionary mode: open addressing, ~0 = empty
+    std::vector<uint32_t> ghash_val;        // -> gram id (CSR row of gram_off)
+    uint32_t ghash_bits = 0;
     uint32_t n_terms = 0, n_short = 0, n_keys = 0;
     uint64_t n_grams = 0;                   // distinct grams -> getLibSize
-    std::vector<uint64_t> gram_off;         // kGramSpace + 1
+    std::vector<uint64_t> gram_off;         // gram space + 1 (kGramSpace codes, or dictionary ids)
     std::vector<uint32_t> post;
     uint32_t n_buckets = 1, bucket_span = 1; // term-id buckets of the skip table
     std::vector<uint32_t> gram_row;         // kGramSpace: row of the skip table, UINT32_MAX = empty list
@@ -39,6 +47,13 @@ struct HostIndex {
 // Builds the index; `threads` workers for the gram CSR (0 = hardware concurrency).
 void build_index(HostIndex& ix, char* const* words, uint64_t size, uint16_t rowSize, const float* weight,
                  unsigned threads = 0);
+
+// Extensions (BASELINE north_star / README gSize; parity self-consistent):
+// narrow strings with gram size gsz (1..3), and wide UTF-32 strings (indexW).
+void build_index_g(HostIndex& ix, char* const* words, uint64_t size, uint16_t rowSize, const float* weight,
+                   uint32_t gsz, unsigned threads = 0);
+void build_index_w(HostIndex& ix, const uint32_t* const* words, uint64_t size, uint16_t rowSize,
+                   const float* weight, uint32_t gsz, unsigned threads = 0);
 
 // Wildcard answer: keys sorted by (wild_w desc, rank asc).
 void wildcard_order(const HostIndex& ix, std::vector<uint32_t>& keys, std::vector<float>& scores);

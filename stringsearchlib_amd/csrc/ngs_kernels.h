@@ -10,7 +10,7 @@ namespace ngs {
 // Normalise every query (escapeBlank -> trim -> toUpper, nGramSearch.hpp:372-376) into
 // qnorm (same offsets as the raw bytes) and its length into qm (kQueryWildcard for ""/"*").
 hipError_t launch_prep(const uint8_t* raw, const uint64_t* off, uint32_t B, const SearchParams& P,
-                       uint8_t* qnorm, uint32_t* qm, hipStream_t s);
+                       uint8_t* qnorm, uint32_t* qm, uint32_t cs, hipStream_t s);
 
 // Fused per-query kernel: short Levenshtein scan of shortLib (4 <= m < 9), 3-gram posting
 // count in an LDS hash table per term-id part, threshold, term->key weighting, per-key max

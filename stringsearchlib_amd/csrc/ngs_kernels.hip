@@ -47,25 +47,35 @@ __device__ __forceinline__ unsigned dev_upper(unsigned c) { return (c >= 'a' && 
 __device__ __forceinline__ unsigned esc(const uint32_t* valid, unsigned c) {
     return ((valid[c >> 5] >> (c & 31u)) & 1u) ? c : 32u;  // escapeBlank
 }
+// Characters are bytes (indexN / indexG) or UTF-32 code points (indexW): cs = 1 or 4. Wide code
+// points below 128 are escaped like bytes; from 128 they are kept, except non-code-points
+// (> 0x10FFFF), which become spaces.
+__device__ __forceinline__ unsigned esc_cs(const uint32_t* valid, uint32_t c, uint32_t cs) {
+    return (cs == 1 || c < 128u) ? esc(valid, c) : (c > 0x10FFFFu ? 32u : c);
+}
+__device__ __forceinline__ uint32_t char_at(const uint8_t* base, uint64_t i, uint32_t cs) {
+    return cs == 4 ? reinterpret_cast<const uint32_t*>(base)[i] : (uint32_t)base[i];
+}
 
 // ---------------------------------------------------------------- normalisation ------
 // One wave per query: ballots find the first / last byte that survives escape + trim.
 __global__ __launch_bounds__(64) void k_prep(const uint8_t* __restrict__ raw, const uint64_t* __restrict__ off,
                                              uint32_t B, SearchParams P, uint8_t* __restrict__ qnorm,
-                                             uint32_t* __restrict__ qm) {
+                                             uint32_t* __restrict__ qm, uint32_t cs) {
     const uint32_t q = blockIdx.x;
     if (q >= B) return;
     const uint32_t lane = threadIdx.x;
-    const uint64_t b = off[q];
-    const uint64_t n = off[q + 1] - b;
-    if (n == 0 || (n == 1 && raw[b] == '*')) {  // wildcard, nGramSearch.hpp:356
+    const uint8_t* rq = raw + off[q];        // query q: characters of cs bytes from byte offset off[q]
+    uint8_t* nq = qnorm + off[q];
+    const uint64_t n = (off[q + 1] - off[q]) / cs;
+    if (n == 0 || (n == 1 && char_at(rq, 0, cs) == '*')) {  // wildcard, nGramSearch.hpp:356
         if (lane == 0) qm[q] = kQueryWildcard;
         return;
     }
     uint64_t first = n, last = 0;
     for (uint64_t base = 0; base < n; base += 64) {
         const uint64_t i = base + lane;
-        const bool keep = i < n && !dev_space(esc(P.valid, raw[b + i]));
+        const bool keep = i < n && !dev_space(esc_cs(P.valid, char_at(rq, i, cs), cs));
         const unsigned long long bal = __ballot(keep);
         if (bal) { first = base + __ffsll((long long)bal) - 1; break; }
     }
@@ -75,42 +85,46 @@ __global__ __launch_bounds__(64) void k_prep(const uint8_t* __restrict__ raw, co
     }
     for (uint64_t base = 0; base < n; base += 64) {
         const uint64_t i = n - 1 - (base + lane);
-        const bool keep = base + lane < n && !dev_space(esc(P.valid, raw[b + i]));
+        const bool keep = base + lane < n && !dev_space(esc_cs(P.valid, char_at(rq, i, cs), cs));
         const unsigned long long bal = __ballot(keep);
         if (bal) { last = n - 1 - (base + __ffsll((long long)bal) - 1); break; }
     }
     const uint64_t m = last - first + 1;
-    for (uint64_t i = lane; i < m; i += 64) qnorm[b + i] = (uint8_t)dev_upper(esc(P.valid, raw[b + first + i]));
+    for (uint64_t i = lane; i < m; i += 64) {
+        const uint32_t c = dev_upper(esc_cs(P.valid, char_at(rq, first + i, cs), cs));
+        if (cs == 4) reinterpret_cast<uint32_t*>(nq)[i] = c; else nq[i] = (uint8_t)c;
+    }
     if (lane == 0) qm[q] = (uint32_t)(m > 0xFFFFFFF0ull ? 0xFFFFFFF0ull : m);
 }
 
 // ---------------------------------------------------------------- shared helpers -----
 // libStr = escapeBlank(key); trim; libStr == query (nGramSearch.hpp:330-334: the key is NOT
 // upper-cased, so only keys already in query form promote).
-__device__ bool key_equals_query(const DevIndex& X, uint32_t k, const uint8_t* q, uint32_t m,
+__device__ bool key_equals_query(const DevIndex& X, uint32_t k, const void* q, uint32_t qcs, uint32_t m,
                                  const uint32_t* valid) {
+    const uint32_t cs = X.csize;
     uint64_t a = X.key_off[k], e = X.key_off[k + 1] - 1;  // drop the NUL
-    while (a < e && dev_space(esc(valid, X.key_bytes[a]))) ++a;
-    while (e > a && dev_space(esc(valid, X.key_bytes[e - 1]))) --e;
+    while (a < e && dev_space(esc_cs(valid, char_at(X.key_bytes, a, cs), cs))) ++a;
+    while (e > a && dev_space(esc_cs(valid, char_at(X.key_bytes, e - 1, cs), cs))) --e;
     if (e - a != m) return false;
     for (uint32_t i = 0; i < m; ++i)
-        if (esc(valid, X.key_bytes[a + i]) != q[i]) return false;
+        if (esc_cs(valid, char_at(X.key_bytes, a + i, cs), cs) != char_at((const uint8_t*)q, i, qcs)) return false;
     return true;
 }
 
 // calcScore's per-pair value (nGramSearch.hpp:326-335) as an order-preserving encoding.
 __device__ __forceinline__ uint32_t pair_enc(uint2 kw, float s, bool promo_possible, const DevIndex& X,
-                                             const uint8_t* q, uint32_t m, const uint32_t* valid) {
+                                             const void* q, uint32_t qcs, uint32_t m, const uint32_t* valid) {
     const float sc = __uint_as_float(kw.y) * s;
     uint32_t enc = sc > 0.0f ? __float_as_uint(sc) + 1u : 1u;  // std::max(w*s, 0.0f) (entry default)
-    if (promo_possible && key_equals_query(X, kw.x, q, m, valid)) enc = kPromoted;
+    if (promo_possible && key_equals_query(X, kw.x, q, qcs, m, valid)) enc = kPromoted;
     return enc;
 }
 
 // stringMatch (nGramSearch.hpp:182-222): min over source substrings of the edit distance to
 // q (m <= 8); returns m - distance. Column DP over the query held in registers.
-__device__ __forceinline__ uint32_t string_match(const uint8_t (&qc)[8], uint32_t m, const uint8_t* s,
-                                                 uint32_t L) {
+template <typename TT>
+__device__ __forceinline__ uint32_t string_match_t(const uint32_t (&qc)[8], uint32_t m, const TT* s, uint32_t L) {
     uint32_t col[9];
 #pragma unroll
     for (int i = 0; i <= 8; ++i) col[i] = (uint32_t)i;
@@ -129,6 +143,35 @@ __device__ __forceinline__ uint32_t string_match(const uint8_t (&qc)[8], uint32_
         }
     }
     return m - best;
+}
+// term t of the index against the query (m <= 8 characters in qc)
+__device__ __forceinline__ uint32_t string_match(const uint32_t (&qc)[8], uint32_t m, const DevIndex& X, uint32_t t) {
+    const uint64_t a = X.term_off[t], b = X.term_off[t + 1];
+    if (X.csize == 4) return string_match_t(qc, m, reinterpret_cast<const uint32_t*>(X.term_bytes) + a, (uint32_t)(b - a));
+    return string_match_t(qc, m, X.term_bytes + a, (uint32_t)(b - a));
+}
+
+// Gram of the query characters at position i (accessor qf), as a row of the gram space:
+// the 21-bit code of three ASCII bytes (indexN), or the dictionary id of the g packed code
+// points (indexG / indexW). UINT32_MAX: the gram is in no term of the index.
+template <class QF>
+__device__ __forceinline__ uint32_t gram_at(const DevIndex& X, QF qf, uint32_t i) {
+    if (X.gram_mode == 0) {
+        const uint32_t c0 = qf(i), c1 = qf(i + 1), c2 = qf(i + 2);
+        return ((c0 | c1 | c2) & ~0x7Fu) ? UINT32_MAX : (c0 << 14) | (c1 << 7) | c2;
+    }
+    uint64_t key = 0;
+    for (uint32_t j = 0; j < X.gsz; ++j) {
+        const uint32_t c = qf(i + j);
+        if (c > 0x1FFFFFu) return UINT32_MAX;
+        key = (key << 21) | c;
+    }
+    const uint64_t mask = (1ull << X.ghash_bits) - 1;
+    for (uint64_t h = (key * 0x9E3779B97F4A7C15ull) >> (64 - X.ghash_bits);; h = (h + 1) & mask) {
+        const uint64_t k = X.ghash_key[h];
+        if (k == key) return X.ghash_val[h];
+        if (k == kGramEmpty) return UINT32_MAX;
+    }
 }
 
 // ---------------------------------------------------------------- fused kernel -------
@@ -224,7 +267,7 @@ __device__ __forceinline__ bool emit_pending(EmitState& st, FastSmem& S, const D
                                              uint32_t m, const uint32_t* valid) {
     while (st.p < st.pe) {
         const uint2 kw = X.tk[st.p];
-        const uint32_t enc = pair_enc(kw, st.s, st.promo, X, S.q, m, valid);
+        const uint32_t enc = pair_enc(kw, st.s, st.promo, X, S.q, 1u, m, valid);
         const uint64_t rec = ((uint64_t)(~enc) << 32) | kw.x;
         if (rec < tau) {
             const uint32_t idx = atomicAdd(&S.cand_n, 1u);
@@ -396,7 +439,8 @@ __device__ void fast_one(const uint32_t q, FastSmem& S, const DevIndex& X, const
         if (tid == 0) out_n[q] = 0;
         return;
     }
-    if (m <= kFullScanQueryLen || m - 2 > kFastMaxGrams || L > kFastMaxLimit) {
+    // tier 2 handles indexN libraries (3-grams of bytes) only; indexG / indexW go to the general path
+    if (m <= kFullScanQueryLen || m - 2 > kFastMaxGrams || L > kFastMaxLimit || X.gram_mode != 0) {
         if (tid == 0) glist[atomicAdd(gcount, 1u)] = q;  // library-wide path
         return;
     }
@@ -419,15 +463,14 @@ __device__ void fast_one(const uint32_t q, FastSmem& S, const DevIndex& X, const
 
     // ---- searchShort over shortLib (nGramSearch.hpp:262-270), 4 <= m < 9 ----
     if (m < kShortQueryLen && X.n_short) {
-        uint8_t qc[8];
+        uint32_t qc[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) qc[i] = (uint32_t)i < m ? S.q[i] : 0;
         uint32_t t = tid;
         const float fm = (float)m;
         produce(S, X, P, m, L, &stats->errors, [&](EmitState& st) -> int {
             if (t >= X.n_short) return 0;
-            const uint64_t a = X.term_off[t], b = X.term_off[t + 1];
-            const uint32_t match = string_match(qc, m, X.term_bytes + a, (uint32_t)(b - a));
+            const uint32_t match = string_match(qc, m, X, t);
             const float s = (float)match / fm;  // nGramSearch.hpp:244
             const uint32_t id = t;
             t += kFastThreads;
@@ -634,7 +677,7 @@ struct alignas(16) WaveSmem {
     uint32_t surv_t[kWaveSurv];      // survivor terms
     uint32_t cbuf[64];               // sketch candidates (terms)
     uint8_t surv_c[kWaveSurv];       // hit count, | 0x80 for a Levenshtein (short search) match count
-    uint8_t q[kWaveMaxGrams + 8];
+    uint32_t q[kWaveMaxGrams + 8];   // normalised query, one code point per entry
     uint32_t surv_total;             // stats
     uint32_t ncand;                  // sketch candidates of the part, all waves
     uint32_t x_surv_n, x_cand_n;     // wave 0's emit state, handed round in exact-path turns
@@ -644,7 +687,6 @@ struct alignas(16) WaveSmem {
 
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
 
-__device__ __forceinline__ unsigned long long lanes_below() { return (1ull << lane_id()) - 1ull; }
 // popcount of the ballot bits of the lanes below this one (v_mbcnt_lo/hi)
 __device__ __forceinline__ uint32_t rank_below(unsigned long long b) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
@@ -794,7 +836,7 @@ __device__ void wave_emit(WaveSmem<W>& S, const DevIndex& X, const SearchParams&
             uint64_t rec = kNoCand;
             if (p < pe) {
                 const uint2 kw = X.tk[p++];
-                const uint32_t enc = pair_enc(kw, s, promo, X, S.q, m, P.valid);
+                const uint32_t enc = pair_enc(kw, s, promo, X, S.q, 4u, m, P.valid);
                 rec = ((uint64_t)(~enc) << 32) | kw.x;
             }
             if (cand_n + 64 > (uint32_t)kWaveCand) wave_flush(S, cand_n, tau, L);
@@ -1140,18 +1182,18 @@ __global__ __launch_bounds__(64 * W, kWaveWavesPerSimd) void k_wave(DevIndex X, 
         if (tid == 0) out_n[q] = 0;
         return;
     }
-    if (m <= kFullScanQueryLen || m - 2 > kWaveMaxGrams || L > kWaveMaxLimit) {
+    if (m <= X.full_scan_len || m - X.gsz + 1 > kWaveMaxGrams || L > kWaveMaxLimit) {
         if (tid == 0) list2[atomicAdd(count2, 1u)] = q;  // tier 2 / library-wide path
         return;
     }
-    const uint32_t n = m - 2;
+    const uint32_t n = m - X.gsz + 1;  // grams of the query (hpp:29-36; 3-grams: m - 2)
     const uint32_t n_long = X.n_terms - X.n_short;
 #ifdef NGS_PHASE_STAMPS
     unsigned long long wt_ = __builtin_amdgcn_s_memtime();
     unsigned long long wacc_[16] = {};
 #endif
     const uint8_t* qg = qnorm + qoff[q];
-    for (uint32_t i = tid; i < m; i += 64 * W) S.q[i] = qg[i];
+    for (uint32_t i = tid; i < m; i += 64 * W) S.q[i] = char_at(qg, i, X.csize);
     if (tid == 0) {
         S.surv_total = 0;
         S.ncand = 0;
@@ -1170,8 +1212,8 @@ __global__ __launch_bounds__(64 * W, kWaveWavesPerSimd) void k_wave(DevIndex X, 
     const float sc_short = lane <= m ? (float)lane / (float)m : 0.0f;
 
     // ---- searchShort over shortLib (nGramSearch.hpp:262-270), 4 <= m < 9, wave 0 ----
-    if (wid == 0 && m < kShortQueryLen && X.n_short) {
-        uint8_t qc[8];
+    if (wid == 0 && m < X.short_query_len && X.n_short) {
+        uint32_t qc[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) qc[i] = (uint32_t)i < m ? S.q[i] : 0;
         const unsigned long long okm = __ballot(lane <= m && !(sc_short < P.thr));  // hpp:315
@@ -1180,10 +1222,7 @@ __global__ __launch_bounds__(64 * W, kWaveWavesPerSimd) void k_wave(DevIndex X, 
             if (surv_n + 64 > (uint32_t)kWaveSurv) wave_emit(S, X, P, m, L, sc_long, sc_short, surv_n, cand_n, tau);
             const uint32_t t = t0 + lane;
             uint32_t match = 0;
-            if (t < X.n_short) {
-                const uint64_t a = X.term_off[t], b = X.term_off[t + 1];
-                match = string_match(qc, m, X.term_bytes + a, (uint32_t)(b - a));
-            }
+            if (t < X.n_short) match = string_match(qc, m, X, t);
             surv_append(S, t < X.n_short && match >= cmin_s, t, match | 0x80u, surv_n);
         }
     }
@@ -1197,9 +1236,8 @@ __global__ __launch_bounds__(64 * W, kWaveWavesPerSimd) void k_wave(DevIndex X, 
     uint32_t glen = 0, grow = 0;
     bool have = false;
     if (lane < n) {
-        const uint32_t c0 = S.q[lane], c1 = S.q[lane + 1], c2 = S.q[lane + 2];
-        if (!((c0 | c1 | c2) & 0x80u)) {
-            const uint32_t code = (c0 << 14) | (c1 << 7) | c2;
+        const uint32_t code = gram_at(X, [&](uint32_t i) { return S.q[i]; }, lane);
+        if (code != UINT32_MAX) {
             gbase = X.gram_off[code];
             glen = (uint32_t)(X.gram_off[code + 1] - gbase);
             grow = X.gram_row[code];
@@ -1432,7 +1470,7 @@ __device__ __forceinline__ void emit_global(const DevIndex& X, uint32_t t, float
     const bool promo = (double)s > 0.999;
     for (uint32_t p = X.tk_off[t]; p < X.tk_off[t + 1]; ++p) {
         const uint2 kw = X.tk[p];
-        atomicMax(&kenc[kw.x], pair_enc(kw, s, promo, X, q, m, valid));
+        atomicMax(&kenc[kw.x], pair_enc(kw, s, promo, X, q, X.csize, m, valid));
     }
 }
 
@@ -1441,17 +1479,16 @@ __global__ __launch_bounds__(256) void k_gen_long(DevIndex X, SearchParams P, co
                                                   const uint32_t* __restrict__ group, uint32_t* __restrict__ cnt,
                                                   uint32_t* __restrict__ kenc, int phase) {
     const uint32_t gi = blockIdx.y, q = group[gi], m = qm[q];
-    if (m == kQueryWildcard || m < 3) return;  // nGramSearch.hpp:281
-    const uint32_t n = m - 2, n_long = X.n_terms - X.n_short;
+    if (m == kQueryWildcard || m < X.gsz) return;  // nGramSearch.hpp:281
+    const uint32_t n = m - X.gsz + 1, n_long = X.n_terms - X.n_short;
     const uint8_t* qs = qnorm + qoff[q];
     uint32_t* C = cnt + (size_t)gi * n_long;
     uint32_t* K = kenc + (size_t)gi * X.n_keys;
     const uint64_t me = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (uint64_t)gridDim.x * blockDim.x;
     const float fn = (float)n;
     for (uint32_t i = 0; i < n; ++i) {
-        const uint32_t c0 = qs[i], c1 = qs[i + 1], c2 = qs[i + 2];
-        if ((c0 | c1 | c2) & 0x80u) continue;
-        const uint32_t g = (c0 << 14) | (c1 << 7) | c2;
+        const uint32_t g = gram_at(X, [&](uint32_t j) { return char_at(qs, j, X.csize); }, i);
+        if (g == UINT32_MAX) continue;
         const uint64_t a = X.gram_off[g], b = X.gram_off[g + 1];
         for (uint64_t p = a + me; p < b; p += stride) {
             const uint32_t t = X.post[p];
@@ -1472,17 +1509,16 @@ __global__ __launch_bounds__(256) void k_gen_short(DevIndex X, SearchParams P, c
                                                    const uint64_t* __restrict__ qoff, const uint32_t* __restrict__ qm,
                                                    const uint32_t* __restrict__ group, uint32_t* __restrict__ kenc) {
     const uint32_t gi = blockIdx.y, q = group[gi], m = qm[q];
-    if (m == kQueryWildcard || m == 0 || m >= kShortQueryLen) return;
-    const uint32_t end = m <= kFullScanQueryLen ? X.n_terms : X.n_short;  // nGramSearch.hpp:247
+    if (m == kQueryWildcard || m == 0 || m >= X.short_query_len) return;
+    const uint32_t end = m <= X.full_scan_len ? X.n_terms : X.n_short;  // nGramSearch.hpp:247
     const uint8_t* qs = qnorm + qoff[q];
-    uint8_t qc[8];
+    uint32_t qc[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) qc[i] = (uint32_t)i < m ? qs[i] : 0;
+    for (int i = 0; i < 8; ++i) qc[i] = (uint32_t)i < m ? char_at(qs, i, X.csize) : 0;
     uint32_t* K = kenc + (size_t)gi * X.n_keys;
     const float fm = (float)m;
     for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < end; t += gridDim.x * blockDim.x) {
-        const uint64_t a = X.term_off[t], b = X.term_off[t + 1];
-        const float s = (float)string_match(qc, m, X.term_bytes + a, (uint32_t)(b - a)) / fm;
+        const float s = (float)string_match(qc, m, X, t) / fm;
         if (!(s < P.thr)) emit_global(X, t, s, qs, m, P.valid, K);
     }
 }
@@ -1576,9 +1612,9 @@ int phase_stats(unsigned long long* out, int n, bool reset) {
 }
 
 hipError_t launch_prep(const uint8_t* raw, const uint64_t* off, uint32_t B, const SearchParams& P, uint8_t* qnorm,
-                       uint32_t* qm, hipStream_t s) {
+                       uint32_t* qm, uint32_t cs, hipStream_t s) {
     if (!B) return hipSuccess;
-    hipLaunchKernelGGL(k_prep, dim3(B), dim3(64), 0, s, raw, off, B, P, qnorm, qm);
+    hipLaunchKernelGGL(k_prep, dim3(B), dim3(64), 0, s, raw, off, B, P, qnorm, qm, cs);
     return hipGetLastError();
 }
 

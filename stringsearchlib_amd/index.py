@@ -20,22 +20,48 @@ def _b(s) -> bytes:
 
 
 class StringIndex:
-    def __init__(self, words, row_size: int = 1, weights=None, device: int | None = None):
+    """One index of byte strings. gram_size 3 is the reference (indexN); 1 or 2 use the indexG
+    extension (every reference threshold scaled by the gram size)."""
+
+    def __init__(self, words, row_size: int = 1, weights=None, device: int | None = None, gram_size: int = 3):
         L = _native.lib()
         if device is not None:
             rc = L.ngsSetDevice(device)
             if rc:
                 raise RuntimeError(f"ngsSetDevice({device}) failed: {rc}")
         n = len(words)
-        arr = (C.c_char_p * max(1, n))()
-        for i, w in enumerate(words):
-            arr[i] = None if w is None else _b(w)
         w = None
         if weights is not None:
             w = (C.c_float * max(1, len(weights)))(*weights)
-        self.handle = L.indexN(arr if n else None, n, row_size, w)
+        self._keep = self._words(words)  # alive during the build only
+        self.handle = self._index(L, self._keep if n else None, n, row_size, w, gram_size)
+        self._keep = None
         if not self.handle:
-            raise RuntimeError("indexN failed (no usable GPU?) — see stderr")
+            raise RuntimeError(f"{self._INDEX} failed (no usable GPU, or gram_size not in 1..3?) — see stderr")
+
+    # -- per-width plumbing (overridden by WideStringIndex) ------------------------------
+    _INDEX = "indexN"
+
+    @staticmethod
+    def _words(words):
+        arr = (C.c_char_p * max(1, len(words)))()
+        for i, w in enumerate(words):
+            arr[i] = None if w is None else _b(w)
+        return arr
+
+    @staticmethod
+    def _index(L, arr, n, row_size, w, gram_size):
+        if gram_size == 3:
+            return L.indexN(arr, n, row_size, w)
+        return L.indexG(arr, n, row_size, w, gram_size)
+
+    _q = staticmethod(_b)
+    _string = staticmethod(C.string_at)
+    _RES = C.POINTER(C.POINTER(C.c_char))
+    _fn = {"search": "search", "score": "score", "release": "release", "scoreBatch": "scoreBatch", "key": "ngsKey"}
+
+    def _queries(self, queries):
+        return (C.c_char_p * max(1, len(queries)))(*[_b(q) for q in queries])
 
     # -- reference exports -------------------------------------------------------------
     def size(self) -> int:
@@ -50,45 +76,46 @@ class StringIndex:
 
     def score(self, query, threshold: float = 0.0, limit: int = 100):
         """dllmain.cpp:82: list of (key bytes, fp32 score), best first."""
-        L = _native.lib()
-        res = C.POINTER(C.POINTER(C.c_char))()
+        L, f = _native.lib(), self._fn
+        res = self._RES()
         sc = C.POINTER(C.c_float)()
-        n = L.score(self.handle, _b(query), C.byref(res), C.byref(sc), threshold, limit)
+        n = getattr(L, f["score"])(self.handle, self._q(query), C.byref(res), C.byref(sc), threshold, limit)
         if not n:
             if res:
-                L.release(self.handle, res, sc)
+                getattr(L, f["release"])(self.handle, res, sc)
             return []
-        out = [(C.string_at(res[i]), sc[i]) for i in range(n)]
-        L.release(self.handle, res, sc)
+        out = [(self._string(res[i]), sc[i]) for i in range(n)]
+        getattr(L, f["release"])(self.handle, res, sc)
         return out
 
     def search(self, query, threshold: float = 0.0, limit: int = 100):
         """dllmain.cpp:61: list of key bytes, best first."""
-        L = _native.lib()
-        res = C.POINTER(C.POINTER(C.c_char))()
-        n = L.search(self.handle, _b(query), C.byref(res), threshold, limit)
-        out = [C.string_at(res[i]) for i in range(n)]
+        L, f = _native.lib(), self._fn
+        res = self._RES()
+        n = getattr(L, f["search"])(self.handle, self._q(query), C.byref(res), threshold, limit)
+        out = [self._string(res[i]) for i in range(n)]
         if res:
-            L.release(self.handle, res, None)
+            getattr(L, f["release"])(self.handle, res, None)
         return out
 
     def score_batch(self, queries, threshold: float = 0.0, limit: int = 100):
         """scoreBatch: one list of (key, score) per query."""
-        L = _native.lib()
+        L, f = _native.lib(), self._fn
         nq = len(queries)
-        qs = (C.c_char_p * max(1, nq))(*[_b(q) for q in queries])
+        qs = self._queries(queries)
         counts = (C.c_uint32 * max(1, nq))()
-        res = C.POINTER(C.POINTER(C.c_char))()
+        res = self._RES()
         sc = C.POINTER(C.c_float)()
-        total = L.scoreBatch(self.handle, qs, nq, threshold, limit, counts, C.byref(res), C.byref(sc))
+        total = getattr(L, f["scoreBatch"])(self.handle, qs, nq, threshold, limit, counts, C.byref(res),
+                                            C.byref(sc))
         out, o = [], 0
         for i in range(nq):
             c = counts[i]
-            out.append([(C.string_at(res[o + j]), sc[o + j]) for j in range(c)])
+            out.append([(self._string(res[o + j]), sc[o + j]) for j in range(c)])
             o += c
         assert o == total
         if res:
-            L.release(self.handle, res, sc)
+            getattr(L, f["release"])(self.handle, res, sc)
         return out
 
     def dispose(self) -> None:
@@ -106,11 +133,14 @@ class StringIndex:
     def num_keys(self) -> int:
         return _native.lib().ngsNumKeys(self.handle)
 
-    def key(self, key_id: int) -> bytes:
-        p = _native.lib().ngsKey(self.handle, key_id)
+    def key(self, key_id: int):
+        p = getattr(_native.lib(), self._fn["key"])(self.handle, key_id)
         if not p:
             raise IndexError(key_id)
-        return C.string_at(p)
+        return self._string(p)
+
+    def gram_size(self) -> int:
+        return _native.lib().ngsGramSize(self.handle)
 
     def set_timing(self, enable: bool = True) -> None:
         _native.lib().ngsSetTiming(self.handle, int(enable))
@@ -127,3 +157,71 @@ class StringIndex:
                                            d_counts, d_keys, d_scores, stream or None)
         if rc:
             raise RuntimeError(f"ngsSearchDevice failed: {rc}")
+
+
+# ---- wide strings (indexW extension) ---------------------------------------------------
+_U32P = C.POINTER(C.c_uint32)
+
+
+def _u32(s):
+    """str (one unit per code point) or a sequence of ints -> NUL-terminated uint32 array."""
+    units = [ord(c) for c in s] if isinstance(s, str) else [int(c) & 0xFFFFFFFF for c in s]
+    return (C.c_uint32 * (len(units) + 1))(*units, 0)
+
+
+def _wstring(p) -> str:
+    """NUL-terminated UTF-32 string at p -> str (raises on units above 0x10FFFF)."""
+    u = C.cast(p, _U32P)
+    out = []
+    i = 0
+    while u[i]:
+        out.append(chr(u[i]))
+        i += 1
+    return "".join(out)
+
+
+class WideStringIndex(StringIndex):
+    """indexW / searchW / scoreW (Readme.md:91,135): UTF-32 strings (Python str, or sequences
+    of ints for raw code units such as values above 0x10FFFF), gram_size 1..3."""
+
+    _INDEX = "indexW"
+    _RES = C.POINTER(_U32P)
+    _fn = {"search": "searchW", "score": "scoreW", "release": "releaseW", "scoreBatch": "scoreBatchW",
+           "key": "ngsKeyW"}
+
+    def __init__(self, words, row_size: int = 1, weights=None, device: int | None = None, gram_size: int = 2):
+        super().__init__(words, row_size, weights, device, gram_size)
+
+    @staticmethod
+    def _words(words):
+        arrs = [None if w is None else _u32(w) for w in words]
+        arr = (_U32P * max(1, len(words)))(*[None if a is None else C.cast(a, _U32P) for a in arrs])
+        arr._arrs = arrs  # keep the strings alive with the pointer array
+        return arr
+
+    @staticmethod
+    def _index(L, arr, n, row_size, w, gram_size):
+        return L.indexW(arr, n, row_size, w, gram_size)
+
+    @staticmethod
+    def _q(query):
+        return C.cast(_u32(query), _U32P)
+
+    _string = staticmethod(_wstring)
+
+    def _queries(self, queries):
+        arrs = [_u32(q) for q in queries]
+        arr = (_U32P * max(1, len(queries)))(*[C.cast(a, _U32P) for a in arrs])
+        arr._arrs = arrs
+        return arr
+
+    def size(self) -> int:
+        return _native.lib().getSizeW(self.handle)
+
+    def lib_size(self) -> int:
+        return _native.lib().getLibSizeW(self.handle)
+
+    def dispose(self) -> None:
+        if self.handle:
+            _native.lib().disposeW(self.handle)
+            self.handle = 0

@@ -68,3 +68,27 @@ def test_unbuilt_library_without_gpu_work():
     finally:
         L.dispose(h)
     assert L.getSize(h) == 0
+
+
+def test_wide_and_gram_size_entry_points_without_gpu_work():
+    """indexG / indexW validate gSize (1..3) and, like indexN, give an un-built handle for a
+    library of < 2 words; width-mismatched or un-built searches answer 0."""
+    L = _native.lib()
+    words = (C.c_char_p * 1)(b"ONLY")
+    assert L.indexG(words, 1, 1, None, 0) == 0 and L.indexG(words, 1, 1, None, 4) == 0
+    U = C.POINTER(C.c_uint32)
+    w0 = (C.c_uint32 * 5)(*map(ord, "ONLY"), 0)
+    wwords = (U * 1)(C.cast(w0, U))
+    assert L.indexW(wwords, 1, 1, None, 0) == 0
+    h = L.indexW(wwords, 1, 1, None, 2)
+    assert h
+    try:
+        assert L.ngsCharSize(h) == 4 and L.ngsGramSize(h) == 2
+        assert L.getSizeW(h) == 0 and L.getLibSizeW(h) == 0
+        res = C.POINTER(U)()
+        assert L.searchW(h, C.cast(w0, U), C.byref(res), 0.0, 10) == 0 and not res
+        nres = C.POINTER(C.POINTER(C.c_char))()
+        assert L.search(h, b"ONLY", C.byref(nres), 0.0, 10) == 0 and not nres
+    finally:
+        L.disposeW(h)
+    assert L.ngsCharSize(h) == 0
