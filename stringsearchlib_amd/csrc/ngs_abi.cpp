@@ -120,7 +120,7 @@ struct Library {
         if (!HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking))) return nullptr;
         for (hipEvent_t& e : c->ev)
             if (!HIP_CHECK(hipEventCreate(&e))) return nullptr;
-        if (!dev_alloc(&c->d_gcount, 2) || !dev_alloc(&c->d_group, 64) || !dev_alloc(&c->d_stats, 1)) return nullptr;
+        if (!dev_alloc(&c->d_gcount, 2) || !dev_alloc(&c->d_group, 64) || !dev_alloc(&c->d_stats, kStatSlots)) return nullptr;
         return c;
     }
     void give_back(std::unique_ptr<Context> c) {
@@ -289,7 +289,7 @@ int device_search(Library& L, Context& c, const uint8_t* d_raw, const uint64_t* 
     const bool timing = L.timing.load();
     ngs_stats st{};
     st.queries = B;
-    if (!HIP_CHECK(hipMemsetAsync(c.d_stats, 0, sizeof(DevStats), s))) return -4;
+    if (!HIP_CHECK(hipMemsetAsync(c.d_stats, 0, sizeof(DevStats) * kStatSlots, s))) return -4;
     if (timing) HIP_CHECK(hipEventRecord(c.ev[0], s));
     if (!HIP_CHECK(launch_prep(d_raw, d_off, B, P, c.d_norm, c.d_qm, L.dev.csize, s))) return -4;
     if (timing) HIP_CHECK(hipEventRecord(c.ev[1], s));
@@ -321,10 +321,18 @@ int device_search(Library& L, Context& c, const uint8_t* d_raw, const uint64_t* 
         }
         if (timing) HIP_CHECK(hipEventRecord(c.ev[5], s));
     }
-    DevStats ds{};
-    if (!HIP_CHECK(hipMemcpyAsync(&ds, c.d_stats, sizeof(ds), hipMemcpyDeviceToHost, s)) ||
+    DevStats slots[kStatSlots], ds{};
+    if (!HIP_CHECK(hipMemcpyAsync(slots, c.d_stats, sizeof(slots), hipMemcpyDeviceToHost, s)) ||
         !HIP_CHECK(hipStreamSynchronize(s)))
         return -4;
+    for (const DevStats& x : slots) {
+        ds.postings += x.postings;
+        ds.lists += x.lists;
+        ds.results += x.results;
+        ds.fast += x.fast;
+        ds.survivors += x.survivors;
+        ds.errors |= x.errors;
+    }
     if (ds.errors) {
         std::fprintf(stderr, "ngram_search: fused kernel reported internal error 0x%x\n", ds.errors);
         return -5;

@@ -50,22 +50,48 @@ constexpr uint32_t kMaxBuckets = 256;
 constexpr uint32_t kMinBucketTerms = 4096;
 
 // ---- wave kernel geometry (tier 1: one wave per query) ----
-constexpr int kWaveSlotBits = 11;
-constexpr int kWaveSlots = 1 << kWaveSlotBits;  // wave-private LDS hash table
+#ifndef NGS_SLOT_BITS
+#define NGS_SLOT_BITS 10   // experiment builds override (make variant VFLAGS=-DNGS_SLOT_BITS=11)
+#endif
+#ifndef NGS_SKETCH_CAP
+#define NGS_SKETCH_CAP 1024
+#endif
+constexpr int kWaveSlotBits = NGS_SLOT_BITS;
+constexpr int kWaveSlots = 1 << kWaveSlotBits;  // wave-private LDS table (u32 words)
 constexpr int kWaveCap = kWaveSlots / 2;        // entries per exact-count pass (<= 50 % table load)
-constexpr int kSketchCap = kWaveCap;            // entries per sketch part (u8 counters, 4 per word: 8 cells per entry)
+constexpr int kSketchCellBits = 4;              // sketch counters: u4, 8 per table word
+constexpr uint32_t kSketchMax = (1u << kSketchCellBits) - 1u;
+constexpr int kSketchCap = NGS_SKETCH_CAP;      // entries per sketch part (<= 1/8 of the cells)
+static_assert(kSketchCap * 8 <= kWaveSlots * (32 / kSketchCellBits), "sketch load");
 constexpr int kWaveCand = 256;                  // candidate buffer per query
 constexpr uint32_t kWaveMaxLimit = kWaveCand / 2;
 constexpr int kWaveChunks = kSketchCap / 4;     // 16-byte chunks per part and wave (sketch parts)
-constexpr int kExactChunks = kWaveCap / 4;      // ... for parts counted exactly (cmin <= 2)
+constexpr int kExactChunks = (kWaveCap < kSketchCap ? kWaveCap : kSketchCap) / 4;  // ... parts counted exactly (cmin <= 2)
 constexpr int kDmaRounds = kWaveChunks / 64;    // dwordx4 loads per lane for one part
-constexpr int kWaveWavesPerSimd = 4;            // occupancy target: <= 128 VGPRs
+#ifndef NGS_WPS
+#define NGS_WPS 4
+#endif
+constexpr int kWaveWavesPerSimd = NGS_WPS;      // occupancy target: 4 -> <= 128 VGPRs
 constexpr uint32_t kDefaultWaves = 1;           // waves per query in the tier-1 kernel
 constexpr int kWaveTarget = kWaveCap * 5 / 8;   // postings per exact part the bucket grouping aims at
 constexpr int kSketchTarget = kSketchCap * 5 / 8;  // ... per sketch part
 constexpr uint32_t kStray = 0xFFFFFFFFu;        // staged entry outside its list segment
 constexpr int kWaveSurv = 128;                  // survivor list (term, count) before calcScore
-constexpr uint32_t kWaveMaxGrams = 63;          // counts <= 63: one lane per count value
+constexpr uint32_t kWaveMaxGrams = 63;
+#ifndef NGS_BND
+#define NGS_BND 0  // 1: preload part boundaries to LDS (measured slower: occupancy)
+#endif
+constexpr bool kBndOn = NGS_BND != 0;
+#ifndef NGS_SINGLE
+#define NGS_SINGLE 0  // 1: one register buffer per part (no prefetch of the next part; fewer VGPRs)
+#endif
+constexpr bool kSingleBuf = NGS_SINGLE != 0;
+#ifndef NGS_SK2
+#define NGS_SK2 2     // smallest cmin counted by the sketch (below: exact hash counting)
+#endif
+constexpr uint32_t kSketchMinCmin = NGS_SK2;
+constexpr int kBndLists = 16;                   // part boundaries preloaded to LDS for queries of <= 16 lists
+constexpr int kBndParts = 48;                   // ... and <= 48 bucket groups          // counts <= 63: one lane per count value
 
 struct DevIndex {  // passed by value to kernels; all pointers are device pointers
     const uint64_t* gram_off;   // [kGramSpace + 1] -> post
@@ -105,7 +131,10 @@ struct SearchParams {
 // per-query normalised length sentinels written by the prep kernel
 constexpr uint32_t kQueryWildcard = 0xFFFFFFFFu;
 
-struct DevStats {  // accumulated by the fused kernel (one atomic per block)
+// Statistics are accumulated into kStatSlots cache-line slots (query q adds to slot q % kStatSlots)
+// and summed on the host: 65,536 queries adding into one line serialised at one memory channel.
+constexpr uint32_t kStatSlots = 256;
+struct alignas(64) DevStats {  // accumulated by the fused kernel (one atomic per query, per slot)
     unsigned long long postings;
     unsigned long long lists;
     unsigned long long results;

@@ -633,11 +633,12 @@ __device__ void fast_one(const uint32_t q, FastSmem& S, const DevIndex& X, const
     }
     if (tid == 0) {
         out_n[q] = nres;
-        atomicAdd(&stats->postings, (unsigned long long)p_total);
-        atomicAdd(&stats->lists, (unsigned long long)ng);
-        atomicAdd(&stats->results, (unsigned long long)nres);
-        atomicAdd(&stats->fast, 1ull);
-        atomicAdd(&stats->survivors, (unsigned long long)S.survivors);
+        DevStats* sl = stats + (q & (kStatSlots - 1));
+        atomicAdd(&sl->postings, (unsigned long long)p_total);
+        atomicAdd(&sl->lists, (unsigned long long)ng);
+        atomicAdd(&sl->results, (unsigned long long)nres);
+        atomicAdd(&sl->fast, 1ull);
+        atomicAdd(&sl->survivors, (unsigned long long)S.survivors);
     }
     STAMP(11);
 }
@@ -670,7 +671,7 @@ __global__ __launch_bounds__(kFastThreads) void k_fast(DevIndex X, SearchParams 
 // occurrence), which is the reference's multiplicity (hpp:289-298).
 template <int W>
 struct alignas(16) WaveSmem {
-    uint32_t table[kWaveSlots * W];  // exact: (term - lo + 1) << 8 | count; sketch: 2 x u16 counters
+    uint32_t table[kWaveSlots * W];  // exact: (term - lo + 1) << 8 | count; sketch: 8 x u4 counters
     uint64_t cand[kWaveCand];        // (~enc) << 32 | key
     uint2 segtab[W][64];             // staging, per wave: per list {first chunk - position, first | end entry << 16}
     uint8_t mark[W][kWaveChunks];    // staging, per wave: list index + 1 at the (wave-local) position of its first chunk
@@ -678,6 +679,7 @@ struct alignas(16) WaveSmem {
     uint32_t cbuf[64];               // sketch candidates (terms)
     uint8_t surv_c[kWaveSurv];       // hit count, | 0x80 for a Levenshtein (short search) match count
     uint32_t q[kWaveMaxGrams + 8];   // normalised query, one code point per entry
+    uint32_t bnd[kBndOn ? kBndLists * (kBndParts + 1) : 1];  // part boundaries: [g * (kBndParts + 1) + j] = skip[row of list g][min(K, j * w)]
     uint32_t surv_total;             // stats
     uint32_t ncand;                  // sketch candidates of the part, all waves
     uint32_t x_surv_n, x_cand_n;     // wave 0's emit state, handed round in exact-path turns
@@ -889,8 +891,8 @@ __device__ __forceinline__ uint32_t wave_insert_slot(uint32_t* T, uint32_t rel, 
 // sketch cell of a term: full-rate shift/xor (v_mul_lo_u32 is quarter rate). Term ids of a part
 // are spread over a range much wider than the table, and consecutive ids get distinct cells.
 template <int W>
-__device__ __forceinline__ uint32_t sketch_cell(uint32_t t) {  // u8 counter index: 4 per table word
-    constexpr uint32_t kBits = kWaveSlotBits + 2 + (W == 4 ? 2 : W == 2 ? 1 : 0);
+__device__ __forceinline__ uint32_t sketch_cell(uint32_t t) {  // u4 counter index: 8 per table word
+    constexpr uint32_t kBits = kWaveSlotBits + 3 + (W == 4 ? 2 : W == 2 ? 1 : 0);
     return (t ^ (t >> kBits)) & ((1u << kBits) - 1u);
 }
 
@@ -906,7 +908,7 @@ __device__ __forceinline__ uint32_t sketch_cell(uint32_t t) {  // u8 counter ind
 template <int W>
 __device__ __forceinline__ uint32_t stage_part(WaveSmem<W>& S, const uint4* __restrict__ post4, uint64_t gbase,
                                                uint32_t a0, uint32_t cur, uint32_t len,
-                                               uint4 (&v)[kDmaRounds], uint32_t& vmask) {
+                                               uint4 (&v)[kDmaRounds], uint32_t& vmask, uint32_t dbg = 0) {
     const uint32_t lane = lane_id(), wid = W == 1 ? 0u : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t head = (a0 + cur) & 3u;
     const uint32_t nch = len ? (head + len + 3) >> 2 : 0u;
@@ -952,7 +954,11 @@ __device__ __forceinline__ uint32_t stage_part(WaveSmem<W>& S, const uint4* __re
             const uint2 seg = S.segtab[wid][(scn[r] - 1u) & 63u];
             // inactive lanes must not load: a shared fallback address would be read by every wave
             // of the GPU and serialise on one L2 channel
-            if (ok) v[r] = post4[seg.x + c];
+            if (ok && !(dbg & 8u)) v[r] = post4[seg.x + c];  // dbg 8: staging without the loads
+            else if (ok) {  // random-looking term ids (no repeats) in place of the loaded ones
+                const uint32_t hsh = (c + 0x9E3779B9u * (uint32_t)(gbase + cur)) * 0x85EBCA6Bu;
+                v[r] = make_uint4(hsh >> 8, (hsh * 0xC2B2AE35u) >> 8, (hsh * 0x27D4EB2Fu) >> 8, (hsh * 0x165667B1u) >> 8);
+            }
             // entries [lo_e, hi_e) of this chunk are in the list segment [y, z)
             const int y = (int)(seg.y & 0xFFFFu), z = (int)(seg.y >> 16);
             const uint32_t lo_e = (uint32_t)min(max(y - (int)(4 * c), 0), 4);
@@ -1050,11 +1056,13 @@ __device__ __forceinline__ void part_exact(WaveSmem<W>& S, uint4 (&v)[kDmaRounds
     }
 }
 
-// Sketch count of a part held in registers (cmin >= 3; all waves): 4 x u8 counters per shared
-// table word, never an undercount (an increment that wraps a counter past 255 is seen in the
-// value the atomic returns and sends the part to exact counting). Entries whose cell reaches cmin are candidates; wave 0 gets
-// their exact counts by comparing the <= 64 candidates with each other. Returns the number of
-// candidate entries; above 64 the caller counts the part exactly (the table is clean again).
+// Sketch count of a part held in registers (3 <= cmin <= 15; all waves): 8 x u4 counters per shared
+// table word, never an undercount (an increment that wraps a counter past 15 is seen in the
+// value the atomic returns and sends the part to exact counting). Entries whose cell reaches cmin
+// are candidates; wave 0 gets their exact counts by comparing the <= 64 candidates with each
+// other. Returns the number of candidate entries; above 64 the caller counts the part exactly
+// (the table is clean again). (u16 counters with no-return adds were measured: the 4x fewer
+// cells per KB cost more in false candidates than the returns cost in waits.)
 template <int W>
 __device__ __forceinline__ uint32_t part_sketch(WaveSmem<W>& S, const uint4 (&v)[kDmaRounds], uint32_t vmask,
                                                 uint32_t mt, uint32_t cmin, uint32_t n_short, uint32_t n_terms,
@@ -1069,9 +1077,9 @@ __device__ __forceinline__ uint32_t part_sketch(WaveSmem<W>& S, const uint4 (&v)
 #pragma unroll
             for (uint32_t e = 0; e < 4; ++e) {
                 const uint32_t c = sketch_cell<W>(t[e]);
-                const uint32_t sh = (c & 3u) << 3;
-                const uint32_t old = atomicAdd(&S.table[c >> 2], ((vmask >> (4 * r + e)) & 1u) << sh);
-                ovf |= ((old >> sh) & 0xFFu) == 0xFFu;
+                const uint32_t sh = (c & 7u) << 2;
+                const uint32_t old = atomicAdd(&S.table[c >> 3], ((vmask >> (4 * r + e)) & 1u) << sh);
+                ovf |= ((old >> sh) & kSketchMax) == kSketchMax;
             }
         }
     }
@@ -1091,11 +1099,11 @@ __device__ __forceinline__ uint32_t part_sketch(WaveSmem<W>& S, const uint4 (&v)
             const uint32_t t[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
             uint32_t w[4];
 #pragma unroll
-            for (uint32_t e = 0; e < 4; ++e) w[e] = S.table[sketch_cell<W>(t[e]) >> 2];
+            for (uint32_t e = 0; e < 4; ++e) w[e] = S.table[sketch_cell<W>(t[e]) >> 3];
 #pragma unroll
             for (uint32_t e = 0; e < 4; ++e) {
                 const uint32_t c = sketch_cell<W>(t[e]);
-                cm |= (((w[e] >> ((c & 3u) << 3)) & 0xFFu) >= cmin ? 1u : 0u) << (4 * r + e);
+                cm |= (((w[e] >> ((c & 7u) << 2)) & kSketchMax) >= cmin ? 1u : 0u) << (4 * r + e);
             }
         }
     }
@@ -1262,24 +1270,47 @@ __global__ __launch_bounds__(64 * W, kWaveWavesPerSimd) void k_wave(DevIndex X, 
     const uint64_t p_total = wave_sum((uint64_t)glen);
     const unsigned long long pm = __ballot(lane <= n && lane > 0 && !(sc_long < P.thr));  // hpp:315
     const uint32_t cmin = pm ? (uint32_t)(__ffsll((long long)pm) - 1) : 1000u;
-    const bool sketch = cmin >= 3;
+    // sketch counting for 2 <= cmin <= 15; at cmin 2 two colliding entries already make a false
+    // candidate, so those parts are cut at half the size
+    const bool sketch = cmin >= kSketchMinCmin && cmin <= kSketchMax;
+    const uint32_t shrink = cmin == 2 ? 1u : 0u;
     // part cap: a sketch part holds twice the entries of an exact pass (u8 vs u32 cells)
-    const uint32_t kChunks = (sketch ? (uint32_t)kWaveChunks : (uint32_t)kExactChunks) * W;
+    const uint32_t kChunks = ((sketch ? (uint32_t)kWaveChunks : (uint32_t)kExactChunks) * W) >> shrink;
     WSTAMP(1);
     if (p_total && cmin <= n) {
         const uint32_t K = X.n_buckets, span = X.bucket_span;
         const uint32_t wmax = (uint32_t)max64(1, min64(K, kMaxPartSpan / max(span, 1u)));
-        const uint32_t w = (uint32_t)max64(1, min64(wmax, (uint64_t)K * (sketch ? kSketchTarget : kWaveTarget) * W / p_total));
+        const uint32_t w = (uint32_t)max64(1, min64(wmax, (uint64_t)K * ((sketch ? kSketchTarget : kWaveTarget) >> shrink) * W / p_total));
         const uint32_t* sk = X.skip + (size_t)grow * (K + 1);
         const uint4* post4 = reinterpret_cast<const uint4*>(X.post);
         const uint32_t a0 = (uint32_t)gbase & 3u;  // list start within its 16-byte chunk
         // entries [s, e) of this lane's list cover 16-byte chunks [(a0 + s) / 4, (a0 + e + 3) / 4)
         auto chunks = [a0](uint32_t s, uint32_t e) -> uint32_t { return e > s ? ((a0 + e + 3) >> 2) - ((a0 + s) >> 2) : 0u; };
+        // part boundaries: the skip-table entries at every w-th bucket of every list, loaded once
+        // per query (one strided load per list) into LDS, so that planning a part never waits on
+        // a dependent global load (that latency, paid per part, was most of the loop time)
+        const uint32_t nb = (K + w - 1) / w + 1;  // boundaries j = 0 .. nb-1 at bucket min(K, j * w)
+        const bool pre = kBndOn && W == 1 && ng <= (uint32_t)kBndLists && nb <= (uint32_t)kBndParts + 1;
+        if (pre) {  // LDS-DMA: lane j's dword lands at row g, column j (no VGPRs, one wait)
+            for (uint32_t g = 0; g < ng; ++g) {
+                const uint32_t row = __builtin_amdgcn_readlane(grow, g);
+                if (lane < nb)
+                    __builtin_amdgcn_global_load_lds(X.skip + (size_t)row * (K + 1) + min(K, lane * w),
+                                                     (__attribute__((address_space(3))) void*)(S.bnd + g * (kBndParts + 1)),
+                                                     4, 0, 0);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            wave_sync();
+        }
+        // end of the next bucket part (group jn + 1): skip[row][min(K, (jn + 1) * w)]; idle lanes load
+        // nothing (a shared row would be a hot spot)
+        auto next_end = [&](uint32_t bn, uint32_t jn) -> uint32_t {
+            return pre ? S.bnd[lane * (kBndParts + 1) + min(jn + 1, nb - 1)] : sk[min(K, bn + w)];
+        };
         // part iterator: buckets [bnext, bnext + w) unless they exceed kChunks, then term-id sub-parts
-        uint32_t cur = 0, bnext = 0;
-        // end of the next bucket part; idle lanes load nothing (a shared row would be a hot spot)
+        uint32_t cur = 0, bnext = 0, jnext = 0;  // jnext = bnext / w
         uint32_t e_pre = 0;
-        if (lane < ng) e_pre = sk[min(K, w)];
+        if (lane < ng) e_pre = next_end(0, 0);
         uint32_t in_sub = 0;
         uint32_t sub_lo = 0, hi_lim = 0, sub_end = 0, sub_bnext = 0, step = 1;
         // software pipeline in registers: part i+1's loads are in flight while part i is counted
@@ -1289,17 +1320,28 @@ __global__ __launch_bounds__(64 * W, kWaveWavesPerSimd) void k_wave(DevIndex X, 
 #pragma unroll
         for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) pv[r] = make_uint4(0, 0, 0, 0);
         for (uint32_t guard = 0;;) {
+            // the part to count: the one staged last iteration (double buffer), or with a single
+            // buffer the one staged below in this iteration
             uint4 cv[kDmaRounds];
+            uint32_t c_vm = 0, c_mt = 0, c_lo = 0, c_hi = 0;
+            bool have_c = false;
+            auto take = [&]() {
 #pragma unroll
-            for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) cv[r] = pv[r];
-            const uint32_t c_vm = p_vm, c_mt = p_mt, c_lo = p_lo, c_hi = p_hi;
-            const bool have_c = have_p;
+                for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) cv[r] = pv[r];
+                c_vm = p_vm;
+                c_mt = p_mt;
+                c_lo = p_lo;
+                c_hi = p_hi;
+                have_c = have_p;
+            };
+            if constexpr (!kSingleBuf) take();
             WSTAMP(2);
             // ---- next part: [lo, ...) with per-lane segments [gbase + cur, gbase + cur + len) ----
             uint32_t lo = 0, hi_t = 0, len = 0;  // part: term ids [lo, hi_t)
             have_p = false;
             in_sub = __builtin_amdgcn_readfirstlane(in_sub);
             bnext = __builtin_amdgcn_readfirstlane(bnext);
+            jnext = __builtin_amdgcn_readfirstlane(jnext);
             // common case, straight-line: the next group of w buckets is non-empty and fits
             // (span * w <= kMaxPartSpan holds by the choice of w)
             bool fast = false;
@@ -1310,8 +1352,9 @@ __global__ __launch_bounds__(64 * W, kWaveWavesPerSimd) void k_wave(DevIndex X, 
                     lo = bnext * span;
                     len = e - cur;
                     bnext = min(K, bnext + w);
+                    ++jnext;
                     hi_t = (uint32_t)min64((uint64_t)bnext * span, n_long);
-                    if (lane < ng) e_pre = sk[min(K, bnext + w)];
+                    if (lane < ng) e_pre = next_end(bnext, jnext);
                     have_p = true;
                     fast = true;
                 }
@@ -1320,6 +1363,7 @@ __global__ __launch_bounds__(64 * W, kWaveWavesPerSimd) void k_wave(DevIndex X, 
                 // loop-carried part state is wave-uniform: keep it in SGPRs
                 guard = __builtin_amdgcn_readfirstlane(guard);
                 bnext = __builtin_amdgcn_readfirstlane(bnext);
+                jnext = __builtin_amdgcn_readfirstlane(jnext);
                 sub_lo = __builtin_amdgcn_readfirstlane(sub_lo);
                 step = __builtin_amdgcn_readfirstlane(step);
                 if (++guard > 8u * K + 4096u) {
@@ -1334,8 +1378,9 @@ __global__ __launch_bounds__(64 * W, kWaveWavesPerSimd) void k_wave(DevIndex X, 
                         lo = bnext * span;
                         len = e - cur;
                         bnext = bhi;
+                        ++jnext;
                         hi_t = (uint32_t)min64((uint64_t)bhi * span, n_long);
-                        if (lane < ng) e_pre = sk[min(K, bnext + w)];
+                        if (lane < ng) e_pre = next_end(bnext, jnext);
                         if (tot) { have_p = true; break; }
                         continue;
                     }
@@ -1372,7 +1417,8 @@ __global__ __launch_bounds__(64 * W, kWaveWavesPerSimd) void k_wave(DevIndex X, 
                 if (sub_lo >= hi_lim) {
                     in_sub = 0;
                     bnext = sub_bnext;
-                    if (lane < ng) e_pre = sk[min(K, bnext + w)];
+                    ++jnext;
+                    if (lane < ng) e_pre = next_end(bnext, jnext);
                 }
                 if (t2) { have_p = true; break; }
                 cur = a;
@@ -1381,12 +1427,13 @@ __global__ __launch_bounds__(64 * W, kWaveWavesPerSimd) void k_wave(DevIndex X, 
             have_p = __builtin_amdgcn_readfirstlane(have_p ? 1u : 0u) != 0;  // uniform: scalar loop exit
             // ---- part i+1: issue this wave's loads ----
             if (have_p) {
-                p_mt = stage_part(S, post4, gbase, a0, cur, len, pv, p_vm);
+                p_mt = stage_part(S, post4, gbase, a0, cur, len, pv, p_vm, P.dbg);
                 p_lo = lo;
                 p_hi = hi_t;
                 cur += len;
             }
             WSTAMP(4);
+            if constexpr (kSingleBuf) take();
             // ---- count part i while part i+1 is in flight ----
             if (have_c && !(P.dbg & 1u)) {  // dbg 1: load only, no counting
                 if (wid == 0 && surv_n + 64 > (uint32_t)kWaveSurv)
@@ -1449,13 +1496,14 @@ __global__ __launch_bounds__(64 * W, kWaveWavesPerSimd) void k_wave(DevIndex X, 
         out_k[ob + i] = (uint32_t)r;
         out_s[ob + i] = enc == kPromoted ? 100.0f : __uint_as_float(enc - 1u);
     }
-    if (lane == 0) {
-        out_n[q] = cand_n;
-        atomicAdd(&stats->postings, (unsigned long long)p_total);
-        atomicAdd(&stats->lists, (unsigned long long)ng);
-        atomicAdd(&stats->results, (unsigned long long)cand_n);
-        atomicAdd(&stats->fast, 1ull);
-        atomicAdd(&stats->survivors, (unsigned long long)S.surv_total);
+    if (lane == 0) out_n[q] = cand_n;
+    if (lane == 0 && !(P.dbg & 32u)) {  // dbg 32: no stats atomics
+        DevStats* sl = stats + (q & (kStatSlots - 1));
+        atomicAdd(&sl->postings, (unsigned long long)p_total);
+        atomicAdd(&sl->lists, (unsigned long long)ng);
+        atomicAdd(&sl->results, (unsigned long long)cand_n);
+        atomicAdd(&sl->fast, 1ull);
+        atomicAdd(&sl->survivors, (unsigned long long)S.surv_total);
     }
     WSTAMP(10);
 #ifdef NGS_PHASE_STAMPS
