@@ -62,7 +62,8 @@ struct Context {
     uint32_t* d_qm = nullptr;
     uint32_t* d_glist = nullptr;
     uint32_t* d_list2 = nullptr;
-    uint32_t* d_gcount = nullptr;  // [0] general-path count, [1] tier-2 count
+    uint32_t* d_gcount = nullptr;  // [0] general-path count, [1] tier-2 count, [2] tier-1b count
+    uint32_t* d_fb = nullptr;      // queries tier 1a handed to tier 1b
     uint32_t* d_group = nullptr;
     DevStats* d_stats = nullptr;
     uint32_t* d_n = nullptr;
@@ -74,7 +75,7 @@ struct Context {
 
     ~Context() {
         hipSetDevice(device);
-        for (void* p : {(void*)d_raw, (void*)d_off, (void*)d_norm, (void*)d_qm, (void*)d_glist, (void*)d_list2, (void*)d_gcount,
+        for (void* p : {(void*)d_raw, (void*)d_off, (void*)d_norm, (void*)d_qm, (void*)d_glist, (void*)d_list2, (void*)d_fb, (void*)d_gcount,
                         (void*)d_group, (void*)d_stats, (void*)d_n, (void*)d_k, (void*)d_s, (void*)gen.cnt,
                         (void*)gen.kenc, (void*)gen.list, (void*)gen.sorted, (void*)gen.lcount, gen.temp})
             if (p) hipFree(p);
@@ -120,7 +121,7 @@ struct Library {
         if (!HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking))) return nullptr;
         for (hipEvent_t& e : c->ev)
             if (!HIP_CHECK(hipEventCreate(&e))) return nullptr;
-        if (!dev_alloc(&c->d_gcount, 2) || !dev_alloc(&c->d_group, 64) || !dev_alloc(&c->d_stats, kStatSlots)) return nullptr;
+        if (!dev_alloc(&c->d_gcount, 3) || !dev_alloc(&c->d_group, 64) || !dev_alloc(&c->d_stats, kStatSlots)) return nullptr;
         return c;
     }
     void give_back(std::unique_ptr<Context> c) {
@@ -210,11 +211,11 @@ bool upload(Library& L) {
 
 bool ensure_queries(Context& c, size_t B, size_t bytes) {
     if (B > c.bcap) {
-        for (void** p : {(void**)&c.d_off, (void**)&c.d_qm, (void**)&c.d_glist, (void**)&c.d_list2})
+        for (void** p : {(void**)&c.d_off, (void**)&c.d_qm, (void**)&c.d_glist, (void**)&c.d_list2, (void**)&c.d_fb})
             if (*p) { hipFree(*p); *p = nullptr; }
         size_t nb = std::max<size_t>(B, 1024);
         if (!dev_alloc(&c.d_off, nb + 1) || !dev_alloc(&c.d_qm, nb) || !dev_alloc(&c.d_glist, nb) ||
-            !dev_alloc(&c.d_list2, nb))
+            !dev_alloc(&c.d_list2, nb) || !dev_alloc(&c.d_fb, nb))
             return false;
         c.bcap = nb;
     }
@@ -278,7 +279,7 @@ int device_search(Library& L, Context& c, const uint8_t* d_raw, const uint64_t* 
     static const uint32_t waves = [] {  // experiment override of the tier-1 waves per query
         const char* e = std::getenv("NGS_WAVES");
         const uint32_t w = e ? (uint32_t)std::strtoul(e, nullptr, 0) : kDefaultWaves;
-        return w == 1 || w == 2 || w == 4 ? w : kDefaultWaves;
+        return w == 0 || w == 1 || w == 2 || w == 4 ? w : kDefaultWaves;
     }();
     P.waves = waves;
     {
@@ -293,10 +294,10 @@ int device_search(Library& L, Context& c, const uint8_t* d_raw, const uint64_t* 
     if (timing) HIP_CHECK(hipEventRecord(c.ev[0], s));
     if (!HIP_CHECK(launch_prep(d_raw, d_off, B, P, c.d_norm, c.d_qm, L.dev.csize, s))) return -4;
     if (timing) HIP_CHECK(hipEventRecord(c.ev[1], s));
-    if (!HIP_CHECK(hipMemsetAsync(c.d_gcount, 0, 2 * sizeof(uint32_t), s))) return -4;
+    if (!HIP_CHECK(hipMemsetAsync(c.d_gcount, 0, 3 * sizeof(uint32_t), s))) return -4;
     if (timing) HIP_CHECK(hipEventRecord(c.ev[2], s));
     if (!HIP_CHECK(launch_fast(L.dev, P, c.d_norm, d_off, c.d_qm, d_n, d_k, d_s, c.d_list2, c.d_gcount + 1,
-                               c.d_glist, c.d_gcount, c.d_stats, s)))
+                               c.d_fb, c.d_gcount + 2, c.d_glist, c.d_gcount, c.d_stats, s)))
         return -4;
     if (timing) HIP_CHECK(hipEventRecord(c.ev[3], s));
     uint32_t ngen = 0;

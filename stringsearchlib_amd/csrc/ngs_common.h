@@ -54,7 +54,7 @@ constexpr uint32_t kMinBucketTerms = 4096;
 #define NGS_SLOT_BITS 10   // experiment builds override (make variant VFLAGS=-DNGS_SLOT_BITS=11)
 #endif
 #ifndef NGS_SKETCH_CAP
-#define NGS_SKETCH_CAP 1024
+#define NGS_SKETCH_CAP 768
 #endif
 constexpr int kWaveSlotBits = NGS_SLOT_BITS;
 constexpr int kWaveSlots = 1 << kWaveSlotBits;  // wave-private LDS table (u32 words)
@@ -71,10 +71,17 @@ constexpr int kDmaRounds = kWaveChunks / 64;    // dwordx4 loads per lane for on
 #ifndef NGS_WPS
 #define NGS_WPS 4
 #endif
-constexpr int kWaveWavesPerSimd = NGS_WPS;      // occupancy target: 4 -> <= 128 VGPRs
-constexpr uint32_t kDefaultWaves = 1;           // waves per query in the tier-1 kernel
+constexpr int kWaveWavesPerSimd = NGS_WPS;      // occupancy target of tier 1b: 4 -> <= 128 VGPRs
+#ifndef NGS_LEAN_WPS
+#define NGS_LEAN_WPS 5
+#endif
+constexpr int kLeanWavesPerSimd = NGS_LEAN_WPS; // tier 1a: 5 -> <= 96 VGPRs (LDS 8 KB: 20 waves per CU)
+constexpr uint32_t kDefaultWaves = 0;           // tier 1: 0 = lean kernel + full kernel on its hand-overs; 1, 2, 4 = full kernel only
 constexpr int kWaveTarget = kWaveCap * 5 / 8;   // postings per exact part the bucket grouping aims at
-constexpr int kSketchTarget = kSketchCap * 5 / 8;  // ... per sketch part
+#ifndef NGS_TGT8
+#define NGS_TGT8 5
+#endif
+constexpr int kSketchTarget = kSketchCap * NGS_TGT8 / 8;  // ... per sketch part (bucket groups aim at NGS_TGT8/8 of the cap)
 constexpr uint32_t kStray = 0xFFFFFFFFu;        // staged entry outside its list segment
 constexpr int kWaveSurv = 128;                  // survivor list (term, count) before calcScore
 constexpr uint32_t kWaveMaxGrams = 63;
@@ -90,6 +97,10 @@ constexpr bool kSingleBuf = NGS_SINGLE != 0;
 #define NGS_SK2 2     // smallest cmin counted by the sketch (below: exact hash counting)
 #endif
 constexpr uint32_t kSketchMinCmin = NGS_SK2;
+#ifndef NGS_ASMATOM
+#define NGS_ASMATOM 0  // 1: each round's four sketch adds issued together from inline asm
+#endif
+constexpr bool kAsmAtomics = NGS_ASMATOM != 0;
 constexpr int kBndLists = 16;                   // part boundaries preloaded to LDS for queries of <= 16 lists
 constexpr int kBndParts = 48;                   // ... and <= 48 bucket groups          // counts <= 63: one lane per count value
 

@@ -19,7 +19,8 @@ hipError_t launch_prep(const uint8_t* raw, const uint64_t* off, uint32_t B, cons
 // per query over list2: <= 255 grams, limit <= 1024); what remains goes to glist.
 hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* qnorm, const uint64_t* off,
                        const uint32_t* qm, uint32_t* out_n, uint32_t* out_k, float* out_s, uint32_t* list2,
-                       uint32_t* count2, uint32_t* glist, uint32_t* gcount, DevStats* stats, hipStream_t s);
+                       uint32_t* count2, uint32_t* fb, uint32_t* fbc, uint32_t* glist, uint32_t* gcount,
+                       DevStats* stats, hipStream_t s);
 
 // Wildcard answer (nGramSearch.hpp:356-369): keys sorted by (weight desc, rank asc).
 hipError_t build_wildcard(const float* d_w, uint32_t n_keys, uint32_t* d_keys, float* d_scores, hipStream_t s);

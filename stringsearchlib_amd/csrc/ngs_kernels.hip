@@ -1074,12 +1074,36 @@ __device__ __forceinline__ uint32_t part_sketch(WaveSmem<W>& S, const uint4 (&v)
     for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) {
         if (64 * r < mt) {
             const uint32_t t[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
+            if constexpr (kAsmAtomics) {
+                // the round's four adds in flight together, one wait (the compiler, short of
+                // registers, would wait after each returning add)
+                uint32_t a[4], x[4], sh[4], o[4];
 #pragma unroll
-            for (uint32_t e = 0; e < 4; ++e) {
-                const uint32_t c = sketch_cell<W>(t[e]);
-                const uint32_t sh = (c & 7u) << 2;
-                const uint32_t old = atomicAdd(&S.table[c >> 3], ((vmask >> (4 * r + e)) & 1u) << sh);
-                ovf |= ((old >> sh) & kSketchMax) == kSketchMax;
+                for (uint32_t e = 0; e < 4; ++e) {
+                    const uint32_t c = sketch_cell<W>(t[e]);
+                    sh[e] = (c & 7u) << 2;
+                    a[e] = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint32_t*)&S.table[c >> 3];
+                    x[e] = ((vmask >> (4 * r + e)) & 1u) << sh[e];
+                }
+                asm volatile(
+                    "ds_add_rtn_u32 %0, %4, %8\n\t"
+                    "ds_add_rtn_u32 %1, %5, %9\n\t"
+                    "ds_add_rtn_u32 %2, %6, %10\n\t"
+                    "ds_add_rtn_u32 %3, %7, %11\n\t"
+                    "s_waitcnt lgkmcnt(0)"
+                    : "=&v"(o[0]), "=&v"(o[1]), "=&v"(o[2]), "=&v"(o[3])
+                    : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3])
+                    : "memory");
+#pragma unroll
+                for (uint32_t e = 0; e < 4; ++e) ovf |= ((o[e] >> sh[e]) & kSketchMax) == kSketchMax;
+            } else {
+#pragma unroll
+                for (uint32_t e = 0; e < 4; ++e) {
+                    const uint32_t c = sketch_cell<W>(t[e]);
+                    const uint32_t sh = (c & 7u) << 2;
+                    const uint32_t old = atomicAdd(&S.table[c >> 3], ((vmask >> (4 * r + e)) & 1u) << sh);
+                    ovf |= ((old >> sh) & kSketchMax) == kSketchMax;
+                }
             }
         }
     }
@@ -1160,19 +1184,24 @@ __device__ __forceinline__ uint32_t part_sketch(WaveSmem<W>& S, const uint4 (&v)
     return nc;
 }
 
-template <int W>
-__global__ __launch_bounds__(64 * W, kWaveWavesPerSimd) void k_wave(DevIndex X, SearchParams P,
-                                                                   const uint8_t* __restrict__ qnorm,
-                                                                   const uint64_t* __restrict__ qoff,
-                                                                   const uint32_t* __restrict__ qm,
-                                                                   uint32_t* __restrict__ out_n,
-                                                                   uint32_t* __restrict__ out_k,
-                                                                   float* __restrict__ out_s,
-                                                                   uint32_t* __restrict__ list2,
-                                                                   uint32_t* __restrict__ count2,
-                                                                   DevStats* __restrict__ stats) {
-    __shared__ WaveSmem<W> S;
-    const uint32_t q = blockIdx.x, lane = lane_id(), tid = threadIdx.x;
+// One query on W waves. LEAN (tier 1a, W = 1): the common case only, sketch counting with no
+// exact-count pass, no mid-loop calcScore and no short search, which keeps the kernel within 96
+// VGPRs (5 waves per SIMD); a query that needs any of those is appended to fb[] untouched and
+// rerun from scratch by the full kernel (tier 1b).
+template <int W, bool LEAN>
+__device__ __forceinline__ void wave_query(WaveSmem<W>& S, const uint32_t q, const DevIndex& X, const SearchParams& P,
+                                           const uint8_t* __restrict__ qnorm, const uint64_t* __restrict__ qoff,
+                                           const uint32_t* __restrict__ qm, uint32_t* __restrict__ out_n,
+                                           uint32_t* __restrict__ out_k, float* __restrict__ out_s,
+                                           uint32_t* __restrict__ list2, uint32_t* __restrict__ count2,
+                                           DevStats* __restrict__ stats, uint32_t* __restrict__ fb,
+                                           uint32_t* __restrict__ fbc) {
+    const uint32_t lane = lane_id(), tid = threadIdx.x;
+    // tier 1a hands the query over (all lanes leave together; nothing of it was written yet)
+    auto bail = [&]() {
+        if (lane == 0) fb[atomicAdd(fbc, 1u)] = q;
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    };
     const uint32_t wid = W == 1 ? 0u : __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t m = qm[q];
     const uint32_t L = P.limit;
@@ -1220,7 +1249,9 @@ __global__ __launch_bounds__(64 * W, kWaveWavesPerSimd) void k_wave(DevIndex X, 
     const float sc_short = lane <= m ? (float)lane / (float)m : 0.0f;
 
     // ---- searchShort over shortLib (nGramSearch.hpp:262-270), 4 <= m < 9, wave 0 ----
-    if (wid == 0 && m < X.short_query_len && X.n_short) {
+    if constexpr (LEAN) {
+        if (m < X.short_query_len && X.n_short) { bail(); return; }
+    } else if (wid == 0 && m < X.short_query_len && X.n_short) {
         uint32_t qc[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) qc[i] = (uint32_t)i < m ? S.q[i] : 0;
@@ -1277,6 +1308,7 @@ __global__ __launch_bounds__(64 * W, kWaveWavesPerSimd) void k_wave(DevIndex X, 
     // part cap: a sketch part holds twice the entries of an exact pass (u8 vs u32 cells)
     const uint32_t kChunks = ((sketch ? (uint32_t)kWaveChunks : (uint32_t)kExactChunks) * W) >> shrink;
     WSTAMP(1);
+    if (LEAN && p_total && cmin <= n && !sketch) { bail(); return; }
     if (p_total && cmin <= n) {
         const uint32_t K = X.n_buckets, span = X.bucket_span;
         const uint32_t wmax = (uint32_t)max64(1, min64(K, kMaxPartSpan / max(span, 1u)));
@@ -1436,8 +1468,10 @@ __global__ __launch_bounds__(64 * W, kWaveWavesPerSimd) void k_wave(DevIndex X, 
             if constexpr (kSingleBuf) take();
             // ---- count part i while part i+1 is in flight ----
             if (have_c && !(P.dbg & 1u)) {  // dbg 1: load only, no counting
-                if (wid == 0 && surv_n + 64 > (uint32_t)kWaveSurv)
-                    wave_emit(S, X, P, m, L, sc_long, sc_short, surv_n, cand_n, tau);
+                if (wid == 0 && surv_n + 64 > (uint32_t)kWaveSurv) {
+                    if constexpr (LEAN) { bail(); return; }
+                    else wave_emit(S, X, P, m, L, sc_long, sc_short, surv_n, cand_n, tau);
+                }
                 const uint32_t nc = sketch ? part_sketch(S, cv, c_vm, c_mt, cmin, X.n_short, X.n_terms, surv_n, P.dbg) : 65u;
                 const bool done = nc <= 64;
                 WCOUNT(11, 1);
@@ -1445,7 +1479,8 @@ __global__ __launch_bounds__(64 * W, kWaveWavesPerSimd) void k_wave(DevIndex X, 
                 WCOUNT(13, sketch ? nc : 0);
                 WCOUNT(14, c_mt);
                 WSTAMP(5);
-                if (!done) {
+                if (LEAN && !done) { bail(); return; }
+                if (!LEAN && !done) {
                     // exact count in term-id ranges of <= kWaveCap entries per wave (one range unless a
                     // sketch part overflowed)
                     const uint32_t mtu = __builtin_amdgcn_readfirstlane(c_mt);
@@ -1510,6 +1545,51 @@ __global__ __launch_bounds__(64 * W, kWaveWavesPerSimd) void k_wave(DevIndex X, 
     if (lane == 0)
         for (int i = 0; i < 16; ++i) atomicAdd(&g_phase[16 + i], wacc_[i]);
 #endif
+}
+
+// Tier 1b / experiments: the full wave kernel, over every query (qlist == nullptr) or over the
+// queries tier 1a handed over (qlist[0 .. *qcount), grid-stride).
+template <int W>
+__global__ __launch_bounds__(64 * W, kWaveWavesPerSimd) void k_wave(DevIndex X, SearchParams P,
+                                                                   const uint8_t* __restrict__ qnorm,
+                                                                   const uint64_t* __restrict__ qoff,
+                                                                   const uint32_t* __restrict__ qm,
+                                                                   uint32_t* __restrict__ out_n,
+                                                                   uint32_t* __restrict__ out_k,
+                                                                   float* __restrict__ out_s,
+                                                                   uint32_t* __restrict__ list2,
+                                                                   uint32_t* __restrict__ count2,
+                                                                   DevStats* __restrict__ stats,
+                                                                   const uint32_t* __restrict__ qlist,
+                                                                   const uint32_t* __restrict__ qcount) {
+    __shared__ WaveSmem<W> S;
+    if (!qlist) {
+        wave_query<W, false>(S, blockIdx.x, X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats,
+                             nullptr, nullptr);
+        return;
+    }
+    const uint32_t cnt = *qcount;
+    for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
+        wave_query<W, false>(S, qlist[i], X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats,
+                             nullptr, nullptr);
+        __syncthreads();
+    }
+}
+
+// Tier 1a: the lean wave kernel over every query.
+__global__ __launch_bounds__(64, kLeanWavesPerSimd) void k_wave_lean(DevIndex X, SearchParams P,
+                                                                    const uint8_t* __restrict__ qnorm,
+                                                                    const uint64_t* __restrict__ qoff,
+                                                                    const uint32_t* __restrict__ qm,
+                                                                    uint32_t* __restrict__ out_n,
+                                                                    uint32_t* __restrict__ out_k,
+                                                                    float* __restrict__ out_s,
+                                                                    uint32_t* __restrict__ list2,
+                                                                    uint32_t* __restrict__ count2,
+                                                                    DevStats* __restrict__ stats,
+                                                                    uint32_t* __restrict__ fb, uint32_t* __restrict__ fbc) {
+    __shared__ WaveSmem<1> S;
+    wave_query<1, true>(S, blockIdx.x, X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats, fb, fbc);
 }
 
 // ---------------------------------------------------------------- general path -------
@@ -1668,20 +1748,30 @@ hipError_t launch_prep(const uint8_t* raw, const uint64_t* off, uint32_t B, cons
 
 hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* qnorm, const uint64_t* off,
                        const uint32_t* qm, uint32_t* out_n, uint32_t* out_k, float* out_s, uint32_t* list2,
-                       uint32_t* count2, uint32_t* glist, uint32_t* gcount, DevStats* stats, hipStream_t s) {
+                       uint32_t* count2, uint32_t* fb, uint32_t* fbc, uint32_t* glist, uint32_t* gcount,
+                       DevStats* stats, hipStream_t s) {
     if (!P.n_queries) return hipSuccess;
-    switch (P.waves) {  // waves per query (SearchParams.waves, NGS_WAVES)
+    switch (P.waves) {  // waves per query (SearchParams.waves, NGS_WAVES; 0 = tier 1a + 1b)
+        case 0: {
+            hipLaunchKernelGGL(k_wave_lean, dim3(P.n_queries), dim3(64), 0, s, X, P, qnorm, off, qm, out_n, out_k,
+                               out_s, list2, count2, stats, fb, fbc);
+            // tier 1b over the handed-over queries: a grid that fills the GPU, grid-stride
+            const uint32_t g1b = std::min<uint32_t>(P.n_queries, 4096);
+            hipLaunchKernelGGL(k_wave<1>, dim3(g1b), dim3(64), 0, s, X, P, qnorm, off, qm, out_n, out_k, out_s,
+                               list2, count2, stats, (const uint32_t*)fb, (const uint32_t*)fbc);
+            break;
+        }
         case 1:
             hipLaunchKernelGGL(k_wave<1>, dim3(P.n_queries), dim3(64), 0, s, X, P, qnorm, off, qm, out_n, out_k,
-                               out_s, list2, count2, stats);
+                               out_s, list2, count2, stats, (const uint32_t*)nullptr, (const uint32_t*)nullptr);
             break;
         case 2:
             hipLaunchKernelGGL(k_wave<2>, dim3(P.n_queries), dim3(128), 0, s, X, P, qnorm, off, qm, out_n, out_k,
-                               out_s, list2, count2, stats);
+                               out_s, list2, count2, stats, (const uint32_t*)nullptr, (const uint32_t*)nullptr);
             break;
         default:
             hipLaunchKernelGGL(k_wave<4>, dim3(P.n_queries), dim3(256), 0, s, X, P, qnorm, off, qm, out_n, out_k,
-                               out_s, list2, count2, stats);
+                               out_s, list2, count2, stats, (const uint32_t*)nullptr, (const uint32_t*)nullptr);
             break;
     }
     const uint32_t grid2 = std::min<uint32_t>(P.n_queries, 1024);
