@@ -73,9 +73,9 @@ constexpr int kDmaRounds = kWaveChunks / 64;    // dwordx4 loads per lane for on
 #endif
 constexpr int kWaveWavesPerSimd = NGS_WPS;      // occupancy target of tier 1b: 4 -> <= 128 VGPRs
 #ifndef NGS_LEAN_WPS
-#define NGS_LEAN_WPS 5
+#define NGS_LEAN_WPS 6
 #endif
-constexpr int kLeanWavesPerSimd = NGS_LEAN_WPS; // tier 1a: 5 -> <= 96 VGPRs (LDS 8 KB: 20 waves per CU)
+constexpr int kLeanWavesPerSimd = NGS_LEAN_WPS; // tier 1a: 6 -> <= 80 VGPRs (LDS 6 KB: 24 waves per CU)
 constexpr uint32_t kDefaultWaves = 0;           // tier 1: 0 = lean kernel + full kernel on its hand-overs; 1, 2, 4 = full kernel only
 constexpr int kWaveTarget = kWaveCap * 5 / 8;   // postings per exact part the bucket grouping aims at
 #ifndef NGS_TGT8

@@ -669,10 +669,15 @@ __global__ __launch_bounds__(kFastThreads) void k_fast(DevIndex X, SearchParams 
 // the next part's loads stay in flight. Candidate resolution, survivors and the top-L run on
 // wave 0. A repeated query gram is kept as a separate occurrence (its list is read once per
 // occurrence), which is the reference's multiplicity (hpp:289-298).
-template <int W>
+template <int W, bool LEAN = false>
 struct alignas(16) WaveSmem {
     uint32_t table[kWaveSlots * W];  // exact: (term - lo + 1) << 8 | count; sketch: 8 x u4 counters
-    uint64_t cand[kWaveCand];        // (~enc) << 32 | key
+    uint64_t cand_own[LEAN ? 1 : kWaveCand];  // (~enc) << 32 | key
+    // the candidate buffer; tier 1a (LEAN) fills it only after the part loop, over the dead table
+    __device__ __forceinline__ uint64_t* cand() {
+        if constexpr (LEAN) return reinterpret_cast<uint64_t*>(table);
+        else return cand_own;
+    }
     uint2 segtab[W][64];             // staging, per wave: per list {first chunk - position, first | end entry << 16}
     uint8_t mark[W][kWaveChunks];    // staging, per wave: list index + 1 at the (wave-local) position of its first chunk
     uint32_t surv_t[kWaveSurv];      // survivor terms
@@ -687,6 +692,7 @@ struct alignas(16) WaveSmem {
     uint64_t x_tau;
 };
 
+static_assert(kWaveSlots * 4 >= kWaveCand * 8, "tier 1a keeps the candidate buffer in the table");
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
 
 // popcount of the ballot bits of the lanes below this one (v_mbcnt_lo/hi)
@@ -766,14 +772,14 @@ __device__ __forceinline__ uint32_t wave_incl_max_scan(uint32_t v) {
 }
 
 // Wave-local running top-L over the candidate buffer (same algorithm as flush()).
-template <int W>
-__device__ void wave_flush(WaveSmem<W>& S, uint32_t& cand_n, uint64_t& tau, uint32_t L) {
+template <int W, bool LEAN>
+__device__ void wave_flush(WaveSmem<W, LEAN>& S, uint32_t& cand_n, uint64_t& tau, uint32_t L) {
     const uint32_t lane = lane_id();
     const uint32_t n = min(cand_n, (uint32_t)kWaveCand);
     const uint32_t P2 = next_pow2(max(n, 2u));
     for (uint32_t i = lane; i < P2; i += 64) {
-        const uint64_t r = i < n ? S.cand[i] : kNoCand;
-        S.cand[i] = i < n ? ((r << 32) | (r >> 32)) : kNoCand;  // key-major for the dedup
+        const uint64_t r = i < n ? S.cand()[i] : kNoCand;
+        S.cand()[i] = i < n ? ((r << 32) | (r >> 32)) : kNoCand;  // key-major for the dedup
     }
     wave_sync();
     for (int pass = 0; pass < 2; ++pass) {
@@ -781,8 +787,8 @@ __device__ void wave_flush(WaveSmem<W>& S, uint32_t& cand_n, uint64_t& tau, uint
             for (uint32_t j = k >> 1; j > 0; j >>= 1) {
                 for (uint32_t p = lane; p < P2 / 2; p += 64) {
                     const uint32_t i = (p / j) * 2 * j + (p % j), l = i + j;
-                    const uint64_t x = S.cand[i], y = S.cand[l];
-                    if ((x > y) == ((i & k) == 0)) { S.cand[i] = y; S.cand[l] = x; }
+                    const uint64_t x = S.cand()[i], y = S.cand()[l];
+                    if ((x > y) == ((i & k) == 0)) { S.cand()[i] = y; S.cand()[l] = x; }
                 }
                 wave_sync();
             }
@@ -794,30 +800,30 @@ __device__ void wave_flush(WaveSmem<W>& S, uint32_t& cand_n, uint64_t& tau, uint
             const uint32_t i = lane + u * 64;
             keep[u] = kNoCand;
             if (i < P2) {
-                const uint64_t d = S.cand[i];
-                if (d != kNoCand && (i == 0 || (S.cand[i - 1] >> 32) != (d >> 32))) keep[u] = (d << 32) | (d >> 32);
+                const uint64_t d = S.cand()[i];
+                if (d != kNoCand && (i == 0 || (S.cand()[i - 1] >> 32) != (d >> 32))) keep[u] = (d << 32) | (d >> 32);
             }
         }
         wave_sync();
 #pragma unroll
         for (int u = 0; u < kWaveCand / 64; ++u) {
             const uint32_t i = lane + u * 64;
-            if (i < P2) S.cand[i] = keep[u];
+            if (i < P2) S.cand()[i] = keep[u];
         }
         wave_sync();
     }
     uint32_t mine = 0;
-    for (uint32_t i = lane; i < P2; i += 64) mine += S.cand[i] != kNoCand;
+    for (uint32_t i = lane; i < P2; i += 64) mine += S.cand()[i] != kNoCand;
     const uint32_t nv = wave_sum(mine);
     cand_n = min(nv, L);
-    tau = nv >= L ? S.cand[L - 1] : kNoCand;
+    tau = nv >= L ? S.cand()[L - 1] : kNoCand;
     wave_sync();
 }
 
 // calcScore (nGramSearch.hpp:310-341) over the survivor list: term -> (key, weight) pairs,
 // max(w*s, 0), exact-match promotion, into the running top-L.
-template <int W>
-__device__ void wave_emit(WaveSmem<W>& S, const DevIndex& X, const SearchParams& P, uint32_t m, uint32_t L,
+template <int W, bool LEAN>
+__device__ void wave_emit(WaveSmem<W, LEAN>& S, const DevIndex& X, const SearchParams& P, uint32_t m, uint32_t L,
                           float sc_long, float sc_short, uint32_t& surv_n, uint32_t& cand_n, uint64_t& tau) {
     const uint32_t lane = lane_id();
     S.surv_total += surv_n;
@@ -844,7 +850,7 @@ __device__ void wave_emit(WaveSmem<W>& S, const DevIndex& X, const SearchParams&
             if (cand_n + 64 > (uint32_t)kWaveCand) wave_flush(S, cand_n, tau, L);
             const bool want = rec < tau;
             const unsigned long long b = __ballot(want);
-            if (want) S.cand[cand_n + rank_below(b)] = rec;
+            if (want) S.cand()[cand_n + rank_below(b)] = rec;
             cand_n += __popcll(b);
         }
     }
@@ -852,8 +858,8 @@ __device__ void wave_emit(WaveSmem<W>& S, const DevIndex& X, const SearchParams&
     wave_sync();
 }
 
-template <int W>
-__device__ __forceinline__ void surv_append(WaveSmem<W>& S, bool pass, uint32_t t, uint32_t code, uint32_t& surv_n) {
+template <int W, bool LEAN>
+__device__ __forceinline__ void surv_append(WaveSmem<W, LEAN>& S, bool pass, uint32_t t, uint32_t code, uint32_t& surv_n) {
     const unsigned long long b = __ballot(pass);
     if (pass) {
         const uint32_t i = surv_n + rank_below(b);
@@ -905,8 +911,8 @@ __device__ __forceinline__ uint32_t sketch_cell(uint32_t t) {  // u4 counter ind
 // start plus a max-scan; vmask bit 4r+e says whether entry e of v[r] belongs to the part (chunk
 // edges hold up to 3 entries of neighbouring lists). Returns this wave's chunk count; *tch_all
 // receives the part's.
-template <int W>
-__device__ __forceinline__ uint32_t stage_part(WaveSmem<W>& S, const uint4* __restrict__ post4, uint64_t gbase,
+template <int W, bool LEAN>
+__device__ __forceinline__ uint32_t stage_part(WaveSmem<W, LEAN>& S, const uint4* __restrict__ post4, uint64_t gbase,
                                                uint32_t a0, uint32_t cur, uint32_t len,
                                                uint4 (&v)[kDmaRounds], uint32_t& vmask, uint32_t dbg = 0) {
     const uint32_t lane = lane_id(), wid = W == 1 ? 0u : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -976,8 +982,8 @@ __device__ __forceinline__ uint32_t stage_part(WaveSmem<W>& S, const uint4* __re
 // so later passes over other term ranges skip it; the extraction exchanges the slot with 0,
 // so the first holder of a term owns its count (no table scan; the table ends empty). With
 // W > 1 the waves extract in turns, handing wave 0's survivor / top-L state round in LDS.
-template <int W>
-__device__ __forceinline__ void part_exact(WaveSmem<W>& S, uint4 (&v)[kDmaRounds], uint32_t vmask, uint32_t mt,
+template <int W, bool LEAN>
+__device__ __forceinline__ void part_exact(WaveSmem<W, LEAN>& S, uint4 (&v)[kDmaRounds], uint32_t vmask, uint32_t mt,
                                            uint32_t ta, uint32_t tb, uint32_t pass, const DevIndex& X,
                                            const SearchParams& P, uint32_t m, uint32_t L, uint32_t cmin,
                                            float sc_long, float sc_short, uint32_t& surv_n, uint32_t& cand_n,
@@ -1063,8 +1069,8 @@ __device__ __forceinline__ void part_exact(WaveSmem<W>& S, uint4 (&v)[kDmaRounds
 // other. Returns the number of candidate entries; above 64 the caller counts the part exactly
 // (the table is clean again). (u16 counters with no-return adds were measured: the 4x fewer
 // cells per KB cost more in false candidates than the returns cost in waits.)
-template <int W>
-__device__ __forceinline__ uint32_t part_sketch(WaveSmem<W>& S, const uint4 (&v)[kDmaRounds], uint32_t vmask,
+template <int W, bool LEAN>
+__device__ __forceinline__ uint32_t part_sketch(WaveSmem<W, LEAN>& S, const uint4 (&v)[kDmaRounds], uint32_t vmask,
                                                 uint32_t mt, uint32_t cmin, uint32_t n_short, uint32_t n_terms,
                                                 uint32_t& surv_n, uint32_t dbg) {
     const uint32_t lane = lane_id(), wid = W == 1 ? 0u : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1189,7 +1195,7 @@ __device__ __forceinline__ uint32_t part_sketch(WaveSmem<W>& S, const uint4 (&v)
 // VGPRs (5 waves per SIMD); a query that needs any of those is appended to fb[] untouched and
 // rerun from scratch by the full kernel (tier 1b).
 template <int W, bool LEAN>
-__device__ __forceinline__ void wave_query(WaveSmem<W>& S, const uint32_t q, const DevIndex& X, const SearchParams& P,
+__device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t q, const DevIndex& X, const SearchParams& P,
                                            const uint8_t* __restrict__ qnorm, const uint64_t* __restrict__ qoff,
                                            const uint32_t* __restrict__ qm, uint32_t* __restrict__ out_n,
                                            uint32_t* __restrict__ out_k, float* __restrict__ out_s,
@@ -1526,7 +1532,7 @@ __device__ __forceinline__ void wave_query(WaveSmem<W>& S, const uint32_t q, con
     wave_flush(S, cand_n, tau, L);
     WSTAMP(9);
     for (uint32_t i = lane; i < cand_n; i += 64) {
-        const uint64_t r = S.cand[i];
+        const uint64_t r = S.cand()[i];
         const uint32_t enc = ~(uint32_t)(r >> 32);
         out_k[ob + i] = (uint32_t)r;
         out_s[ob + i] = enc == kPromoted ? 100.0f : __uint_as_float(enc - 1u);
@@ -1588,7 +1594,7 @@ __global__ __launch_bounds__(64, kLeanWavesPerSimd) void k_wave_lean(DevIndex X,
                                                                     uint32_t* __restrict__ count2,
                                                                     DevStats* __restrict__ stats,
                                                                     uint32_t* __restrict__ fb, uint32_t* __restrict__ fbc) {
-    __shared__ WaveSmem<1> S;
+    __shared__ WaveSmem<1, true> S;
     wave_query<1, true>(S, blockIdx.x, X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats, fb, fbc);
 }
 
