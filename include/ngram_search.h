@@ -156,6 +156,8 @@ typedef struct {
     double fast_kernel_ms;     /* fused kernel time from HIP events on the call's stream */
     double prep_kernel_ms;     /* normalisation kernel time */
     double general_ms;         /* general path time (all its kernels) */
+    uint64_t handover_queries; /* queries the lean tier-1a kernel handed to the full tier-1b kernel */
+    uint64_t tier2_queries;    /* queries routed to the block-per-query tier-2 kernel */
 } ngs_stats;
 NGS_API int ngsSetTiming(uint32_t handle, int enable);
 NGS_API int ngsLastStats(uint32_t handle, ngs_stats* out);

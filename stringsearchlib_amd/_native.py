@@ -26,7 +26,8 @@ CSRC = os.path.join(PKG, "csrc")
 class NgsStats(C.Structure):
     _fields_ = [("queries", C.c_uint64), ("fast_queries", C.c_uint64), ("general_queries", C.c_uint64),
                 ("postings", C.c_uint64), ("lists", C.c_uint64), ("results", C.c_uint64), ("survivors", C.c_uint64),
-                ("fast_kernel_ms", C.c_double), ("prep_kernel_ms", C.c_double), ("general_ms", C.c_double)]
+                ("fast_kernel_ms", C.c_double), ("prep_kernel_ms", C.c_double), ("general_ms", C.c_double),
+                ("handover_queries", C.c_uint64), ("tier2_queries", C.c_uint64)]
 
 
 def build(jobs: int = 4) -> None:

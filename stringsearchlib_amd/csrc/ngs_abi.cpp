@@ -54,6 +54,8 @@ bool dev_upload(T** p, const std::vector<T>& v, std::vector<void*>& owned, size_
 struct Context {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipStream_t side = nullptr;      // tier 1b on heavy queries, beside tier 1a
+    hipEvent_t fork = nullptr, join = nullptr;
     hipEvent_t ev[6] = {};
     size_t qcap = 0, bcap = 0, ncap = 0, ocap = 0;
     uint8_t* d_raw = nullptr;
@@ -62,8 +64,9 @@ struct Context {
     uint32_t* d_qm = nullptr;
     uint32_t* d_glist = nullptr;
     uint32_t* d_list2 = nullptr;
-    uint32_t* d_gcount = nullptr;  // [0] general-path count, [1] tier-2 count, [2] tier-1b count
+    uint32_t* d_gcount = nullptr;  // [0] general-path count, [1] tier-2 count, [2] tier-1b hand-overs, [3] heavy
     uint32_t* d_fb = nullptr;      // queries tier 1a handed to tier 1b
+    uint32_t* d_heavy = nullptr;   // queries the prep kernel routed to tier 1b
     uint32_t* d_group = nullptr;
     DevStats* d_stats = nullptr;
     uint32_t* d_n = nullptr;
@@ -75,13 +78,16 @@ struct Context {
 
     ~Context() {
         hipSetDevice(device);
-        for (void* p : {(void*)d_raw, (void*)d_off, (void*)d_norm, (void*)d_qm, (void*)d_glist, (void*)d_list2, (void*)d_fb, (void*)d_gcount,
+        for (void* p : {(void*)d_raw, (void*)d_off, (void*)d_norm, (void*)d_qm, (void*)d_glist, (void*)d_list2, (void*)d_fb, (void*)d_heavy, (void*)d_gcount,
                         (void*)d_group, (void*)d_stats, (void*)d_n, (void*)d_k, (void*)d_s, (void*)gen.cnt,
                         (void*)gen.kenc, (void*)gen.list, (void*)gen.sorted, (void*)gen.lcount, gen.temp})
             if (p) hipFree(p);
         for (hipEvent_t e : ev)
             if (e) hipEventDestroy(e);
+        for (hipEvent_t e : {fork, join})
+            if (e) hipEventDestroy(e);
         if (stream) hipStreamDestroy(stream);
+        if (side) hipStreamDestroy(side);
     }
 };
 
@@ -118,10 +124,14 @@ struct Library {
         }
         auto c = std::make_unique<Context>();
         c->device = device;
-        if (!HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking))) return nullptr;
+        if (!HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) ||
+            !HIP_CHECK(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking)) ||
+            !HIP_CHECK(hipEventCreateWithFlags(&c->fork, hipEventDisableTiming)) ||
+            !HIP_CHECK(hipEventCreateWithFlags(&c->join, hipEventDisableTiming)))
+            return nullptr;
         for (hipEvent_t& e : c->ev)
             if (!HIP_CHECK(hipEventCreate(&e))) return nullptr;
-        if (!dev_alloc(&c->d_gcount, 3) || !dev_alloc(&c->d_group, 64) || !dev_alloc(&c->d_stats, kStatSlots)) return nullptr;
+        if (!dev_alloc(&c->d_gcount, 4) || !dev_alloc(&c->d_group, 64) || !dev_alloc(&c->d_stats, kStatSlots)) return nullptr;
         return c;
     }
     void give_back(std::unique_ptr<Context> c) {
@@ -211,11 +221,12 @@ bool upload(Library& L) {
 
 bool ensure_queries(Context& c, size_t B, size_t bytes) {
     if (B > c.bcap) {
-        for (void** p : {(void**)&c.d_off, (void**)&c.d_qm, (void**)&c.d_glist, (void**)&c.d_list2, (void**)&c.d_fb})
+        for (void** p : {(void**)&c.d_off, (void**)&c.d_qm, (void**)&c.d_glist, (void**)&c.d_list2, (void**)&c.d_fb,
+                         (void**)&c.d_heavy})
             if (*p) { hipFree(*p); *p = nullptr; }
         size_t nb = std::max<size_t>(B, 1024);
         if (!dev_alloc(&c.d_off, nb + 1) || !dev_alloc(&c.d_qm, nb) || !dev_alloc(&c.d_glist, nb) ||
-            !dev_alloc(&c.d_list2, nb) || !dev_alloc(&c.d_fb, nb))
+            !dev_alloc(&c.d_list2, nb) || !dev_alloc(&c.d_fb, nb) || !dev_alloc(&c.d_heavy, nb))
             return false;
         c.bcap = nb;
     }
@@ -291,19 +302,23 @@ int device_search(Library& L, Context& c, const uint8_t* d_raw, const uint64_t* 
     ngs_stats st{};
     st.queries = B;
     if (!HIP_CHECK(hipMemsetAsync(c.d_stats, 0, sizeof(DevStats) * kStatSlots, s))) return -4;
+    if (!HIP_CHECK(hipMemsetAsync(c.d_gcount, 0, 4 * sizeof(uint32_t), s))) return -4;
     if (timing) HIP_CHECK(hipEventRecord(c.ev[0], s));
-    if (!HIP_CHECK(launch_prep(d_raw, d_off, B, P, c.d_norm, c.d_qm, L.dev.csize, s))) return -4;
+    if (!HIP_CHECK(launch_prep(d_raw, d_off, B, P, c.d_norm, c.d_qm, L.dev.csize, L.dev, c.d_heavy, c.d_gcount + 3,
+                               s)))
+        return -4;
     if (timing) HIP_CHECK(hipEventRecord(c.ev[1], s));
-    if (!HIP_CHECK(hipMemsetAsync(c.d_gcount, 0, 3 * sizeof(uint32_t), s))) return -4;
     if (timing) HIP_CHECK(hipEventRecord(c.ev[2], s));
     if (!HIP_CHECK(launch_fast(L.dev, P, c.d_norm, d_off, c.d_qm, d_n, d_k, d_s, c.d_list2, c.d_gcount + 1,
-                               c.d_fb, c.d_gcount + 2, c.d_glist, c.d_gcount, c.d_stats, s)))
+                               c.d_fb, c.d_gcount + 2, c.d_heavy, c.d_gcount + 3, c.d_glist, c.d_gcount, c.d_stats,
+                               s, c.side, c.fork, c.join)))
         return -4;
     if (timing) HIP_CHECK(hipEventRecord(c.ev[3], s));
-    uint32_t ngen = 0;
-    if (!HIP_CHECK(hipMemcpyAsync(&ngen, c.d_gcount, sizeof(uint32_t), hipMemcpyDeviceToHost, s)) ||
+    uint32_t counts3[4] = {0, 0, 0, 0};  // general, tier 2, tier 1a hand-overs, heavy
+    if (!HIP_CHECK(hipMemcpyAsync(counts3, c.d_gcount, sizeof(counts3), hipMemcpyDeviceToHost, s)) ||
         !HIP_CHECK(hipStreamSynchronize(s)))
         return -4;
+    const uint32_t ngen = counts3[0];
     if (ngen) {
         std::vector<uint32_t> gl(ngen);
         if (!HIP_CHECK(hipMemcpyAsync(gl.data(), c.d_glist, sizeof(uint32_t) * ngen, hipMemcpyDeviceToHost, s)) ||
@@ -342,6 +357,8 @@ int device_search(Library& L, Context& c, const uint8_t* d_raw, const uint64_t* 
         float ms = 0;
         st.fast_queries = ds.fast;
         st.general_queries = ngen;
+        st.tier2_queries = counts3[1];
+        st.handover_queries = counts3[2] + counts3[3];
         st.postings = ds.postings;
         st.lists = ds.lists;
         st.results = ds.results;

@@ -76,6 +76,14 @@ constexpr int kWaveWavesPerSimd = NGS_WPS;      // occupancy target of tier 1b: 
 #define NGS_LEAN_WPS 6
 #endif
 constexpr int kLeanWavesPerSimd = NGS_LEAN_WPS; // tier 1a: 6 -> <= 80 VGPRs (LDS 6 KB: 24 waves per CU)
+#ifndef NGS_LEAN_CAND_IN_TABLE
+#define NGS_LEAN_CAND_IN_TABLE 1
+#endif
+// tier 1a keeps its candidate buffer over the sketch table (no calcScore until the part loop
+// ends; a query with more survivors than the survivor list holds goes to tier 1b), or in its
+// own 2 KB (calcScore mid-loop like tier 1b, 8 KB of LDS)
+constexpr bool kLeanCandInTable = NGS_LEAN_CAND_IN_TABLE != 0;
+constexpr uint32_t kHeavyCmin = 2;              // queries with cmin <= 2 go to tier 1b from the start
 constexpr uint32_t kDefaultWaves = 0;           // tier 1: 0 = lean kernel + full kernel on its hand-overs; 1, 2, 4 = full kernel only
 constexpr int kWaveTarget = kWaveCap * 5 / 8;   // postings per exact part the bucket grouping aims at
 #ifndef NGS_TGT8

@@ -10,7 +10,8 @@ namespace ngs {
 // Normalise every query (escapeBlank -> trim -> toUpper, nGramSearch.hpp:372-376) into
 // qnorm (same offsets as the raw bytes) and its length into qm (kQueryWildcard for ""/"*").
 hipError_t launch_prep(const uint8_t* raw, const uint64_t* off, uint32_t B, const SearchParams& P,
-                       uint8_t* qnorm, uint32_t* qm, uint32_t cs, hipStream_t s);
+                       uint8_t* qnorm, uint32_t* qm, uint32_t cs, const DevIndex& X, uint32_t* heavy,
+                       uint32_t* hcount, hipStream_t s);
 
 // Fused per-query kernel: short Levenshtein scan of shortLib (4 <= m < 9), 3-gram posting
 // count in an LDS hash table per term-id part, threshold, term->key weighting, per-key max
@@ -19,8 +20,9 @@ hipError_t launch_prep(const uint8_t* raw, const uint64_t* off, uint32_t B, cons
 // per query over list2: <= 255 grams, limit <= 1024); what remains goes to glist.
 hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* qnorm, const uint64_t* off,
                        const uint32_t* qm, uint32_t* out_n, uint32_t* out_k, float* out_s, uint32_t* list2,
-                       uint32_t* count2, uint32_t* fb, uint32_t* fbc, uint32_t* glist, uint32_t* gcount,
-                       DevStats* stats, hipStream_t s);
+                       uint32_t* count2, uint32_t* fb, uint32_t* fbc, const uint32_t* heavy,
+                       const uint32_t* hcount, uint32_t* glist, uint32_t* gcount, DevStats* stats, hipStream_t s,
+                       hipStream_t side, hipEvent_t fork, hipEvent_t join);
 
 // Wildcard answer (nGramSearch.hpp:356-369): keys sorted by (weight desc, rank asc).
 hipError_t build_wildcard(const float* d_w, uint32_t n_keys, uint32_t* d_keys, float* d_scores, hipStream_t s);

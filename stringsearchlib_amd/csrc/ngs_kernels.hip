@@ -57,11 +57,29 @@ __device__ __forceinline__ uint32_t char_at(const uint8_t* base, uint64_t i, uin
     return cs == 4 ? reinterpret_cast<const uint32_t*>(base)[i] : (uint32_t)base[i];
 }
 
+// Queries tier 1a would hand over anyway, known from the normalised length alone: a short search
+// over shortLib (m < 3g, hpp:381), or a match-count threshold cmin <= 2, where every term sharing
+// a (g+1)-gram with the query survives (hundreds of calcScore survivors, or exact counting at
+// cmin 1). The prep kernel lists them for tier 1b up front, which then runs beside tier 1a.
+// cmin is computed exactly as the wave kernel does: the first c with !((float)c / n < thr).
+__device__ __forceinline__ bool heavy_query(const DevIndex& X, const SearchParams& P, uint32_t m) {
+    if (m == kQueryWildcard || m == 0 || m <= X.full_scan_len) return false;
+    const uint32_t n = m - X.gsz + 1;
+    if (n > kWaveMaxGrams || P.limit > kWaveMaxLimit) return false;  // tier 2
+    if (m < X.short_query_len && X.n_short) return true;
+    const float fn = (float)n;
+    uint32_t cmin = 1000u;
+    for (uint32_t c = n; c >= 1; --c)
+        if (!((float)c / fn < P.thr)) cmin = c;
+    return cmin <= kHeavyCmin;
+}
+
 // ---------------------------------------------------------------- normalisation ------
 // One wave per query: ballots find the first / last byte that survives escape + trim.
 __global__ __launch_bounds__(64) void k_prep(const uint8_t* __restrict__ raw, const uint64_t* __restrict__ off,
                                              uint32_t B, SearchParams P, uint8_t* __restrict__ qnorm,
-                                             uint32_t* __restrict__ qm, uint32_t cs) {
+                                             uint32_t* __restrict__ qm, uint32_t cs, DevIndex X,
+                                             uint32_t* __restrict__ heavy, uint32_t* __restrict__ hcount) {
     const uint32_t q = blockIdx.x;
     if (q >= B) return;
     const uint32_t lane = threadIdx.x;
@@ -94,7 +112,11 @@ __global__ __launch_bounds__(64) void k_prep(const uint8_t* __restrict__ raw, co
         const uint32_t c = dev_upper(esc_cs(P.valid, char_at(rq, first + i, cs), cs));
         if (cs == 4) reinterpret_cast<uint32_t*>(nq)[i] = c; else nq[i] = (uint8_t)c;
     }
-    if (lane == 0) qm[q] = (uint32_t)(m > 0xFFFFFFF0ull ? 0xFFFFFFF0ull : m);
+    const uint32_t mq = (uint32_t)(m > 0xFFFFFFF0ull ? 0xFFFFFFF0ull : m);
+    if (lane == 0) {
+        qm[q] = mq;
+        if (heavy && heavy_query(X, P, mq)) heavy[atomicAdd(hcount, 1u)] = q;
+    }
 }
 
 // ---------------------------------------------------------------- shared helpers -----
@@ -672,10 +694,10 @@ __global__ __launch_bounds__(kFastThreads) void k_fast(DevIndex X, SearchParams 
 template <int W, bool LEAN = false>
 struct alignas(16) WaveSmem {
     uint32_t table[kWaveSlots * W];  // exact: (term - lo + 1) << 8 | count; sketch: 8 x u4 counters
-    uint64_t cand_own[LEAN ? 1 : kWaveCand];  // (~enc) << 32 | key
+    uint64_t cand_own[LEAN && kLeanCandInTable ? 1 : kWaveCand];  // (~enc) << 32 | key
     // the candidate buffer; tier 1a (LEAN) fills it only after the part loop, over the dead table
     __device__ __forceinline__ uint64_t* cand() {
-        if constexpr (LEAN) return reinterpret_cast<uint64_t*>(table);
+        if constexpr (LEAN && kLeanCandInTable) return reinterpret_cast<uint64_t*>(table);
         else return cand_own;
     }
     uint2 segtab[W][64];             // staging, per wave: per list {first chunk - position, first | end entry << 16}
@@ -1253,6 +1275,11 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
     // lane c holds the fp32 score of c hits: (float)c / n (hpp:300) and (float)c / m (hpp:244)
     const float sc_long = lane <= n ? (float)lane / (float)n : 0.0f;
     const float sc_short = lane <= m ? (float)lane / (float)m : 0.0f;
+    // the smallest hit count whose score passes the threshold (hpp:300,315)
+    const unsigned long long pm = __ballot(lane <= n && lane > 0 && !(sc_long < P.thr));
+    const uint32_t cmin = pm ? (uint32_t)(__ffsll((long long)pm) - 1) : 1000u;
+    // the queries heavy_query() lists in k_prep are tier 1b's (same test, same cmin)
+    if (LEAN && (cmin <= kHeavyCmin || (m < X.short_query_len && X.n_short))) return;
 
     // ---- searchShort over shortLib (nGramSearch.hpp:262-270), 4 <= m < 9, wave 0 ----
     if constexpr (LEAN) {
@@ -1305,8 +1332,6 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
         grow = lane < ng ? r2 : 0;
     }
     const uint64_t p_total = wave_sum((uint64_t)glen);
-    const unsigned long long pm = __ballot(lane <= n && lane > 0 && !(sc_long < P.thr));  // hpp:315
-    const uint32_t cmin = pm ? (uint32_t)(__ffsll((long long)pm) - 1) : 1000u;
     // sketch counting for 2 <= cmin <= 15; at cmin 2 two colliding entries already make a false
     // candidate, so those parts are cut at half the size
     const bool sketch = cmin >= kSketchMinCmin && cmin <= kSketchMax;
@@ -1475,7 +1500,7 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
             // ---- count part i while part i+1 is in flight ----
             if (have_c && !(P.dbg & 1u)) {  // dbg 1: load only, no counting
                 if (wid == 0 && surv_n + 64 > (uint32_t)kWaveSurv) {
-                    if constexpr (LEAN) { bail(); return; }
+                    if constexpr (LEAN && kLeanCandInTable) { bail(); return; }
                     else wave_emit(S, X, P, m, L, sc_long, sc_short, surv_n, cand_n, tau);
                 }
                 const uint32_t nc = sketch ? part_sketch(S, cv, c_vm, c_mt, cmin, X.n_short, X.n_terms, surv_n, P.dbg) : 65u;
@@ -1746,25 +1771,36 @@ int phase_stats(unsigned long long* out, int n, bool reset) {
 }
 
 hipError_t launch_prep(const uint8_t* raw, const uint64_t* off, uint32_t B, const SearchParams& P, uint8_t* qnorm,
-                       uint32_t* qm, uint32_t cs, hipStream_t s) {
+                       uint32_t* qm, uint32_t cs, const DevIndex& X, uint32_t* heavy, uint32_t* hcount,
+                       hipStream_t s) {
     if (!B) return hipSuccess;
-    hipLaunchKernelGGL(k_prep, dim3(B), dim3(64), 0, s, raw, off, B, P, qnorm, qm, cs);
+    hipLaunchKernelGGL(k_prep, dim3(B), dim3(64), 0, s, raw, off, B, P, qnorm, qm, cs, X,
+                       P.waves == 0 ? heavy : nullptr, hcount);
     return hipGetLastError();
 }
 
 hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* qnorm, const uint64_t* off,
                        const uint32_t* qm, uint32_t* out_n, uint32_t* out_k, float* out_s, uint32_t* list2,
-                       uint32_t* count2, uint32_t* fb, uint32_t* fbc, uint32_t* glist, uint32_t* gcount,
-                       DevStats* stats, hipStream_t s) {
+                       uint32_t* count2, uint32_t* fb, uint32_t* fbc, const uint32_t* heavy,
+                       const uint32_t* hcount, uint32_t* glist, uint32_t* gcount, DevStats* stats, hipStream_t s,
+                       hipStream_t side, hipEvent_t fork, hipEvent_t join) {
     if (!P.n_queries) return hipSuccess;
+    hipError_t e = hipSuccess;
     switch (P.waves) {  // waves per query (SearchParams.waves, NGS_WAVES; 0 = tier 1a + 1b)
         case 0: {
+            // tier 1b on the prep kernel's heavy list, on the side stream beside tier 1a
+            const uint32_t g1b = std::min<uint32_t>(P.n_queries, 4096);  // grid-stride over the list
+            if ((e = hipEventRecord(fork, s)) != hipSuccess || (e = hipStreamWaitEvent(side, fork, 0)) != hipSuccess)
+                return e;
+            hipLaunchKernelGGL(k_wave<1>, dim3(g1b), dim3(64), 0, side, X, P, qnorm, off, qm, out_n, out_k, out_s,
+                               list2, count2, stats, heavy, hcount);
+            if ((e = hipEventRecord(join, side)) != hipSuccess) return e;
             hipLaunchKernelGGL(k_wave_lean, dim3(P.n_queries), dim3(64), 0, s, X, P, qnorm, off, qm, out_n, out_k,
                                out_s, list2, count2, stats, fb, fbc);
-            // tier 1b over the handed-over queries: a grid that fills the GPU, grid-stride
-            const uint32_t g1b = std::min<uint32_t>(P.n_queries, 4096);
+            // tier 1b over the queries tier 1a handed over
             hipLaunchKernelGGL(k_wave<1>, dim3(g1b), dim3(64), 0, s, X, P, qnorm, off, qm, out_n, out_k, out_s,
                                list2, count2, stats, (const uint32_t*)fb, (const uint32_t*)fbc);
+            if ((e = hipStreamWaitEvent(s, join, 0)) != hipSuccess) return e;
             break;
         }
         case 1:

@@ -1,6 +1,7 @@
 """Diagnostic: average k_wave launch time (HIP events) on the C3 bench stream.
 Used for ablations: NGS_DEBUG / NGS_LIB variants are read by the library at first use.
 usage: python tools/kms.py [rows] [batch] [thr]"""
+import ctypes as C
 import os
 import sys
 
@@ -24,8 +25,11 @@ def main():
     raw, offs = corpus.queries(B)
     qs = [raw[offs[i]:offs[i + 1]] for i in range(B)]
     ms, ppq = locality_probe.run(L, h, qs, thr=thr)
+    st = _native.NgsStats()
+    L.ngsLastStats(h, C.byref(st))
     print(f"NGS_DEBUG={os.environ.get('NGS_DEBUG', '0')} NGS_LIB={os.environ.get('NGS_LIB', '')} "
-          f"rows={rows} B={B} thr={thr}: kernel {ms:.3f} ms, {B / ms / 1e3:.2f} Mq/s, postings/q {ppq:.0f}", flush=True)
+          f"rows={rows} B={B} thr={thr}: kernel {ms:.3f} ms, {B / ms / 1e3:.2f} Mq/s, postings/q {ppq:.0f}, "
+          f"handover {st.handover_queries} tier2 {st.tier2_queries} general {st.general_queries}", flush=True)
 
 
 if __name__ == "__main__":

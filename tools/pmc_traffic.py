@@ -16,7 +16,7 @@ from collections import defaultdict
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def main(src, cfg, kernel="k_wave"):
+def main(src, cfg, kernel="k_wave_lean"):
     per = defaultdict(float)
     files = glob.glob(os.path.join(src, "**", "run_counter_collection.csv"), recursive=True)
     for f in files:
