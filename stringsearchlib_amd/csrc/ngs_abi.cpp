@@ -293,6 +293,12 @@ int device_search(Library& L, Context& c, const uint8_t* d_raw, const uint64_t* 
         return w == 0 || w == 1 || w == 2 || w == 4 ? w : kDefaultWaves;
     }();
     P.waves = waves;
+    static const uint32_t heavy_waves = [] {
+        const char* e = std::getenv("NGS_HEAVY_WAVES");
+        const uint32_t w = e ? (uint32_t)std::strtoul(e, nullptr, 0) : kHeavyWaves;
+        return w == 1 || w == 2 || w == 4 ? w : kHeavyWaves;
+    }();
+    P.heavy_waves = heavy_waves;
     {
         std::lock_guard<std::mutex> g(L.valid_mu);
         std::memcpy(P.valid, L.valid, sizeof(P.valid));

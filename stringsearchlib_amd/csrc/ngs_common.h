@@ -84,6 +84,11 @@ constexpr int kLeanWavesPerSimd = NGS_LEAN_WPS; // tier 1a: 6 -> <= 80 VGPRs (LD
 // own 2 KB (calcScore mid-loop like tier 1b, 8 KB of LDS)
 constexpr bool kLeanCandInTable = NGS_LEAN_CAND_IN_TABLE != 0;
 constexpr uint32_t kHeavyCmin = 2;              // queries with cmin <= 2 go to tier 1b from the start
+constexpr uint32_t kHeavyWaves = 1;             // ... on this many waves per query
+#ifndef NGS_SHRINK2
+#define NGS_SHRINK2 0
+#endif
+constexpr uint32_t kShrink2 = NGS_SHRINK2;      // cmin 2 sketch parts: cap and target >> this
 constexpr uint32_t kDefaultWaves = 0;           // tier 1: 0 = lean kernel + full kernel on its hand-overs; 1, 2, 4 = full kernel only
 constexpr int kWaveTarget = kWaveCap * 5 / 8;   // postings per exact part the bucket grouping aims at
 #ifndef NGS_TGT8
@@ -144,7 +149,8 @@ struct SearchParams {
     uint32_t n_queries;
     uint32_t valid[8];   // 256-bit validChar mask (h:307-313 / setValidChar)
     uint32_t dbg;        // ablation switches for performance experiments (NGS_DEBUG); 0 in production
-    uint32_t waves;      // waves per query in the tier-1 kernel: 1, 2 or 4 (kDefaultWaves; NGS_WAVES)
+    uint32_t waves;      // tier 1: 0 = lean 1a + full 1b, or 1, 2, 4 waves per query in the full kernel only (NGS_WAVES)
+    uint32_t heavy_waves;  // waves per query of tier 1b on the heavy list (kHeavyWaves; NGS_HEAVY_WAVES)
 };
 
 // per-query normalised length sentinels written by the prep kernel

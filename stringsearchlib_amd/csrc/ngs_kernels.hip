@@ -1335,7 +1335,7 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
     // sketch counting for 2 <= cmin <= 15; at cmin 2 two colliding entries already make a false
     // candidate, so those parts are cut at half the size
     const bool sketch = cmin >= kSketchMinCmin && cmin <= kSketchMax;
-    const uint32_t shrink = cmin == 2 ? 1u : 0u;
+    const uint32_t shrink = cmin == 2 ? kShrink2 : 0u;
     // part cap: a sketch part holds twice the entries of an exact pass (u8 vs u32 cells)
     const uint32_t kChunks = ((sketch ? (uint32_t)kWaveChunks : (uint32_t)kExactChunks) * W) >> shrink;
     WSTAMP(1);
@@ -1792,8 +1792,15 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
             const uint32_t g1b = std::min<uint32_t>(P.n_queries, 4096);  // grid-stride over the list
             if ((e = hipEventRecord(fork, s)) != hipSuccess || (e = hipStreamWaitEvent(side, fork, 0)) != hipSuccess)
                 return e;
-            hipLaunchKernelGGL(k_wave<1>, dim3(g1b), dim3(64), 0, side, X, P, qnorm, off, qm, out_n, out_k, out_s,
-                               list2, count2, stats, heavy, hcount);
+            if (P.heavy_waves == 4)
+                hipLaunchKernelGGL(k_wave<4>, dim3(g1b), dim3(256), 0, side, X, P, qnorm, off, qm, out_n, out_k,
+                                   out_s, list2, count2, stats, heavy, hcount);
+            else if (P.heavy_waves == 2)
+                hipLaunchKernelGGL(k_wave<2>, dim3(g1b), dim3(128), 0, side, X, P, qnorm, off, qm, out_n, out_k,
+                                   out_s, list2, count2, stats, heavy, hcount);
+            else
+                hipLaunchKernelGGL(k_wave<1>, dim3(g1b), dim3(64), 0, side, X, P, qnorm, off, qm, out_n, out_k,
+                                   out_s, list2, count2, stats, heavy, hcount);
             if ((e = hipEventRecord(join, side)) != hipSuccess) return e;
             hipLaunchKernelGGL(k_wave_lean, dim3(P.n_queries), dim3(64), 0, s, X, P, qnorm, off, qm, out_n, out_k,
                                out_s, list2, count2, stats, fb, fbc);
