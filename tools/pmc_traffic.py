@@ -17,21 +17,28 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def main(src, cfg, kernel="k_wave_lean"):
-    per = defaultdict(float)
+    """HBM bytes of one search call's tier-1 phase: every k_wave* / k_fast dispatch of the pass
+    (tier 1a, tier 1b on the heavy list and on hand-overs, tier 2), divided by the number of
+    tier-1a dispatches (one per call)."""
+    fetch = defaultdict(float)
+    names = {}
     files = glob.glob(os.path.join(src, "**", "run_counter_collection.csv"), recursive=True)
     for f in files:
         with open(f) as fh:
             for r in csv.DictReader(fh):
-                if kernel in r["Kernel_Name"] and r["Counter_Name"] == "FETCH_SIZE":
-                    per[(f, r["Dispatch_Id"])] += float(r["Counter_Value"])
-    if not per:
+                if r["Counter_Name"] == "FETCH_SIZE" and ("k_wave" in r["Kernel_Name"] or "k_fast" in r["Kernel_Name"]):
+                    fetch[(f, r["Dispatch_Id"])] += float(r["Counter_Value"])
+                    names[(f, r["Dispatch_Id"])] = r["Kernel_Name"]
+    calls = sum(1 for k in fetch if kernel in names[k])
+    if not calls:
         raise SystemExit(f"no FETCH_SIZE rows for {kernel} under {src}")
-    vals = sorted(per.values())
-    kib = vals[len(vals) // 2]
+    kib = sum(fetch.values()) / calls
+    lean = sorted(v for k, v in fetch.items() if kernel in names[k])
     out = {
-        "kernel": kernel,
-        "dispatches": len(vals),
-        "fetch_size_kib_median": kib,
+        "kernel": "tier-1 phase (k_wave_lean + k_wave heavy + k_wave hand-over + k_fast)",
+        "calls": calls,
+        "fetch_size_kib_per_call": kib,
+        "fetch_size_kib_k_wave_lean_median": lean[len(lean) // 2],
         "correction": "x1024 (KiB) x2 (gfx950 FETCH_SIZE reports half of 16 B/lane reads)",
         "hbm_bytes_per_launch": int(kib * 1024 * 2),
         "source": os.path.relpath(src, ROOT),
@@ -40,6 +47,7 @@ def main(src, cfg, kernel="k_wave_lean"):
     with open(dst, "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out))
+    return out
 
 
 if __name__ == "__main__":
