@@ -56,7 +56,11 @@ constexpr uint32_t kMinBucketTerms = 4096;
 #ifndef NGS_SKETCH_CAP
 #define NGS_SKETCH_CAP 768
 #endif
-constexpr int kWaveSlotBits = NGS_SLOT_BITS;
+constexpr int kWaveSlotBits = NGS_SLOT_BITS;     // tier 1a table: 2^10 words = 4 KB
+#ifndef NGS_FULL_SLOT_BITS
+#define NGS_FULL_SLOT_BITS 11
+#endif
+constexpr int kFullSlotBits = NGS_FULL_SLOT_BITS;  // tier 1b (full kernel) table: 8 KB
 constexpr int kWaveSlots = 1 << kWaveSlotBits;  // wave-private LDS table (u32 words)
 constexpr int kWaveCap = kWaveSlots / 2;        // entries per exact-count pass (<= 50 % table load)
 constexpr int kSketchCellBits = 4;              // sketch counters: u4, 8 per table word

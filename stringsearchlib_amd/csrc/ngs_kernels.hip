@@ -691,9 +691,18 @@ __global__ __launch_bounds__(kFastThreads) void k_fast(DevIndex X, SearchParams 
 // the next part's loads stay in flight. Candidate resolution, survivors and the top-L run on
 // wave 0. A repeated query gram is kept as a separate occurrence (its list is read once per
 // occurrence), which is the reference's multiplicity (hpp:289-298).
+// LDS table geometry: tier 1a keeps 4 KB (occupancy), the full kernel 8 KB (its occupancy is
+// set by VGPRs; a bigger sketch means fewer false candidates on the heavy queries it runs)
+template <bool LEAN>
+struct TableGeom {
+    static constexpr int kBits = LEAN ? kWaveSlotBits : kFullSlotBits;
+    static constexpr int kSlots = 1 << kBits;  // u32 words: exact hash slots, or 8 u4 sketch cells each
+    static constexpr int kCap = kSlots / 2;    // entries per exact-count pass (<= 50 % load)
+};
+
 template <int W, bool LEAN = false>
 struct alignas(16) WaveSmem {
-    uint32_t table[kWaveSlots * W];  // exact: (term - lo + 1) << 8 | count; sketch: 8 x u4 counters
+    uint32_t table[TableGeom<LEAN>::kSlots * W];  // exact: (term - lo + 1) << 8 | count; sketch: 8 x u4 counters
     uint64_t cand_own[LEAN && kLeanCandInTable ? 1 : kWaveCand];  // (~enc) << 32 | key
     // the candidate buffer; tier 1a (LEAN) fills it only after the part loop, over the dead table
     __device__ __forceinline__ uint64_t* cand() {
@@ -891,11 +900,11 @@ __device__ __forceinline__ void surv_append(WaveSmem<W, LEAN>& S, bool pass, uin
     surv_n += __popcll(b);
 }
 
-template <int W>
+template <int W, bool LEAN>
 __device__ __forceinline__ uint32_t wave_insert_slot(uint32_t* T, uint32_t rel, unsigned* err) {
-    constexpr uint32_t kSlots = kWaveSlots * W;
+    constexpr uint32_t kSlots = TableGeom<LEAN>::kSlots * W;
     uint32_t probes = 0;
-    uint32_t h = (rel * 0x9E3779B1u) >> (32 - kWaveSlotBits - (W == 4 ? 2 : W == 2 ? 1 : 0));
+    uint32_t h = (rel * 0x9E3779B1u) >> (32 - TableGeom<LEAN>::kBits - (W == 4 ? 2 : W == 2 ? 1 : 0));
     const uint32_t want = rel << 8;
     for (;;) {
         uint32_t cur = T[h];
@@ -918,9 +927,9 @@ __device__ __forceinline__ uint32_t wave_insert_slot(uint32_t* T, uint32_t rel, 
 
 // sketch cell of a term: full-rate shift/xor (v_mul_lo_u32 is quarter rate). Term ids of a part
 // are spread over a range much wider than the table, and consecutive ids get distinct cells.
-template <int W>
+template <int W, bool LEAN>
 __device__ __forceinline__ uint32_t sketch_cell(uint32_t t) {  // u4 counter index: 8 per table word
-    constexpr uint32_t kBits = kWaveSlotBits + 3 + (W == 4 ? 2 : W == 2 ? 1 : 0);
+    constexpr uint32_t kBits = TableGeom<LEAN>::kBits + 3 + (W == 4 ? 2 : W == 2 ? 1 : 0);
     return (t ^ (t >> kBits)) & ((1u << kBits) - 1u);
 }
 
@@ -1020,7 +1029,7 @@ __device__ __forceinline__ void part_exact(WaveSmem<W, LEAN>& S, uint4 (&v)[kDma
             for (uint32_t e = 0; e < 4; ++e) {
                 uint32_t& x = e == 0 ? v[r].x : e == 1 ? v[r].y : e == 2 ? v[r].z : v[r].w;
                 if (((vmask >> (4 * r + e)) & 1u) && x - ta < tb - ta)
-                    x = tag | wave_insert_slot<W>(S.table, x - ta + 1u, err);
+                    x = tag | wave_insert_slot<W, LEAN>(S.table, x - ta + 1u, err);
             }
         }
     }
@@ -1108,7 +1117,7 @@ __device__ __forceinline__ uint32_t part_sketch(WaveSmem<W, LEAN>& S, const uint
                 uint32_t a[4], x[4], sh[4], o[4];
 #pragma unroll
                 for (uint32_t e = 0; e < 4; ++e) {
-                    const uint32_t c = sketch_cell<W>(t[e]);
+                    const uint32_t c = sketch_cell<W, LEAN>(t[e]);
                     sh[e] = (c & 7u) << 2;
                     a[e] = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint32_t*)&S.table[c >> 3];
                     x[e] = ((vmask >> (4 * r + e)) & 1u) << sh[e];
@@ -1127,7 +1136,7 @@ __device__ __forceinline__ uint32_t part_sketch(WaveSmem<W, LEAN>& S, const uint
             } else {
 #pragma unroll
                 for (uint32_t e = 0; e < 4; ++e) {
-                    const uint32_t c = sketch_cell<W>(t[e]);
+                    const uint32_t c = sketch_cell<W, LEAN>(t[e]);
                     const uint32_t sh = (c & 7u) << 2;
                     const uint32_t old = atomicAdd(&S.table[c >> 3], ((vmask >> (4 * r + e)) & 1u) << sh);
                     ovf |= ((old >> sh) & kSketchMax) == kSketchMax;
@@ -1137,8 +1146,8 @@ __device__ __forceinline__ uint32_t part_sketch(WaveSmem<W, LEAN>& S, const uint
     }
     grp_sync<W>();
     if (dbg & 2u) {  // ablation: add pass only (table cleared, no candidates)
-        uint4* T4 = reinterpret_cast<uint4*>(S.table) + wid * (kWaveSlots / 4);
-        for (uint32_t i = lane; i < (uint32_t)kWaveSlots / 4; i += 64) T4[i] = make_uint4(0, 0, 0, 0);
+        uint4* T4 = reinterpret_cast<uint4*>(S.table) + wid * (TableGeom<LEAN>::kSlots / 4);
+        for (uint32_t i = lane; i < (uint32_t)TableGeom<LEAN>::kSlots / 4; i += 64) T4[i] = make_uint4(0, 0, 0, 0);
         grp_sync<W>();
         return 0;
     }
@@ -1151,10 +1160,10 @@ __device__ __forceinline__ uint32_t part_sketch(WaveSmem<W, LEAN>& S, const uint
             const uint32_t t[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
             uint32_t w[4];
 #pragma unroll
-            for (uint32_t e = 0; e < 4; ++e) w[e] = S.table[sketch_cell<W>(t[e]) >> 3];
+            for (uint32_t e = 0; e < 4; ++e) w[e] = S.table[sketch_cell<W, LEAN>(t[e]) >> 3];
 #pragma unroll
             for (uint32_t e = 0; e < 4; ++e) {
-                const uint32_t c = sketch_cell<W>(t[e]);
+                const uint32_t c = sketch_cell<W, LEAN>(t[e]);
                 cm |= (((w[e] >> ((c & 7u) << 2)) & kSketchMax) >= cmin ? 1u : 0u) << (4 * r + e);
             }
         }
@@ -1188,8 +1197,8 @@ __device__ __forceinline__ uint32_t part_sketch(WaveSmem<W, LEAN>& S, const uint
     grp_sync<W>();
     uint32_t nc = __builtin_amdgcn_readfirstlane(W == 1 ? wnc : S.ncand);
     {
-        uint4* T4 = reinterpret_cast<uint4*>(S.table) + wid * (kWaveSlots / 4);
-        for (uint32_t i = lane; i < (uint32_t)kWaveSlots / 4; i += 64) T4[i] = make_uint4(0, 0, 0, 0);
+        uint4* T4 = reinterpret_cast<uint4*>(S.table) + wid * (TableGeom<LEAN>::kSlots / 4);
+        for (uint32_t i = lane; i < (uint32_t)TableGeom<LEAN>::kSlots / 4; i += 64) T4[i] = make_uint4(0, 0, 0, 0);
     }
     if (wid == 0 && nc && nc <= 64 && !(dbg & 4u)) {
         // lane l < nc holds candidate l; its term's exact count is the number of candidates with
@@ -1266,7 +1275,7 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
     }
     {
         uint4* T4 = reinterpret_cast<uint4*>(S.table);
-        for (uint32_t i = tid; i < (uint32_t)kWaveSlots * W / 4; i += 64 * W) T4[i] = make_uint4(0, 0, 0, 0);
+        for (uint32_t i = tid; i < (uint32_t)TableGeom<LEAN>::kSlots * W / 4; i += 64 * W) T4[i] = make_uint4(0, 0, 0, 0);
     }
     grp_sync<W>();
     uint32_t cand_n = 0, surv_n = 0;
@@ -1537,7 +1546,7 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
                                 grp_sync<W>();
                                 if (wid == 0 && lane == 0) S.xcnt = 0;
                             }
-                            if (cnt <= (uint32_t)kWaveCap || tb - ta <= 1) break;
+                            if (cnt <= (uint32_t)TableGeom<LEAN>::kCap || tb - ta <= 1) break;
                             tb = ta + (tb - ta) / 2;
                         }
                         part_exact(S, cv, c_vm, c_mt, ta, tb, pass++, X, P, m, L, cmin, sc_long, sc_short, surv_n,

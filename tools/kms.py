@@ -24,6 +24,10 @@ def main():
     L = _native.lib()
     raw, offs = corpus.queries(B)
     qs = [raw[offs[i]:offs[i + 1]] for i in range(B)]
+    qlen = int(os.environ.get("KMS_QLEN", "0"))  # only queries of this length (heavy-query studies)
+    if qlen:
+        sel = [q for q in qs if len(q) == qlen]
+        qs = [sel[i % len(sel)] for i in range(B)]
     ms, ppq = locality_probe.run(L, h, qs, thr=thr)
     st = _native.NgsStats()
     L.ngsLastStats(h, C.byref(st))

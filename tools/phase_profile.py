@@ -23,6 +23,10 @@ def main():
     L = _native.lib()
     raw, offs = corpus.queries(B)
     qs = [raw[offs[i]:offs[i + 1]] for i in range(B)]
+    qlen = int(os.environ.get("KMS_QLEN", "0"))  # only queries of this length
+    if qlen:
+        sel = [q for q in qs if len(q) == qlen]
+        qs = [sel[i % len(sel)] for i in range(B)]
     arr = (C.c_char_p * B)(*qs)
     counts = (C.c_uint32 * B)()
     for it in range(3):
