@@ -42,6 +42,13 @@ CONFIGS = {
     # BASELINE.json configs[1]
     "c2": dict(rows=1_000_000, batch=4096, threshold=0.0, limit=100, weights=False,
                workload="C2: 1M-row ASCII corpus, gSize=3, weight=NULL, batch=4096/GPU, threshold=0, limit=100"),
+    # BASELINE.json configs[3] (our indexW/gSize extension, parity unpinned). With gSize 2 over the
+    # 37-symbol alphabet a list holds ~440k postings and a 12-character query reads ~4.7M (19 MB),
+    # 180x a C3 query, so the default batch is 16,384 queries rather than 65,536.
+    "c4": dict(rows=10_000_000, batch=16384, threshold=0.3, limit=100, weights=False, row_size=4, gram=2,
+               wide=True,
+               workload="C4: 10M-row UTF-32 corpus via indexW, gSize=2, rowSize=4 (key + 3 aliases), weight=NULL, "
+                        "batch=16384/GPU, threshold=0.3, limit=100"),
 }
 
 
@@ -53,20 +60,25 @@ def log(rank, *a):
 class Corpus:
     """Synthetic rows + queries in C memory (10M rows would be slow as Python objects)."""
 
-    def __init__(self, rows: int, seed: int = 42):
+    def __init__(self, rows: int, seed: int = 42, row_size: int = 1, wide: bool = False):
         S = _native.synth()
-        self.S, self.rows = S, rows
+        self.S, self.rows, self.row_size, self.wide = S, rows, row_size, wide
+        self.n_words = rows * row_size
         self.blob, self.words, self.weights, self.state = C.c_void_p(), C.POINTER(C.c_char_p)(), \
             C.POINTER(C.c_float)(), C.c_uint64()
-        if S.ngs_synth_corpus(rows, seed, 8, 17, 1, C.byref(self.blob), C.byref(self.words), C.byref(self.weights),
-                              C.byref(self.state)):
+        if S.ngs_synth_corpus(rows, seed, 8, 17, row_size, C.byref(self.blob), C.byref(self.words),
+                              C.byref(self.weights), C.byref(self.state)):
             raise MemoryError("synthetic corpus")
+        self.wblob, self.wwords = C.POINTER(C.c_uint32)(), C.POINTER(C.POINTER(C.c_uint32))()
+        if wide and S.ngs_synth_widen(self.words, self.n_words, C.byref(self.wblob), C.byref(self.wwords)):
+            raise MemoryError("synthetic corpus (UTF-32)")
 
     def queries(self, n: int, skip: int = 0):
         """n queries after `skip` queries of the stream (rank slices of one global stream)."""
         st = C.c_uint64(self.state.value)
         qb, qo = C.c_void_p(), C.POINTER(C.c_uint64)()
-        if self.S.ngs_synth_queries(self.words, self.rows, 1, skip + n, C.byref(st), 12, C.byref(qb), C.byref(qo)):
+        if self.S.ngs_synth_queries(self.words, self.n_words, self.row_size, skip + n, C.byref(st), 12, C.byref(qb),
+                                    C.byref(qo)):
             raise MemoryError("synthetic queries")
         lo, hi = qo[skip], qo[skip + n]
         raw = C.string_at(qb.value + lo, hi - lo)
@@ -76,15 +88,22 @@ class Corpus:
         return raw, offs
 
     def free(self):
-        for p in (self.blob, C.cast(self.words, C.c_void_p), C.cast(self.weights, C.c_void_p)):
+        for p in (self.blob, C.cast(self.words, C.c_void_p), C.cast(self.weights, C.c_void_p),
+                  C.cast(self.wblob, C.c_void_p), C.cast(self.wwords, C.c_void_p)):
             self.S.ngs_synth_free(p)
 
 
-def build_index(corpus: Corpus, weights: bool, device: int) -> int:
+def build_index(corpus: Corpus, weights: bool, device: int, gram: int = 3) -> int:
     L = _native.lib()
     if L.ngsSetDevice(device):
         raise RuntimeError(f"ngsSetDevice({device}) failed")
-    h = L.indexN(corpus.words, corpus.rows, 1, corpus.weights if weights else None)
+    w = corpus.weights if weights else None
+    if corpus.wide:
+        h = L.indexW(corpus.wwords, corpus.n_words, corpus.row_size, w, gram)
+    elif gram != 3:
+        h = L.indexG(corpus.words, corpus.n_words, corpus.row_size, w, gram)
+    else:
+        h = L.indexN(corpus.words, corpus.n_words, corpus.row_size, w)
     if not h:
         raise RuntimeError("indexN failed")
     return h
@@ -94,22 +113,36 @@ def cpu_baseline(corpus: Corpus, cfg: dict, raw: bytes, offs: list, target_s: fl
     """Time the oracle (oracle/, the CPU restatement of the reference path) on host cores."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_py
-    O = oracle_py.lib()
     threads = max(1, min(16, os.cpu_count() or 1))
-    t0 = time.time()
-    h = O.ngo_build(corpus.words, corpus.rows, 1, corpus.weights if cfg["weights"] else None)
-    build_s = time.time() - t0
+    w = corpus.weights if cfg["weights"] else None
     qs = [raw[offs[i]:offs[i + 1]] for i in range(len(offs) - 1)]
     cap = cfg["limit"]
+    generic = corpus.wide or cfg.get("gram", 3) != 3
+    t0 = time.time()
+    if generic:  # the gram-size / UTF-32 restatement (oracle/ngs_oracle_g.c)
+        O = oracle_py.lib_g()
+        U = C.POINTER(C.c_uint32)
+        ptrs = corpus.wwords if corpus.wide else C.cast(corpus.words, C.POINTER(U))
+        h = O.ngog_build(ptrs, corpus.n_words, corpus.row_size, w, cfg.get("gram", 3), int(corpus.wide))
+        qs = [(C.c_uint32 * (len(q) + 1))(*q, 0) if corpus.wide else q for q in qs]
+        search_batch, free, name = O.ngog_search_batch, O.ngog_free, "oracle/ngs_oracle_g.c"
+    else:
+        O = oracle_py.lib()
+        h = O.ngo_build(corpus.words, corpus.n_words, corpus.row_size, w)
+        search_batch, free, name = O.ngo_search_batch, O.ngo_free, "oracle/ngs_oracle.c"
+    build_s = time.time() - t0
 
     def run(n):
         sample = [qs[i % len(qs)] for i in range(n)]
-        arr = (C.c_char_p * n)(*sample)
+        if generic:
+            arr = (C.POINTER(C.c_uint32) * n)(*[C.cast(q, C.POINTER(C.c_uint32)) for q in sample])
+        else:
+            arr = (C.c_char_p * n)(*sample)
         counts = (C.c_uint32 * n)()
         keys = (C.c_uint32 * (n * cap))()
         scores = (C.c_float * (n * cap))()
         t = time.time()
-        O.ngo_search_batch(h, arr, n, cfg["threshold"], cfg["limit"], counts, keys, scores, cap, threads)
+        search_batch(h, arr, n, cfg["threshold"], cfg["limit"], counts, keys, scores, cap, threads)
         return time.time() - t
 
     n = 1024
@@ -120,10 +153,10 @@ def cpu_baseline(corpus: Corpus, cfg: dict, raw: bytes, offs: list, target_s: fl
     if dt < target_s:
         n = min(1 << 23, int(n * target_s / max(dt, 1e-3)))
         dt = run(n)
-    O.ngo_free(h)
+    free(h)
     return {"value": n / dt, "unit": "queries/s", "cores": threads, "kind": "port",
             "sample": f"{n} queries of the same stream ({cfg['workload'].split(',')[0]} index, "
-                      f"threshold {cfg['threshold']}, limit {cfg['limit']}), oracle/ngs_oracle.c on {threads} "
+                      f"threshold {cfg['threshold']}, limit {cfg['limit']}), {name} on {threads} "
                       f"host threads; index build {build_s:.1f}s not timed"}
 
 
@@ -166,8 +199,8 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     t0 = time.time()
-    corpus = Corpus(cfg["rows"])
-    h = build_index(corpus, cfg["weights"], local)
+    corpus = Corpus(cfg["rows"], row_size=cfg.get("row_size", 1), wide=cfg.get("wide", False))
+    h = build_index(corpus, cfg["weights"], local, cfg.get("gram", 3))
     index_s = time.time() - t0
     L = _native.lib()
     n_keys = L.ngsNumKeys(h)
@@ -176,8 +209,12 @@ def main():
 
     B = cfg["batch"]
     raw, offs = corpus.queries(B, skip=rank * B)
-    d_raw = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(dev)
-    d_off = torch.tensor(offs, dtype=torch.int64, device=dev)
+    if corpus.wide:  # UTF-32 queries: one 4-byte code point per byte, offsets in bytes
+        d_raw = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(torch.int32).to(dev).view(torch.uint8)
+        d_off = torch.tensor([4 * o for o in offs], dtype=torch.int64, device=dev)
+    else:
+        d_raw = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(dev)
+        d_off = torch.tensor(offs, dtype=torch.int64, device=dev)
     stride = min(cfg["limit"], n_keys)
     d_cnt = torch.zeros(B, dtype=torch.int32, device=dev)
     d_key = torch.zeros(B * stride, dtype=torch.int32, device=dev)
@@ -216,7 +253,7 @@ def main():
         elapsed = float(e.item())
 
     # per-launch algorithmic bytes of the fused kernel
-    qbytes = offs[-1]
+    qbytes = offs[-1] * (4 if corpus.wide else 1)
     alg_bytes = (4 * st.postings + 16 * st.lists + qbytes + 16 * st.survivors + 8 * st.results + 4 * B)
     fast_ms = sum(k[0] for k in ktimes) / len(ktimes)
     achieved = alg_bytes / (fast_ms * 1e-3) / 1e9

@@ -138,6 +138,9 @@ def synth():
                                         C.POINTER(C.POINTER(C.c_uint64))]
         S.ngs_synth_free.restype = None
         S.ngs_synth_free.argtypes = [C.c_void_p]
+        S.ngs_synth_widen.restype = C.c_int
+        S.ngs_synth_widen.argtypes = [C.POINTER(C.c_char_p), C.c_uint64, C.POINTER(C.POINTER(C.c_uint32)),
+                                      C.POINTER(C.POINTER(C.POINTER(C.c_uint32)))]
         _synth = S
     return _synth
 

@@ -48,6 +48,8 @@ constexpr uint32_t kMaxPartSpan = (1u << 24) - 2;  // 24-bit relative term id in
 // bucket skip table: K <= kMaxBuckets term-id buckets of >= kMinBucketTerms terms each
 constexpr uint32_t kMaxBuckets = 256;
 constexpr uint32_t kMinBucketTerms = 4096;
+constexpr uint64_t kDenseBucketLen = 16;          // dense lists: postings of the longest list per bucket
+constexpr uint64_t kSkipBudget = 512ull << 20;    // ... within this many bytes of skip table
 
 // ---- wave kernel geometry (tier 1: one wave per query) ----
 #ifndef NGS_SLOT_BITS

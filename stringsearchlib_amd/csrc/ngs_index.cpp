@@ -437,16 +437,25 @@ static void build_impl(HostIndex& ix, const CharT* const* words, uint64_t size, 
     // bucket skip table: for every non-empty list, the offset of its first posting in each of
     // K equal term-id buckets. Lets a query cut its lists into term-id parts with one load per
     // (gram, bucket) instead of a binary search (DESIGN.md §Index layout).
-    ix.n_buckets = 1;
-    while (ix.n_buckets < kMaxBuckets && (uint64_t)ix.n_buckets * kMinBucketTerms < n_long) ix.n_buckets <<= 1;
-    ix.bucket_span = n_long ? (n_long + ix.n_buckets - 1) / ix.n_buckets : 1;
     ix.gram_row.assign(nspace, UINT32_MAX);
     std::vector<uint32_t> rows;
+    uint64_t max_len = 0;
     for (uint32_t gi = 0; gi < nspace; ++gi)
         if (ix.gram_off[gi + 1] > ix.gram_off[gi]) {
             ix.gram_row[gi] = (uint32_t)rows.size();
             rows.push_back(gi);
+            max_len = std::max<uint64_t>(max_len, ix.gram_off[gi + 1] - ix.gram_off[gi]);
         }
+    // K: up to kMaxBuckets buckets of >= kMinBucketTerms terms; more (a power of two) when the
+    // lists are dense, so that the longest list has about kDenseBucketLen postings per bucket and
+    // a query's parts stay whole buckets (small gram sizes: 1,369 2-grams over 40M terms), as
+    // long as the table stays within kSkipBudget bytes
+    ix.n_buckets = 1;
+    while (ix.n_buckets < kMaxBuckets && (uint64_t)ix.n_buckets * kMinBucketTerms < n_long) ix.n_buckets <<= 1;
+    while ((uint64_t)ix.n_buckets * 2 <= n_long && max_len / ix.n_buckets > kDenseBucketLen &&
+           (uint64_t)rows.size() * (ix.n_buckets * 2 + 1) * sizeof(uint32_t) <= kSkipBudget)
+        ix.n_buckets <<= 1;
+    ix.bucket_span = n_long ? (n_long + ix.n_buckets - 1) / ix.n_buckets : 1;
     const uint32_t K = ix.n_buckets;
     ix.skip.assign((size_t)rows.size() * (K + 1), 0);
     run([&](unsigned t) {

@@ -542,14 +542,17 @@ __device__ void fast_one(const uint32_t q, FastSmem& S, const DevIndex& X, const
     STAMP(2);
     const uint32_t ng = S.ng;
     const uint64_t p_total = S.seg_total;
-    const uint32_t K = X.n_buckets, span = X.bucket_span;
+    // tier 2 plans over at most kMaxBuckets buckets: every kst-th boundary of the skip table
+    // (the index may hold more, power-of-two many, for dense lists)
+    const uint32_t kst = X.n_buckets > kMaxBuckets ? X.n_buckets / kMaxBuckets : 1u;
+    const uint32_t K = X.n_buckets / kst, span = X.bucket_span * kst, KS = X.n_buckets;
     // postings per term-id bucket, straight from the skip table
     const bool one_part = p_total <= (uint64_t)kPartCap && n_long <= kMaxPartSpan;
     if (!one_part) {
         for (uint32_t idx = tid; idx < ng * K; idx += kFastThreads) {
             const uint32_t g = idx / K, b = idx - g * K;
-            const uint32_t* sk = X.skip + (size_t)S.g_row[g] * (K + 1);
-            const uint32_t c = sk[b + 1] - sk[b];
+            const uint32_t* sk = X.skip + (size_t)S.g_row[g] * (KS + 1);
+            const uint32_t c = sk[(b + 1) * kst] - sk[b * kst];
             if (c) atomicAdd(&S.btot[b], c);
         }
     }
@@ -588,9 +591,9 @@ __device__ void fast_one(const uint32_t q, FastSmem& S, const DevIndex& X, const
         const uint32_t lo_id = blo * span;
         const uint32_t hi_id = (uint32_t)min64((uint64_t)bhi * span, n_long);
         if (tid < ng) {
-            const uint32_t* sk = X.skip + (size_t)S.g_row[tid] * (K + 1);
-            S.g_cur[tid] = S.g_base[tid] + sk[blo];
-            S.g_end[tid] = S.g_base[tid] + sk[bhi];
+            const uint32_t* sk = X.skip + (size_t)S.g_row[tid] * (KS + 1);
+            S.g_cur[tid] = S.g_base[tid] + sk[blo * kst];
+            S.g_end[tid] = S.g_base[tid] + sk[bhi * kst];
         }
         __syncthreads();
         STAMP(5);

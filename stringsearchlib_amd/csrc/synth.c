@@ -71,3 +71,23 @@ __attribute__((visibility("default"))) int ngs_synth_queries(char* const* words,
 }
 
 __attribute__((visibility("default"))) void ngs_synth_free(void* p) { free(p); }
+
+/* UTF-32 copies of n NUL-terminated byte strings (the C4 wide corpus: every byte becomes one
+ * code point), for indexW. Free both outputs with ngs_synth_free. */
+__attribute__((visibility("default"))) int ngs_synth_widen(char* const* words, uint64_t n, uint32_t** blob_out,
+                                                           uint32_t*** words_out) {
+    uint64_t total = 0;
+    for (uint64_t i = 0; i < n; ++i) total += strlen(words[i]) + 1;
+    uint32_t* blob = malloc(sizeof(uint32_t) * (total ? total : 1));
+    uint32_t** w = malloc(sizeof(uint32_t*) * (n ? n : 1));
+    if (!blob || !w) { free(blob); free(w); return -1; }
+    uint64_t o = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        w[i] = blob + o;
+        for (const unsigned char* p = (const unsigned char*)words[i]; *p; ++p) blob[o++] = *p;
+        blob[o++] = 0;
+    }
+    *blob_out = blob;
+    *words_out = w;
+    return 0;
+}
