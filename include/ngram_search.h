@@ -162,6 +162,12 @@ typedef struct {
 NGS_API int ngsSetTiming(uint32_t handle, int enable);
 NGS_API int ngsLastStats(uint32_t handle, ngs_stats* out);
 
+/* Test support: digests of the gram CSR as the kernels read it, for comparing the GPU index
+ * build (default for indexN) with the host build (environment NGS_HOST_GRAMS=1 at build time).
+ * out[0..7] = postings, lists, skip buckets, FNV-1a of gram_off, post, gram_row, skip, bucket
+ * span. Returns 8, -1 (bad handle), -3 (dictionary index), -4 (HIP error). */
+NGS_API int ngsIndexDigest(uint32_t handle, uint64_t* out, int n);
+
 /* Library build identification (e.g. "gfx950 ngram_search 0.1"). */
 NGS_API const char* ngsVersion(void);
 

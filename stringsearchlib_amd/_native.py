@@ -114,6 +114,8 @@ def lib():
     L.ngsSetTiming.argtypes = [u32, C.c_int]
     L.ngsLastStats.restype = C.c_int
     L.ngsLastStats.argtypes = [u32, C.POINTER(NgsStats)]
+    L.ngsIndexDigest.restype = C.c_int
+    L.ngsIndexDigest.argtypes = [u32, C.POINTER(u64), C.c_int]
     L.ngsVersion.restype = cp
     L.ngsVersion.argtypes = []
     L.ngsPhaseStats.restype = C.c_int

@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -19,6 +20,7 @@
 #include <vector>
 
 #include "../../include/ngram_search.h"
+#include "ngs_build.h"
 #include "ngs_index.h"
 #include "ngs_kernels.h"
 
@@ -166,12 +168,40 @@ bool upload(Library& L) {
     uint2* tk;
     float *wild_w, *wild_score;
     L.on_device = true;  // from here on the destructor frees what was allocated
-    bool ok = dev_upload(&gram_off, H.gram_off, L.owned) && dev_upload(&post, H.post, L.owned, 4) /* k_wave stages whole 16-byte chunks */ &&
-              dev_upload(&term_off, H.term_off, L.owned) && dev_upload(&term_bytes, H.term_bytes, L.owned) &&
+    bool ok = dev_upload(&term_off, H.term_off, L.owned) && dev_upload(&term_bytes, H.term_bytes, L.owned) &&
               dev_upload(&tk_off, H.tk_off, L.owned) && dev_upload(&tk, H.tk, L.owned) &&
               dev_upload(&key_off, H.key_off, L.owned) && dev_upload(&key_bytes, kb, L.owned) &&
-              dev_upload(&wild_w, H.wild_w, L.owned) && dev_upload(&gram_row, H.gram_row, L.owned) &&
-              dev_upload(&skip, H.skip, L.owned);
+              dev_upload(&wild_w, H.wild_w, L.owned);
+    if (!ok) return false;
+    bool dev_built = false;
+    if (!H.grams_built) {
+        // the gram CSR and skip table from the terms now in HBM (ngs_build.hip); on failure the
+        // host builds them
+        DeviceGrams dg;
+        const auto t0 = std::chrono::steady_clock::now();
+        const hipError_t e = build_grams_device(term_off, term_bytes, H.n_short, H.n_terms, dg);
+        if (std::getenv("NGS_BUILD_TIMING"))
+            std::fprintf(stderr, "[ngs build] %-22s %8.3f s\n", "gram CSR + skip (GPU)",
+                         std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+        if (e == hipSuccess) {
+            for (void* p : {(void*)dg.gram_off, (void*)dg.post, (void*)dg.gram_row, (void*)dg.skip}) L.owned.push_back(p);
+            gram_off = dg.gram_off;
+            post = dg.post;
+            gram_row = dg.gram_row;
+            skip = dg.skip;
+            H.n_grams = dg.n_grams;
+            H.n_buckets = dg.n_buckets;
+            H.bucket_span = dg.bucket_span;
+            dev_built = true;
+        } else {
+            (void)hipGetLastError();
+            build_grams_host(H);
+            if (!H.grams_built) return false;
+        }
+    }
+    if (!dev_built)  // host-built gram CSR (dictionary indexes, NGS_HOST_GRAMS, device-build failure)
+        ok = dev_upload(&gram_off, H.gram_off, L.owned) && dev_upload(&post, H.post, L.owned, 4) /* k_wave stages whole 16-byte chunks */ &&
+             dev_upload(&gram_row, H.gram_row, L.owned) && dev_upload(&skip, H.skip, L.owned);
     if (!ok) return false;
     uint64_t* ghash_key = nullptr;
     uint32_t* ghash_val = nullptr;
@@ -733,6 +763,37 @@ NGS_API int ngsLastStats(uint32_t handle, ngs_stats* out) {
 }
 
 NGS_API const char* ngsVersion(void) { return "ngram_search 0.1 gfx950"; }
+
+NGS_API int ngsIndexDigest(uint32_t handle, uint64_t* out, int n) {
+    std::shared_lock<std::shared_mutex> lk(g_lock);
+    auto it = g_libs.find(handle);
+    if (it == g_libs.end() || !it->second->on_device || !out) return -1;
+    Library& L = *it->second;
+    const DevIndex& X = L.dev;
+    if (!HIP_CHECK(hipSetDevice(L.device))) return -4;
+    // (bytes, FNV-1a) of gram_off, post, gram_row, skip as the kernels read them
+    auto digest = [](const void* d, size_t bytes, uint64_t& h) -> bool {
+        std::vector<uint8_t> v(bytes);
+        if (bytes && !HIP_CHECK(hipMemcpy(v.data(), d, bytes, hipMemcpyDeviceToHost))) return false;
+        h = 1469598103934665603ull;
+        for (uint8_t c : v) h = (h ^ c) * 1099511628211ull;
+        return true;
+    };
+    uint64_t n_post = 0;
+    const size_t nspace = X.gram_mode == 0 ? kGramSpace : 0;
+    if (X.gram_mode != 0) return -3;  // dictionary indexes: host-built only
+    if (!HIP_CHECK(hipMemcpy(&n_post, X.gram_off + nspace, sizeof(uint64_t), hipMemcpyDeviceToHost))) return -4;
+    const size_t rows = L.host.n_grams;
+    const size_t sizes[4] = {sizeof(uint64_t) * (nspace + 1), sizeof(uint32_t) * n_post, sizeof(uint32_t) * nspace,
+                             sizeof(uint32_t) * rows * (X.n_buckets + 1)};
+    const void* ptrs[4] = {X.gram_off, X.post, X.gram_row, X.skip};
+    uint64_t vals[11] = {n_post, rows, X.n_buckets};
+    for (int i = 0; i < 4; ++i)
+        if (!digest(ptrs[i], sizes[i], vals[3 + i])) return -4;
+    vals[7] = X.bucket_span;
+    for (int i = 0; i < n && i < 8; ++i) out[i] = vals[i];
+    return 8;
+}
 
 NGS_API int ngsPhaseStats(uint64_t* out, int n, int reset) {
     return phase_stats((unsigned long long*)out, n, reset != 0);

@@ -51,6 +51,20 @@ constexpr uint32_t kMinBucketTerms = 4096;
 constexpr uint64_t kDenseBucketLen = 16;          // dense lists: postings of the longest list per bucket
 constexpr uint64_t kSkipBudget = 512ull << 20;    // ... within this many bytes of skip table
 
+// Skip-table geometry of an index (host and device builds alike): K buckets (a power of two) of
+// span term ids. Up to kMaxBuckets buckets of >= kMinBucketTerms terms; more when the lists are
+// dense, so that the longest list has about kDenseBucketLen postings per bucket and a query's
+// parts stay whole buckets (small gram sizes: 1,369 2-grams over 40M terms), as long as the
+// table stays within kSkipBudget bytes.
+inline void skip_buckets(uint32_t n_long, uint32_t rows, uint64_t max_len, uint32_t& K, uint32_t& span) {
+    K = 1;
+    while (K < kMaxBuckets && (uint64_t)K * kMinBucketTerms < n_long) K <<= 1;
+    while ((uint64_t)K * 2 <= n_long && max_len / K > kDenseBucketLen &&
+           (uint64_t)rows * (K * 2 + 1) * sizeof(uint32_t) <= kSkipBudget)
+        K <<= 1;
+    span = n_long ? (n_long + K - 1) / K : 1;
+}
+
 // ---- wave kernel geometry (tier 1: one wave per query) ----
 #ifndef NGS_SLOT_BITS
 #define NGS_SLOT_BITS 10   // experiment builds override (make variant VFLAGS=-DNGS_SLOT_BITS=11)

@@ -185,6 +185,148 @@ struct U64Map {
 
 }  // namespace
 
+// The gram CSR over longLib and its skip table (nGramSearch.hpp:13-21, 41-46), from the laid-out
+// terms: two passes, term-range parallel (postings stay sorted by term id).
+template <typename CharT>
+static void build_grams_impl(HostIndex& ix, unsigned threads, PhaseTimer& pt) {
+    const uint32_t g = ix.gsz;
+
+    // gram CSR over longLib, two passes, term-range parallel (postings stay sorted by term id)
+    const uint32_t n_long = ix.n_terms - ix.n_short;
+    if (!threads) threads = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    threads = std::max(1u, std::min<unsigned>(threads, n_long / 4096 + 1));
+    auto range = [&](unsigned t, uint32_t& b, uint32_t& e) {
+        b = ix.n_short + (uint32_t)((uint64_t)n_long * t / threads);
+        e = ix.n_short + (uint32_t)((uint64_t)n_long * (t + 1) / threads);
+    };
+    auto run = [&](auto&& body) {
+        std::vector<std::thread> th;
+        for (unsigned t = 0; t < threads; ++t) th.emplace_back(body, t);
+        for (auto& x : th) x.join();
+    };
+    const CharT* tchars = reinterpret_cast<const CharT*>(ix.term_bytes.data());
+    // dictionary mode: distinct gram keys -> ids in key order; the device looks them up in an
+    // open-addressing table (ghash)
+    U64Map dict;
+    uint32_t nspace = kGramSpace;
+    if (ix.gram_mode == 1) {
+        std::vector<U64Map> sets(threads);
+        run([&](unsigned t) {
+            uint32_t b, e;
+            range(t, b, e);
+            sets[t].init(1024);
+            for (uint32_t id = b; id < e; ++id) {
+                const uint32_t L = (uint32_t)(ix.term_off[id + 1] - ix.term_off[id]);
+                const CharT* p = tchars + ix.term_off[id];
+                for (uint32_t i = 0; i + g <= L; ++i) sets[t].insert(gram_key(p + i, g));
+            }
+        });
+        std::vector<uint64_t> all;
+        for (auto& st : sets)
+            for (uint64_t k : st.key)
+                if (k != ~0ull) all.push_back(k);
+        sets.clear();
+        std::sort(all.begin(), all.end());
+        all.erase(std::unique(all.begin(), all.end()), all.end());
+        dict.init(all.size() + 1);
+        for (uint32_t i = 0; i < all.size(); ++i) dict.insert(all[i]);
+        for (size_t i = 0; i < dict.key.size(); ++i)
+            if (dict.key[i] != ~0ull)
+                dict.val[i] = (uint32_t)(std::lower_bound(all.begin(), all.end(), dict.key[i]) - all.begin());
+        nspace = (uint32_t)all.size();
+        ix.ghash_key = dict.key;
+        ix.ghash_val = dict.val;
+        ix.ghash_bits = dict.bits;
+    }
+    // distinct grams of one long term (ngrams[h].insert(id) deduplicates per term, hpp:13-21)
+    auto grams_of = [&](uint32_t id, std::vector<uint32_t>& gv) -> uint32_t {
+        const uint32_t L = (uint32_t)(ix.term_off[id + 1] - ix.term_off[id]);
+        if (L > gv.size()) gv.resize(L);
+        if (ix.gram_mode == 0) return term_grams(ix.term_bytes.data() + ix.term_off[id], L, gv.data());
+        const CharT* p = tchars + ix.term_off[id];
+        uint32_t n = 0;
+        for (uint32_t i = 0; i + g <= L; ++i) gv[n++] = dict.find(gram_key(p + i, g));
+        std::sort(gv.begin(), gv.begin() + n);
+        return (uint32_t)(std::unique(gv.begin(), gv.begin() + n) - gv.begin());
+    };
+    ix.gram_off.assign((size_t)nspace + 1, 0);
+    std::vector<std::vector<uint32_t>> counts(threads, std::vector<uint32_t>(nspace, 0));
+    run([&](unsigned t) {
+        uint32_t b, e;
+        range(t, b, e);
+        std::vector<uint32_t> gv(64);
+        uint32_t* c = counts[t].data();
+        for (uint32_t id = b; id < e; ++id) {
+            uint32_t n = grams_of(id, gv);
+            for (uint32_t i = 0; i < n; ++i) c[gv[i]]++;
+        }
+    });
+    {
+        uint64_t o = 0;
+        for (uint32_t gi = 0; gi < nspace; ++gi) {
+            ix.gram_off[gi] = o;
+            uint64_t tot = 0;
+            for (unsigned t = 0; t < threads; ++t) {
+                uint32_t c = counts[t][gi];
+                counts[t][gi] = (uint32_t)(o + tot);  // becomes this thread's write cursor
+                tot += c;
+            }
+            ix.n_grams += tot != 0;
+            o += tot;
+        }
+        ix.gram_off[nspace] = o;
+        ix.post.resize(o);
+    }
+    run([&](unsigned t) {
+        uint32_t b, e;
+        range(t, b, e);
+        std::vector<uint32_t> gv(64);
+        uint32_t* cur = counts[t].data();
+        for (uint32_t id = b; id < e; ++id) {
+            uint32_t n = grams_of(id, gv);
+            for (uint32_t i = 0; i < n; ++i) ix.post[cur[gv[i]]++] = id - ix.n_short;
+        }
+    });
+    counts.clear();
+    pt.mark("gram CSR");
+    // bucket skip table: for every non-empty list, the offset of its first posting in each of
+    // K equal term-id buckets. Lets a query cut its lists into term-id parts with one load per
+    // (gram, bucket) instead of a binary search (DESIGN.md §Index layout).
+    ix.gram_row.assign(nspace, UINT32_MAX);
+    std::vector<uint32_t> rows;
+    uint64_t max_len = 0;
+    for (uint32_t gi = 0; gi < nspace; ++gi)
+        if (ix.gram_off[gi + 1] > ix.gram_off[gi]) {
+            ix.gram_row[gi] = (uint32_t)rows.size();
+            rows.push_back(gi);
+            max_len = std::max<uint64_t>(max_len, ix.gram_off[gi + 1] - ix.gram_off[gi]);
+        }
+    // K: up to kMaxBuckets buckets of >= kMinBucketTerms terms; more (a power of two) when the
+    // lists are dense, so that the longest list has about kDenseBucketLen postings per bucket and
+    // a query's parts stay whole buckets (small gram sizes: 1,369 2-grams over 40M terms), as
+    // long as the table stays within kSkipBudget bytes
+    skip_buckets(n_long, (uint32_t)rows.size(), max_len, ix.n_buckets, ix.bucket_span);
+    const uint32_t K = ix.n_buckets;
+    ix.skip.assign((size_t)rows.size() * (K + 1), 0);
+    run([&](unsigned t) {
+        for (size_t r = t; r < rows.size(); r += threads) {
+            const uint32_t gi = rows[r];
+            const uint32_t* p = ix.post.data() + ix.gram_off[gi];
+            const uint32_t len = (uint32_t)(ix.gram_off[gi + 1] - ix.gram_off[gi]);
+            uint32_t* out = ix.skip.data() + r * (K + 1);
+            uint32_t i = 0;
+            for (uint32_t b = 0; b <= K; ++b) {
+                const uint64_t lo = (uint64_t)b * ix.bucket_span;
+                while (i < len && p[i] < lo) ++i;
+                out[b] = i;
+            }
+            out[K] = len;
+        }
+    });
+    pt.mark("skip table");
+    ix.grams_built = true;
+}
+
 template <typename CharT>
 static void build_impl(HostIndex& ix, const CharT* const* words, uint64_t size, uint16_t rowSize,
                        const float* weight, uint32_t g, unsigned threads) {
@@ -336,145 +478,18 @@ static void build_impl(HostIndex& ix, const CharT* const* words, uint64_t size, 
     std::vector<Pair>().swap(pairs);
 
     pt.mark("term->key CSR");
-    // gram CSR over longLib, two passes, term-range parallel (postings stay sorted by term id)
-    const uint32_t n_long = ix.n_terms - ix.n_short;
-    if (!threads) threads = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-    threads = std::max(1u, std::min<unsigned>(threads, n_long / 4096 + 1));
-    auto range = [&](unsigned t, uint32_t& b, uint32_t& e) {
-        b = ix.n_short + (uint32_t)((uint64_t)n_long * t / threads);
-        e = ix.n_short + (uint32_t)((uint64_t)n_long * (t + 1) / threads);
-    };
-    auto run = [&](auto&& body) {
-        std::vector<std::thread> th;
-        for (unsigned t = 0; t < threads; ++t) th.emplace_back(body, t);
-        for (auto& x : th) x.join();
-    };
-    const CharT* tchars = reinterpret_cast<const CharT*>(ix.term_bytes.data());
-    // dictionary mode: distinct gram keys -> ids in key order; the device looks them up in an
-    // open-addressing table (ghash)
-    U64Map dict;
-    uint32_t nspace = kGramSpace;
-    if (ix.gram_mode == 1) {
-        std::vector<U64Map> sets(threads);
-        run([&](unsigned t) {
-            uint32_t b, e;
-            range(t, b, e);
-            sets[t].init(1024);
-            for (uint32_t id = b; id < e; ++id) {
-                const uint32_t L = (uint32_t)(ix.term_off[id + 1] - ix.term_off[id]);
-                const CharT* p = tchars + ix.term_off[id];
-                for (uint32_t i = 0; i + g <= L; ++i) sets[t].insert(gram_key(p + i, g));
-            }
-        });
-        std::vector<uint64_t> all;
-        for (auto& st : sets)
-            for (uint64_t k : st.key)
-                if (k != ~0ull) all.push_back(k);
-        sets.clear();
-        std::sort(all.begin(), all.end());
-        all.erase(std::unique(all.begin(), all.end()), all.end());
-        dict.init(all.size() + 1);
-        for (uint32_t i = 0; i < all.size(); ++i) dict.insert(all[i]);
-        for (size_t i = 0; i < dict.key.size(); ++i)
-            if (dict.key[i] != ~0ull)
-                dict.val[i] = (uint32_t)(std::lower_bound(all.begin(), all.end(), dict.key[i]) - all.begin());
-        nspace = (uint32_t)all.size();
-        ix.ghash_key = dict.key;
-        ix.ghash_val = dict.val;
-        ix.ghash_bits = dict.bits;
-    }
-    // distinct grams of one long term (ngrams[h].insert(id) deduplicates per term, hpp:13-21)
-    auto grams_of = [&](uint32_t id, std::vector<uint32_t>& gv) -> uint32_t {
-        const uint32_t L = (uint32_t)(ix.term_off[id + 1] - ix.term_off[id]);
-        if (L > gv.size()) gv.resize(L);
-        if (ix.gram_mode == 0) return term_grams(ix.term_bytes.data() + ix.term_off[id], L, gv.data());
-        const CharT* p = tchars + ix.term_off[id];
-        uint32_t n = 0;
-        for (uint32_t i = 0; i + g <= L; ++i) gv[n++] = dict.find(gram_key(p + i, g));
-        std::sort(gv.begin(), gv.begin() + n);
-        return (uint32_t)(std::unique(gv.begin(), gv.begin() + n) - gv.begin());
-    };
-    ix.gram_off.assign((size_t)nspace + 1, 0);
-    std::vector<std::vector<uint32_t>> counts(threads, std::vector<uint32_t>(nspace, 0));
-    run([&](unsigned t) {
-        uint32_t b, e;
-        range(t, b, e);
-        std::vector<uint32_t> gv(64);
-        uint32_t* c = counts[t].data();
-        for (uint32_t id = b; id < e; ++id) {
-            uint32_t n = grams_of(id, gv);
-            for (uint32_t i = 0; i < n; ++i) c[gv[i]]++;
-        }
-    });
-    {
-        uint64_t o = 0;
-        for (uint32_t gi = 0; gi < nspace; ++gi) {
-            ix.gram_off[gi] = o;
-            uint64_t tot = 0;
-            for (unsigned t = 0; t < threads; ++t) {
-                uint32_t c = counts[t][gi];
-                counts[t][gi] = (uint32_t)(o + tot);  // becomes this thread's write cursor
-                tot += c;
-            }
-            ix.n_grams += tot != 0;
-            o += tot;
-        }
-        ix.gram_off[nspace] = o;
-        ix.post.resize(o);
-    }
-    run([&](unsigned t) {
-        uint32_t b, e;
-        range(t, b, e);
-        std::vector<uint32_t> gv(64);
-        uint32_t* cur = counts[t].data();
-        for (uint32_t id = b; id < e; ++id) {
-            uint32_t n = grams_of(id, gv);
-            for (uint32_t i = 0; i < n; ++i) ix.post[cur[gv[i]]++] = id - ix.n_short;
-        }
-    });
-    counts.clear();
-    pt.mark("gram CSR");
-    // bucket skip table: for every non-empty list, the offset of its first posting in each of
-    // K equal term-id buckets. Lets a query cut its lists into term-id parts with one load per
-    // (gram, bucket) instead of a binary search (DESIGN.md §Index layout).
-    ix.gram_row.assign(nspace, UINT32_MAX);
-    std::vector<uint32_t> rows;
-    uint64_t max_len = 0;
-    for (uint32_t gi = 0; gi < nspace; ++gi)
-        if (ix.gram_off[gi + 1] > ix.gram_off[gi]) {
-            ix.gram_row[gi] = (uint32_t)rows.size();
-            rows.push_back(gi);
-            max_len = std::max<uint64_t>(max_len, ix.gram_off[gi + 1] - ix.gram_off[gi]);
-        }
-    // K: up to kMaxBuckets buckets of >= kMinBucketTerms terms; more (a power of two) when the
-    // lists are dense, so that the longest list has about kDenseBucketLen postings per bucket and
-    // a query's parts stay whole buckets (small gram sizes: 1,369 2-grams over 40M terms), as
-    // long as the table stays within kSkipBudget bytes
-    ix.n_buckets = 1;
-    while (ix.n_buckets < kMaxBuckets && (uint64_t)ix.n_buckets * kMinBucketTerms < n_long) ix.n_buckets <<= 1;
-    while ((uint64_t)ix.n_buckets * 2 <= n_long && max_len / ix.n_buckets > kDenseBucketLen &&
-           (uint64_t)rows.size() * (ix.n_buckets * 2 + 1) * sizeof(uint32_t) <= kSkipBudget)
-        ix.n_buckets <<= 1;
-    ix.bucket_span = n_long ? (n_long + ix.n_buckets - 1) / ix.n_buckets : 1;
-    const uint32_t K = ix.n_buckets;
-    ix.skip.assign((size_t)rows.size() * (K + 1), 0);
-    run([&](unsigned t) {
-        for (size_t r = t; r < rows.size(); r += threads) {
-            const uint32_t gi = rows[r];
-            const uint32_t* p = ix.post.data() + ix.gram_off[gi];
-            const uint32_t len = (uint32_t)(ix.gram_off[gi + 1] - ix.gram_off[gi]);
-            uint32_t* out = ix.skip.data() + r * (K + 1);
-            uint32_t i = 0;
-            for (uint32_t b = 0; b <= K; ++b) {
-                const uint64_t lo = (uint64_t)b * ix.bucket_span;
-                while (i < len && p[i] < lo) ++i;
-                out[b] = i;
-            }
-            out[K] = len;
-        }
-    });
-    pt.mark("skip table");
     ix.indexed = true;                                                    // hpp:45
+    // narrow 3-grams: the GPU builds the gram CSR and the skip table at upload (ngs_build.hip)
+    // unless NGS_HOST_GRAMS is set; every other shape builds them here
+    ix.grams_built = false;
+    if (ix.gram_mode == 0 && !std::getenv("NGS_HOST_GRAMS")) return;
+    build_grams_impl<CharT>(ix, threads, pt);
+}
+
+void build_grams_host(HostIndex& ix, unsigned threads) {
+    PhaseTimer pt;
+    if (ix.csize == 1) build_grams_impl<uint8_t>(ix, threads, pt);
+    else build_grams_impl<uint32_t>(ix, threads, pt);
 }
 
 void build_index(HostIndex& ix, char* const* words, uint64_t size, uint16_t rowSize, const float* weight,

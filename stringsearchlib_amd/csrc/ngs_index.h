@@ -20,6 +20,7 @@ namespace ngs {
 
 struct HostIndex {
     bool indexed = false;                   // nGramSearch.h:301
+    bool grams_built = false;               // gram CSR + skip table on the host (else the GPU builds them)
     // characters: 1 byte (indexN / indexG) or 4 (indexW, UTF-32); offsets below count characters
     uint32_t csize = 1, gsz = 3;
     // 0: gram = 21-bit code of 3 ASCII bytes, direct-indexed; 1: gram dictionary (ghash)
@@ -54,6 +55,10 @@ void build_index_g(HostIndex& ix, char* const* words, uint64_t size, uint16_t ro
                    uint32_t gsz, unsigned threads = 0);
 void build_index_w(HostIndex& ix, const uint32_t* const* words, uint64_t size, uint16_t rowSize,
                    const float* weight, uint32_t gsz, unsigned threads = 0);
+
+// The gram CSR and skip table of an index whose terms are laid out (grams_built == false): the
+// host fallback of the device build.
+void build_grams_host(HostIndex& ix, unsigned threads = 0);
 
 // Wildcard answer: keys sorted by (wild_w desc, rank asc).
 void wildcard_order(const HostIndex& ix, std::vector<uint32_t>& keys, std::vector<float>& scores);
