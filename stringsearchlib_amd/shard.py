@@ -23,12 +23,37 @@ def compact(counts: torch.Tensor, keys: torch.Tensor, scores: torch.Tensor, stri
     return counts, keys.view(B, stride)[mask], scores.view(B, stride)[mask]
 
 
-def gather_to_root(counts: torch.Tensor, pkeys: torch.Tensor, pscores: torch.Tensor, group=None):
+class PendingGather:
+    """An in-flight gather (``gather_to_root(..., async_op=True)``): ``wait()`` returns what the
+    blocking call returns (the per-rank lists on rank 0, None elsewhere)."""
+
+    def __init__(self, work, buf, bufs, o, pad_k, rank):
+        self.work, self.buf, self.bufs, self.o, self.pad_k, self.rank = work, buf, bufs, o, pad_k, rank
+
+    def complete(self):
+        """Orders the current stream after the gather (no host synchronisation, no decode)."""
+        self.work.wait()
+
+    def wait(self):
+        self.work.wait()
+        if self.rank != 0:
+            return None
+        out = []
+        o, pad_k = self.o, self.pad_k
+        for b in self.bufs:
+            nk, nb = int(b[0]), int(b[1])
+            out.append((b[2:2 + nb], b[o:o + nk], b[o + pad_k:o + pad_k + nk].view(torch.float32)))
+        return out
+
+
+def gather_to_root(counts: torch.Tensor, pkeys: torch.Tensor, pscores: torch.Tensor, group=None,
+                   async_op: bool = False):
     """Gathers every rank's (counts, packed keys, packed scores) on rank 0.
 
     Two collectives: an all-reduce of the packed length (so every rank pads to the same
     size) and one gather of a single fused buffer per rank. Returns the per-rank lists on
-    rank 0 and None elsewhere."""
+    rank 0 and None elsewhere; with ``async_op`` the gather stays in flight (RCCL runs it on
+    its own stream, beside the next batch's kernels) and a PendingGather is returned."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     dev = counts.device
@@ -44,11 +69,6 @@ def gather_to_root(counts: torch.Tensor, pkeys: torch.Tensor, pscores: torch.Ten
     buf[o:o + pkeys.numel()] = pkeys.to(torch.int32)
     buf[o + pad_k:o + pad_k + pscores.numel()] = pscores.contiguous().view(torch.int32)
     bufs = [torch.empty_like(buf) for _ in range(world)] if rank == 0 else None
-    dist.gather(buf, bufs, dst=0, group=group)
-    if rank != 0:
-        return None
-    out = []
-    for b in bufs:
-        nk, nb = int(b[0]), int(b[1])
-        out.append((b[2:2 + nb], b[o:o + nk], b[o + pad_k:o + pad_k + nk].view(torch.float32)))
-    return out
+    work = dist.gather(buf, bufs, dst=0, group=group, async_op=True)
+    pending = PendingGather(work, buf, bufs, o, pad_k, rank)
+    return pending if async_op else pending.wait()

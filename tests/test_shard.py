@@ -52,6 +52,12 @@ def _worker(rank, world, port, result_path):
         stride = LIMIT
         c, k, s = shard.compact(*_device_layout(oi, queries[lo:hi], stride), stride)
         got = shard.gather_to_root(c, k, s)
+        # the in-flight form bench.py uses: same buffers once waited for
+        got_async = shard.gather_to_root(c, k, s, async_op=True).wait()
+        if rank == 0:
+            assert all(torch.equal(a, b) for x, y in zip(got, got_async) for a, b in zip(x, y))
+        else:
+            assert got is None and got_async is None
         if rank == 0:
             flat = []
             for counts, keys, scores in got:
