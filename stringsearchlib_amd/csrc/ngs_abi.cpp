@@ -93,6 +93,21 @@ struct Context {
     }
 };
 
+// The side stream runs tier 1b on the heavy list beside tier 1a. At the highest priority
+// (NGS_SIDE_PRIO=1) its workgroups are dispatched first, so the few long heavy queries start
+// at once instead of queueing behind tier 1a's.
+hipError_t make_side_stream(hipStream_t* s) {
+    static const bool prio = [] {
+        const char* e = std::getenv("NGS_SIDE_PRIO");
+        return e ? std::atoi(e) != 0 : kSidePriority;
+    }();
+    if (!prio) return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+    int lo = 0, hi = 0;
+    hipError_t e = hipDeviceGetStreamPriorityRange(&lo, &hi);
+    if (e != hipSuccess) return e;
+    return hipStreamCreateWithPriority(s, hipStreamNonBlocking, hi);
+}
+
 struct Library {
     HostIndex host;
     int device = 0;
@@ -127,7 +142,7 @@ struct Library {
         auto c = std::make_unique<Context>();
         c->device = device;
         if (!HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) ||
-            !HIP_CHECK(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking)) ||
+            !HIP_CHECK(make_side_stream(&c->side)) ||
             !HIP_CHECK(hipEventCreateWithFlags(&c->fork, hipEventDisableTiming)) ||
             !HIP_CHECK(hipEventCreateWithFlags(&c->join, hipEventDisableTiming)))
             return nullptr;
@@ -329,6 +344,11 @@ int device_search(Library& L, Context& c, const uint8_t* d_raw, const uint64_t* 
         return w == 1 || w == 2 || w == 4 ? w : kHeavyWaves;
     }();
     P.heavy_waves = heavy_waves;
+    static const uint32_t heavy_grid = [] {
+        const char* e = std::getenv("NGS_HEAVY_GRID");
+        return e ? (uint32_t)std::strtoul(e, nullptr, 0) : kHeavyGrid;
+    }();
+    P.heavy_grid = heavy_grid;
     {
         std::lock_guard<std::mutex> g(L.valid_mu);
         std::memcpy(P.valid, L.valid, sizeof(P.valid));

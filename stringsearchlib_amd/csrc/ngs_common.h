@@ -105,6 +105,8 @@ constexpr int kLeanWavesPerSimd = NGS_LEAN_WPS; // tier 1a: 6 -> <= 80 VGPRs (LD
 constexpr bool kLeanCandInTable = NGS_LEAN_CAND_IN_TABLE != 0;
 constexpr uint32_t kHeavyCmin = 2;              // queries with cmin <= 2 go to tier 1b from the start
 constexpr uint32_t kHeavyWaves = 1;             // ... on this many waves per query
+constexpr uint32_t kHeavyGrid = 4096;           // ... by this many workgroups (grid-stride)
+constexpr bool kSidePriority = false;           // ... on a highest-priority stream
 #ifndef NGS_SHRINK2
 #define NGS_SHRINK2 0
 #endif
@@ -171,6 +173,7 @@ struct SearchParams {
     uint32_t dbg;        // ablation switches for performance experiments (NGS_DEBUG); 0 in production
     uint32_t waves;      // tier 1: 0 = lean 1a + full 1b, or 1, 2, 4 waves per query in the full kernel only (NGS_WAVES)
     uint32_t heavy_waves;  // waves per query of tier 1b on the heavy list (kHeavyWaves; NGS_HEAVY_WAVES)
+    uint32_t heavy_grid;   // workgroups of tier 1b on the heavy list (kHeavyGrid; NGS_HEAVY_GRID)
 };
 
 // per-query normalised length sentinels written by the prep kernel

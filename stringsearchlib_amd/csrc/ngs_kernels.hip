@@ -1802,16 +1802,17 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
         case 0: {
             // tier 1b on the prep kernel's heavy list, on the side stream beside tier 1a
             const uint32_t g1b = std::min<uint32_t>(P.n_queries, 4096);  // grid-stride over the list
+            const uint32_t gh = std::min<uint32_t>(P.n_queries, P.heavy_grid ? P.heavy_grid : 4096);
             if ((e = hipEventRecord(fork, s)) != hipSuccess || (e = hipStreamWaitEvent(side, fork, 0)) != hipSuccess)
                 return e;
             if (P.heavy_waves == 4)
-                hipLaunchKernelGGL(k_wave<4>, dim3(g1b), dim3(256), 0, side, X, P, qnorm, off, qm, out_n, out_k,
+                hipLaunchKernelGGL(k_wave<4>, dim3(gh), dim3(256), 0, side, X, P, qnorm, off, qm, out_n, out_k,
                                    out_s, list2, count2, stats, heavy, hcount);
             else if (P.heavy_waves == 2)
-                hipLaunchKernelGGL(k_wave<2>, dim3(g1b), dim3(128), 0, side, X, P, qnorm, off, qm, out_n, out_k,
+                hipLaunchKernelGGL(k_wave<2>, dim3(gh), dim3(128), 0, side, X, P, qnorm, off, qm, out_n, out_k,
                                    out_s, list2, count2, stats, heavy, hcount);
             else
-                hipLaunchKernelGGL(k_wave<1>, dim3(g1b), dim3(64), 0, side, X, P, qnorm, off, qm, out_n, out_k,
+                hipLaunchKernelGGL(k_wave<1>, dim3(gh), dim3(64), 0, side, X, P, qnorm, off, qm, out_n, out_k,
                                    out_s, list2, count2, stats, heavy, hcount);
             if ((e = hipEventRecord(join, side)) != hipSuccess) return e;
             hipLaunchKernelGGL(k_wave_lean, dim3(P.n_queries), dim3(64), 0, s, X, P, qnorm, off, qm, out_n, out_k,
