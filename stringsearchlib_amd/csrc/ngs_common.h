@@ -119,25 +119,11 @@ constexpr int kWaveTarget = kWaveCap * 5 / 8;   // postings per exact part the b
 constexpr int kSketchTarget = kSketchCap * NGS_TGT8 / 8;  // ... per sketch part (bucket groups aim at NGS_TGT8/8 of the cap)
 constexpr uint32_t kStray = 0xFFFFFFFFu;        // staged entry outside its list segment
 constexpr int kWaveSurv = 128;                  // survivor list (term, count) before calcScore
-constexpr uint32_t kWaveMaxGrams = 63;
-#ifndef NGS_BND
-#define NGS_BND 0  // 1: preload part boundaries to LDS (measured slower: occupancy)
-#endif
-constexpr bool kBndOn = NGS_BND != 0;
-#ifndef NGS_SINGLE
-#define NGS_SINGLE 0  // 1: one register buffer per part (no prefetch of the next part; fewer VGPRs)
-#endif
-constexpr bool kSingleBuf = NGS_SINGLE != 0;
+constexpr uint32_t kWaveMaxGrams = 63;          // counts <= 63: one lane per count value
 #ifndef NGS_SK2
 #define NGS_SK2 2     // smallest cmin counted by the sketch (below: exact hash counting)
 #endif
 constexpr uint32_t kSketchMinCmin = NGS_SK2;
-#ifndef NGS_ASMATOM
-#define NGS_ASMATOM 0  // 1: each round's four sketch adds issued together from inline asm
-#endif
-constexpr bool kAsmAtomics = NGS_ASMATOM != 0;
-constexpr int kBndLists = 16;                   // part boundaries preloaded to LDS for queries of <= 16 lists
-constexpr int kBndParts = 48;                   // ... and <= 48 bucket groups          // counts <= 63: one lane per count value
 
 struct DevIndex {  // passed by value to kernels; all pointers are device pointers
     const uint64_t* gram_off;   // [kGramSpace + 1] -> post

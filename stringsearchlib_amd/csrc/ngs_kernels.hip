@@ -718,7 +718,6 @@ struct alignas(16) WaveSmem {
     uint32_t cbuf[64];               // sketch candidates (terms)
     uint8_t surv_c[kWaveSurv];       // hit count, | 0x80 for a Levenshtein (short search) match count
     uint32_t q[kWaveMaxGrams + 8];   // normalised query, one code point per entry
-    uint32_t bnd[kBndOn ? kBndLists * (kBndParts + 1) : 1];  // part boundaries: [g * (kBndParts + 1) + j] = skip[row of list g][min(K, j * w)]
     uint32_t surv_total;             // stats
     uint32_t ncand;                  // sketch candidates of the part, all waves
     uint32_t x_surv_n, x_cand_n;     // wave 0's emit state, handed round in exact-path turns
@@ -1114,36 +1113,14 @@ __device__ __forceinline__ uint32_t part_sketch(WaveSmem<W, LEAN>& S, const uint
     for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) {
         if (64 * r < mt) {
             const uint32_t t[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
-            if constexpr (kAsmAtomics) {
-                // the round's four adds in flight together, one wait (the compiler, short of
-                // registers, would wait after each returning add)
-                uint32_t a[4], x[4], sh[4], o[4];
+            // (issuing the four returning adds together, one wait, was measured no faster: the
+            // other waves of the SIMD already cover the LDS latency)
 #pragma unroll
-                for (uint32_t e = 0; e < 4; ++e) {
-                    const uint32_t c = sketch_cell<W, LEAN>(t[e]);
-                    sh[e] = (c & 7u) << 2;
-                    a[e] = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint32_t*)&S.table[c >> 3];
-                    x[e] = ((vmask >> (4 * r + e)) & 1u) << sh[e];
-                }
-                asm volatile(
-                    "ds_add_rtn_u32 %0, %4, %8\n\t"
-                    "ds_add_rtn_u32 %1, %5, %9\n\t"
-                    "ds_add_rtn_u32 %2, %6, %10\n\t"
-                    "ds_add_rtn_u32 %3, %7, %11\n\t"
-                    "s_waitcnt lgkmcnt(0)"
-                    : "=&v"(o[0]), "=&v"(o[1]), "=&v"(o[2]), "=&v"(o[3])
-                    : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3])
-                    : "memory");
-#pragma unroll
-                for (uint32_t e = 0; e < 4; ++e) ovf |= ((o[e] >> sh[e]) & kSketchMax) == kSketchMax;
-            } else {
-#pragma unroll
-                for (uint32_t e = 0; e < 4; ++e) {
-                    const uint32_t c = sketch_cell<W, LEAN>(t[e]);
-                    const uint32_t sh = (c & 7u) << 2;
-                    const uint32_t old = atomicAdd(&S.table[c >> 3], ((vmask >> (4 * r + e)) & 1u) << sh);
-                    ovf |= ((old >> sh) & kSketchMax) == kSketchMax;
-                }
+            for (uint32_t e = 0; e < 4; ++e) {
+                const uint32_t c = sketch_cell<W, LEAN>(t[e]);
+                const uint32_t sh = (c & 7u) << 2;
+                const uint32_t old = atomicAdd(&S.table[c >> 3], ((vmask >> (4 * r + e)) & 1u) << sh);
+                ovf |= ((old >> sh) & kSketchMax) == kSketchMax;
             }
         }
     }
@@ -1361,31 +1338,14 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
         const uint32_t a0 = (uint32_t)gbase & 3u;  // list start within its 16-byte chunk
         // entries [s, e) of this lane's list cover 16-byte chunks [(a0 + s) / 4, (a0 + e + 3) / 4)
         auto chunks = [a0](uint32_t s, uint32_t e) -> uint32_t { return e > s ? ((a0 + e + 3) >> 2) - ((a0 + s) >> 2) : 0u; };
-        // part boundaries: the skip-table entries at every w-th bucket of every list, loaded once
-        // per query (one strided load per list) into LDS, so that planning a part never waits on
-        // a dependent global load (that latency, paid per part, was most of the loop time)
-        const uint32_t nb = (K + w - 1) / w + 1;  // boundaries j = 0 .. nb-1 at bucket min(K, j * w)
-        const bool pre = kBndOn && W == 1 && ng <= (uint32_t)kBndLists && nb <= (uint32_t)kBndParts + 1;
-        if (pre) {  // LDS-DMA: lane j's dword lands at row g, column j (no VGPRs, one wait)
-            for (uint32_t g = 0; g < ng; ++g) {
-                const uint32_t row = __builtin_amdgcn_readlane(grow, g);
-                if (lane < nb)
-                    __builtin_amdgcn_global_load_lds(X.skip + (size_t)row * (K + 1) + min(K, lane * w),
-                                                     (__attribute__((address_space(3))) void*)(S.bnd + g * (kBndParts + 1)),
-                                                     4, 0, 0);
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            wave_sync();
-        }
-        // end of the next bucket part (group jn + 1): skip[row][min(K, (jn + 1) * w)]; idle lanes load
-        // nothing (a shared row would be a hot spot)
-        auto next_end = [&](uint32_t bn, uint32_t jn) -> uint32_t {
-            return pre ? S.bnd[lane * (kBndParts + 1) + min(jn + 1, nb - 1)] : sk[min(K, bn + w)];
-        };
+        // end of the next bucket part: skip[row][min(K, bn + w)]; idle lanes load nothing (a shared
+        // row would be a hot spot). (Preloading every boundary of the query into LDS was measured
+        // slower: the LDS it takes costs occupancy.)
+        auto next_end = [&](uint32_t bn) -> uint32_t { return sk[min(K, bn + w)]; };
         // part iterator: buckets [bnext, bnext + w) unless they exceed kChunks, then term-id sub-parts
-        uint32_t cur = 0, bnext = 0, jnext = 0;  // jnext = bnext / w
+        uint32_t cur = 0, bnext = 0;
         uint32_t e_pre = 0;
-        if (lane < ng) e_pre = next_end(0, 0);
+        if (lane < ng) e_pre = next_end(0);
         uint32_t in_sub = 0;
         uint32_t sub_lo = 0, hi_lim = 0, sub_end = 0, sub_bnext = 0, step = 1;
         // software pipeline in registers: part i+1's loads are in flight while part i is counted
@@ -1395,8 +1355,8 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
 #pragma unroll
         for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) pv[r] = make_uint4(0, 0, 0, 0);
         for (uint32_t guard = 0;;) {
-            // the part to count: the one staged last iteration (double buffer), or with a single
-            // buffer the one staged below in this iteration
+            // the part to count: the one staged last iteration (double buffer; one buffer with the
+            // loads waited for in place was measured slower)
             uint4 cv[kDmaRounds];
             uint32_t c_vm = 0, c_mt = 0, c_lo = 0, c_hi = 0;
             bool have_c = false;
@@ -1409,14 +1369,13 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
                 c_hi = p_hi;
                 have_c = have_p;
             };
-            if constexpr (!kSingleBuf) take();
+            take();
             WSTAMP(2);
             // ---- next part: [lo, ...) with per-lane segments [gbase + cur, gbase + cur + len) ----
             uint32_t lo = 0, hi_t = 0, len = 0;  // part: term ids [lo, hi_t)
             have_p = false;
             in_sub = __builtin_amdgcn_readfirstlane(in_sub);
             bnext = __builtin_amdgcn_readfirstlane(bnext);
-            jnext = __builtin_amdgcn_readfirstlane(jnext);
             // common case, straight-line: the next group of w buckets is non-empty and fits
             // (span * w <= kMaxPartSpan holds by the choice of w)
             bool fast = false;
@@ -1427,9 +1386,8 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
                     lo = bnext * span;
                     len = e - cur;
                     bnext = min(K, bnext + w);
-                    ++jnext;
                     hi_t = (uint32_t)min64((uint64_t)bnext * span, n_long);
-                    if (lane < ng) e_pre = next_end(bnext, jnext);
+                    if (lane < ng) e_pre = next_end(bnext);
                     have_p = true;
                     fast = true;
                 }
@@ -1438,8 +1396,7 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
                 // loop-carried part state is wave-uniform: keep it in SGPRs
                 guard = __builtin_amdgcn_readfirstlane(guard);
                 bnext = __builtin_amdgcn_readfirstlane(bnext);
-                jnext = __builtin_amdgcn_readfirstlane(jnext);
-                sub_lo = __builtin_amdgcn_readfirstlane(sub_lo);
+                    sub_lo = __builtin_amdgcn_readfirstlane(sub_lo);
                 step = __builtin_amdgcn_readfirstlane(step);
                 if (++guard > 8u * K + 4096u) {
                     atomicOr(err, 4u);  // every lane (idempotent): a lane-0 branch would make the loop divergent
@@ -1453,9 +1410,8 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
                         lo = bnext * span;
                         len = e - cur;
                         bnext = bhi;
-                        ++jnext;
-                        hi_t = (uint32_t)min64((uint64_t)bhi * span, n_long);
-                        if (lane < ng) e_pre = next_end(bnext, jnext);
+                            hi_t = (uint32_t)min64((uint64_t)bhi * span, n_long);
+                        if (lane < ng) e_pre = next_end(bnext);
                         if (tot) { have_p = true; break; }
                         continue;
                     }
@@ -1492,8 +1448,7 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
                 if (sub_lo >= hi_lim) {
                     in_sub = 0;
                     bnext = sub_bnext;
-                    ++jnext;
-                    if (lane < ng) e_pre = next_end(bnext, jnext);
+                    if (lane < ng) e_pre = next_end(bnext);
                 }
                 if (t2) { have_p = true; break; }
                 cur = a;
@@ -1508,7 +1463,6 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
                 cur += len;
             }
             WSTAMP(4);
-            if constexpr (kSingleBuf) take();
             // ---- count part i while part i+1 is in flight ----
             if (have_c && !(P.dbg & 1u)) {  // dbg 1: load only, no counting
                 if (wid == 0 && surv_n + 64 > (uint32_t)kWaveSurv) {
