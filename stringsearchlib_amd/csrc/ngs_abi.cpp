@@ -56,8 +56,9 @@ bool dev_upload(T** p, const std::vector<T>& v, std::vector<void*>& owned, size_
 struct Context {
     int device = 0;
     hipStream_t stream = nullptr;
-    hipStream_t side = nullptr;      // tier 1b on heavy queries, beside tier 1a
-    hipEvent_t fork = nullptr, join = nullptr;
+    hipStream_t side = nullptr;      // the heavy list (cmin 2) beside tier 1a
+    hipStream_t side2 = nullptr;     // tier 1b on the full list (cmin 1, short search) beside both
+    hipEvent_t fork = nullptr, join = nullptr, join2 = nullptr;
     hipEvent_t ev[6] = {};
     size_t qcap = 0, bcap = 0, ncap = 0, ocap = 0;
     uint8_t* d_raw = nullptr;
@@ -66,9 +67,15 @@ struct Context {
     uint32_t* d_qm = nullptr;
     uint32_t* d_glist = nullptr;
     uint32_t* d_list2 = nullptr;
-    uint32_t* d_gcount = nullptr;  // [0] general-path count, [1] tier-2 count, [2] tier-1b hand-overs, [3] heavy
+    uint32_t* d_gcount = nullptr;  // [0] general-path count, [1] tier-2 count, [2] tier-1b hand-overs, [3] heavy,
+                                   // [4] hand-overs of the heavy list's lean launch, [5] full list
     uint32_t* d_fb = nullptr;      // queries tier 1a handed to tier 1b
-    uint32_t* d_heavy = nullptr;   // queries the prep kernel routed to tier 1b
+    uint32_t* d_fb2 = nullptr;     // ... from the heavy list (side stream)
+    uint32_t* d_heavy = nullptr;   // queries the prep kernel listed as heavy (cmin 2)
+    uint32_t* d_full = nullptr;    // ... for tier 1b (cmin 1, short search)
+    uint32_t* d_esn = nullptr;     // tier 1a survivor lists for k_emit: count per query,
+    uint32_t* d_est = nullptr;     // kEmitCap terms and
+    uint8_t* d_esc = nullptr;      // kEmitCap hit counts per query
     uint32_t* d_group = nullptr;
     DevStats* d_stats = nullptr;
     uint32_t* d_n = nullptr;
@@ -80,16 +87,18 @@ struct Context {
 
     ~Context() {
         hipSetDevice(device);
-        for (void* p : {(void*)d_raw, (void*)d_off, (void*)d_norm, (void*)d_qm, (void*)d_glist, (void*)d_list2, (void*)d_fb, (void*)d_heavy, (void*)d_gcount,
+        for (void* p : {(void*)d_raw, (void*)d_off, (void*)d_norm, (void*)d_qm, (void*)d_glist, (void*)d_list2, (void*)d_fb, (void*)d_fb2, (void*)d_heavy, (void*)d_full, (void*)d_gcount,
+                        (void*)d_esn, (void*)d_est, (void*)d_esc,
                         (void*)d_group, (void*)d_stats, (void*)d_n, (void*)d_k, (void*)d_s, (void*)gen.cnt,
                         (void*)gen.kenc, (void*)gen.list, (void*)gen.sorted, (void*)gen.lcount, gen.temp})
             if (p) hipFree(p);
         for (hipEvent_t e : ev)
             if (e) hipEventDestroy(e);
-        for (hipEvent_t e : {fork, join})
+        for (hipEvent_t e : {fork, join, join2})
             if (e) hipEventDestroy(e);
         if (stream) hipStreamDestroy(stream);
         if (side) hipStreamDestroy(side);
+        if (side2) hipStreamDestroy(side2);
     }
 };
 
@@ -142,13 +151,14 @@ struct Library {
         auto c = std::make_unique<Context>();
         c->device = device;
         if (!HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) ||
-            !HIP_CHECK(make_side_stream(&c->side)) ||
+            !HIP_CHECK(make_side_stream(&c->side)) || !HIP_CHECK(make_side_stream(&c->side2)) ||
             !HIP_CHECK(hipEventCreateWithFlags(&c->fork, hipEventDisableTiming)) ||
-            !HIP_CHECK(hipEventCreateWithFlags(&c->join, hipEventDisableTiming)))
+            !HIP_CHECK(hipEventCreateWithFlags(&c->join, hipEventDisableTiming)) ||
+            !HIP_CHECK(hipEventCreateWithFlags(&c->join2, hipEventDisableTiming)))
             return nullptr;
         for (hipEvent_t& e : c->ev)
             if (!HIP_CHECK(hipEventCreate(&e))) return nullptr;
-        if (!dev_alloc(&c->d_gcount, 4) || !dev_alloc(&c->d_group, 64) || !dev_alloc(&c->d_stats, kStatSlots)) return nullptr;
+        if (!dev_alloc(&c->d_gcount, 6) || !dev_alloc(&c->d_group, 64) || !dev_alloc(&c->d_stats, kStatSlots)) return nullptr;
         return c;
     }
     void give_back(std::unique_ptr<Context> c) {
@@ -267,11 +277,12 @@ bool upload(Library& L) {
 bool ensure_queries(Context& c, size_t B, size_t bytes) {
     if (B > c.bcap) {
         for (void** p : {(void**)&c.d_off, (void**)&c.d_qm, (void**)&c.d_glist, (void**)&c.d_list2, (void**)&c.d_fb,
-                         (void**)&c.d_heavy})
+                         (void**)&c.d_fb2, (void**)&c.d_heavy, (void**)&c.d_full, (void**)&c.d_esn, (void**)&c.d_est, (void**)&c.d_esc})
             if (*p) { hipFree(*p); *p = nullptr; }
         size_t nb = std::max<size_t>(B, 1024);
         if (!dev_alloc(&c.d_off, nb + 1) || !dev_alloc(&c.d_qm, nb) || !dev_alloc(&c.d_glist, nb) ||
-            !dev_alloc(&c.d_list2, nb) || !dev_alloc(&c.d_fb, nb) || !dev_alloc(&c.d_heavy, nb))
+            !dev_alloc(&c.d_list2, nb) || !dev_alloc(&c.d_fb, nb) || !dev_alloc(&c.d_fb2, nb) || !dev_alloc(&c.d_heavy, nb) || !dev_alloc(&c.d_full, nb) ||
+            !dev_alloc(&c.d_esn, nb) || !dev_alloc(&c.d_est, nb * kEmitCap) || !dev_alloc(&c.d_esc, nb * kEmitCap))
             return false;
         c.bcap = nb;
     }
@@ -354,23 +365,27 @@ int device_search(Library& L, Context& c, const uint8_t* d_raw, const uint64_t* 
         std::memcpy(P.valid, L.valid, sizeof(P.valid));
     }
     if (!ensure_queries(c, B, qbytes)) return -4;
+    P.esn = c.d_esn;
+    P.est = c.d_est;
+    P.esc = c.d_esc;
     const bool timing = L.timing.load();
     ngs_stats st{};
     st.queries = B;
     if (!HIP_CHECK(hipMemsetAsync(c.d_stats, 0, sizeof(DevStats) * kStatSlots, s))) return -4;
-    if (!HIP_CHECK(hipMemsetAsync(c.d_gcount, 0, 4 * sizeof(uint32_t), s))) return -4;
+    if (!HIP_CHECK(hipMemsetAsync(c.d_gcount, 0, 6 * sizeof(uint32_t), s))) return -4;
     if (timing) HIP_CHECK(hipEventRecord(c.ev[0], s));
     if (!HIP_CHECK(launch_prep(d_raw, d_off, B, P, c.d_norm, c.d_qm, L.dev.csize, L.dev, c.d_heavy, c.d_gcount + 3,
-                               s)))
+                               c.d_full, c.d_gcount + 5, s)))
         return -4;
     if (timing) HIP_CHECK(hipEventRecord(c.ev[1], s));
     if (timing) HIP_CHECK(hipEventRecord(c.ev[2], s));
     if (!HIP_CHECK(launch_fast(L.dev, P, c.d_norm, d_off, c.d_qm, d_n, d_k, d_s, c.d_list2, c.d_gcount + 1,
-                               c.d_fb, c.d_gcount + 2, c.d_heavy, c.d_gcount + 3, c.d_glist, c.d_gcount, c.d_stats,
-                               s, c.side, c.fork, c.join)))
+                               c.d_fb, c.d_gcount + 2, c.d_fb2, c.d_gcount + 4, c.d_heavy, c.d_gcount + 3, c.d_full,
+                               c.d_gcount + 5, c.d_glist, c.d_gcount, c.d_stats, s, c.side, c.side2, c.fork, c.join,
+                               c.join2)))
         return -4;
     if (timing) HIP_CHECK(hipEventRecord(c.ev[3], s));
-    uint32_t counts3[4] = {0, 0, 0, 0};  // general, tier 2, tier 1a hand-overs, heavy
+    uint32_t counts3[6] = {};  // general, tier 2, tier 1a hand-overs, heavy, heavy hand-overs, full
     if (!HIP_CHECK(hipMemcpyAsync(counts3, c.d_gcount, sizeof(counts3), hipMemcpyDeviceToHost, s)) ||
         !HIP_CHECK(hipStreamSynchronize(s)))
         return -4;
@@ -414,7 +429,8 @@ int device_search(Library& L, Context& c, const uint8_t* d_raw, const uint64_t* 
         st.fast_queries = ds.fast;
         st.general_queries = ngen;
         st.tier2_queries = counts3[1];
-        st.handover_queries = counts3[2] + counts3[3];
+        // queries tier 1b ran: hand-overs of both lean launches and the full list
+        st.handover_queries = counts3[2] + counts3[4] + counts3[5];
         st.postings = ds.postings;
         st.lists = ds.lists;
         st.results = ds.results;

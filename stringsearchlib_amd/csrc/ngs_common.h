@@ -103,7 +103,29 @@ constexpr int kLeanWavesPerSimd = NGS_LEAN_WPS; // tier 1a: 6 -> <= 80 VGPRs (LD
 // ends; a query with more survivors than the survivor list holds goes to tier 1b), or in its
 // own 2 KB (calcScore mid-loop like tier 1b, 8 KB of LDS)
 constexpr bool kLeanCandInTable = NGS_LEAN_CAND_IN_TABLE != 0;
-constexpr uint32_t kHeavyCmin = 2;              // queries with cmin <= 2 go to tier 1b from the start
+#ifndef NGS_DEFER_EMIT
+#define NGS_DEFER_EMIT 1
+#endif
+// tier 1a writes its survivor list (term, count) to HBM and k_emit runs calcScore and the top-L
+// per query afterwards: the dependent term -> key loads and the sorts leave the occupancy-bound
+// counting kernel (SearchParams.esn / est / esc)
+constexpr bool kDeferEmit = NGS_DEFER_EMIT != 0;
+constexpr uint32_t kNoEmit = 0xFFFFFFFFu;       // esn[q]: query not finished by tier 1a
+constexpr uint32_t kEmitHeavy = 0x80000000u;    // esn[q] flag: finished by the heavy-list launch
+#ifndef NGS_HEAVY_CMIN
+#define NGS_HEAVY_CMIN 2
+#endif
+constexpr uint32_t kHeavyCmin = NGS_HEAVY_CMIN; // queries with cmin <= this go to the heavy list from the start
+#ifndef NGS_HEAVY_LEAN
+#define NGS_HEAVY_LEAN 1
+#endif
+// the heavy list runs through the lean kernel (its survivors spill to k_emit; cmin-1 and
+// short-search queries hand over to tier 1b), else through tier 1b directly
+constexpr bool kHeavyLean = NGS_HEAVY_LEAN != 0;
+#ifndef NGS_LEAN_SHRINK2
+#define NGS_LEAN_SHRINK2 1
+#endif
+constexpr uint32_t kLeanShrink2 = NGS_LEAN_SHRINK2;  // tier 1a cmin-2 sketch parts: cap and target >> this
 constexpr uint32_t kHeavyWaves = 1;             // ... on this many waves per query
 constexpr uint32_t kHeavyGrid = 4096;           // ... by this many workgroups (grid-stride)
 constexpr bool kSidePriority = false;           // ... on a highest-priority stream
@@ -119,6 +141,7 @@ constexpr int kWaveTarget = kWaveCap * 5 / 8;   // postings per exact part the b
 constexpr int kSketchTarget = kSketchCap * NGS_TGT8 / 8;  // ... per sketch part (bucket groups aim at NGS_TGT8/8 of the cap)
 constexpr uint32_t kStray = 0xFFFFFFFFu;        // staged entry outside its list segment
 constexpr int kWaveSurv = 128;                  // survivor list (term, count) before calcScore
+constexpr uint32_t kEmitCap = 1024;             // tier 1a survivors per query spilled to HBM for k_emit
 constexpr uint32_t kWaveMaxGrams = 63;          // counts <= 63: one lane per count value
 #ifndef NGS_SK2
 #define NGS_SK2 2     // smallest cmin counted by the sketch (below: exact hash counting)
@@ -160,6 +183,12 @@ struct SearchParams {
     uint32_t waves;      // tier 1: 0 = lean 1a + full 1b, or 1, 2, 4 waves per query in the full kernel only (NGS_WAVES)
     uint32_t heavy_waves;  // waves per query of tier 1b on the heavy list (kHeavyWaves; NGS_HEAVY_WAVES)
     uint32_t heavy_grid;   // workgroups of tier 1b on the heavy list (kHeavyGrid; NGS_HEAVY_GRID)
+    uint32_t lean_all;     // tier 1a also takes heavy queries (its launch over the heavy list)
+    // deferred calcScore (kDeferEmit): per query the survivor count (kNoEmit = none) and
+    // kEmitCap survivor slots, terms and hit counts
+    uint32_t* esn;
+    uint32_t* est;
+    uint8_t* esc;
 };
 
 // per-query normalised length sentinels written by the prep kernel

@@ -11,7 +11,7 @@ namespace ngs {
 // qnorm (same offsets as the raw bytes) and its length into qm (kQueryWildcard for ""/"*").
 hipError_t launch_prep(const uint8_t* raw, const uint64_t* off, uint32_t B, const SearchParams& P,
                        uint8_t* qnorm, uint32_t* qm, uint32_t cs, const DevIndex& X, uint32_t* heavy,
-                       uint32_t* hcount, hipStream_t s);
+                       uint32_t* hcount, uint32_t* full, uint32_t* fcount, hipStream_t s);
 
 // Fused per-query kernel: short Levenshtein scan of shortLib (4 <= m < 9), 3-gram posting
 // count in an LDS hash table per term-id part, threshold, term->key weighting, per-key max
@@ -20,9 +20,10 @@ hipError_t launch_prep(const uint8_t* raw, const uint64_t* off, uint32_t B, cons
 // per query over list2: <= 255 grams, limit <= 1024); what remains goes to glist.
 hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* qnorm, const uint64_t* off,
                        const uint32_t* qm, uint32_t* out_n, uint32_t* out_k, float* out_s, uint32_t* list2,
-                       uint32_t* count2, uint32_t* fb, uint32_t* fbc, const uint32_t* heavy,
-                       const uint32_t* hcount, uint32_t* glist, uint32_t* gcount, DevStats* stats, hipStream_t s,
-                       hipStream_t side, hipEvent_t fork, hipEvent_t join);
+                       uint32_t* count2, uint32_t* fb, uint32_t* fbc, uint32_t* fb2, uint32_t* fbc2,
+                       const uint32_t* heavy, const uint32_t* hcount, const uint32_t* full,
+                       const uint32_t* fcount, uint32_t* glist, uint32_t* gcount, DevStats* stats, hipStream_t s,
+                       hipStream_t side, hipStream_t side2, hipEvent_t fork, hipEvent_t join, hipEvent_t join2);
 
 // Wildcard answer (nGramSearch.hpp:356-369): keys sorted by (weight desc, rank asc).
 hipError_t build_wildcard(const float* d_w, uint32_t n_keys, uint32_t* d_keys, float* d_scores, hipStream_t s);

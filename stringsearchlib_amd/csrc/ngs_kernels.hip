@@ -57,21 +57,25 @@ __device__ __forceinline__ uint32_t char_at(const uint8_t* base, uint64_t i, uin
     return cs == 4 ? reinterpret_cast<const uint32_t*>(base)[i] : (uint32_t)base[i];
 }
 
-// Queries tier 1a would hand over anyway, known from the normalised length alone: a short search
-// over shortLib (m < 3g, hpp:381), or a match-count threshold cmin <= 2, where every term sharing
-// a (g+1)-gram with the query survives (hundreds of calcScore survivors, or exact counting at
-// cmin 1). The prep kernel lists them for tier 1b up front, which then runs beside tier 1a.
-// cmin is computed exactly as the wave kernel does: the first c with !((float)c / n < thr).
-__device__ __forceinline__ bool heavy_query(const DevIndex& X, const SearchParams& P, uint32_t m) {
-    if (m == kQueryWildcard || m == 0 || m <= X.full_scan_len) return false;
+// Queries tier 1a leaves to a launch of their own, known from the normalised length alone:
+// 1 (heavy list) match-count threshold cmin == 2, where every term sharing a (g+1)-gram with the
+//   query survives: hundreds of survivors, which the heavy list's lean launch spills to k_emit
+//   (kHeavyLean);
+// 2 (full list, tier 1b) cmin 1, which needs exact counting, or a short search over shortLib
+//   (m < 3g, hpp:381); without kHeavyLean also cmin 2.
+// Both run beside tier 1a. cmin is computed exactly as the wave kernel does: the first c with
+// !((float)c / n < thr).
+__device__ __forceinline__ uint32_t heavy_class(const DevIndex& X, const SearchParams& P, uint32_t m) {
+    if (m == kQueryWildcard || m == 0 || m <= X.full_scan_len) return 0;
     const uint32_t n = m - X.gsz + 1;
-    if (n > kWaveMaxGrams || P.limit > kWaveMaxLimit) return false;  // tier 2
-    if (m < X.short_query_len && X.n_short) return true;
+    if (n > kWaveMaxGrams || P.limit > kWaveMaxLimit) return 0;  // tier 2
+    if (m < X.short_query_len && X.n_short) return 2;
     const float fn = (float)n;
     uint32_t cmin = 1000u;
     for (uint32_t c = n; c >= 1; --c)
         if (!((float)c / fn < P.thr)) cmin = c;
-    return cmin <= kHeavyCmin;
+    if (cmin > kHeavyCmin) return 0;
+    return kHeavyLean && cmin >= kSketchMinCmin ? 1 : 2;
 }
 
 // ---------------------------------------------------------------- normalisation ------
@@ -79,7 +83,8 @@ __device__ __forceinline__ bool heavy_query(const DevIndex& X, const SearchParam
 __global__ __launch_bounds__(64) void k_prep(const uint8_t* __restrict__ raw, const uint64_t* __restrict__ off,
                                              uint32_t B, SearchParams P, uint8_t* __restrict__ qnorm,
                                              uint32_t* __restrict__ qm, uint32_t cs, DevIndex X,
-                                             uint32_t* __restrict__ heavy, uint32_t* __restrict__ hcount) {
+                                             uint32_t* __restrict__ heavy, uint32_t* __restrict__ hcount,
+                                             uint32_t* __restrict__ full, uint32_t* __restrict__ fcount) {
     const uint32_t q = blockIdx.x;
     if (q >= B) return;
     const uint32_t lane = threadIdx.x;
@@ -115,7 +120,9 @@ __global__ __launch_bounds__(64) void k_prep(const uint8_t* __restrict__ raw, co
     const uint32_t mq = (uint32_t)(m > 0xFFFFFFF0ull ? 0xFFFFFFF0ull : m);
     if (lane == 0) {
         qm[q] = mq;
-        if (heavy && heavy_query(X, P, mq)) heavy[atomicAdd(hcount, 1u)] = q;
+        const uint32_t hk = heavy ? heavy_class(X, P, mq) : 0u;
+        if (hk == 1) heavy[atomicAdd(hcount, 1u)] = q;
+        if (hk == 2) full[atomicAdd(fcount, 1u)] = q;
     }
 }
 
@@ -805,8 +812,8 @@ __device__ __forceinline__ uint32_t wave_incl_max_scan(uint32_t v) {
 }
 
 // Wave-local running top-L over the candidate buffer (same algorithm as flush()).
-template <int W, bool LEAN>
-__device__ void wave_flush(WaveSmem<W, LEAN>& S, uint32_t& cand_n, uint64_t& tau, uint32_t L) {
+template <class SM>
+__device__ void wave_flush(SM& S, uint32_t& cand_n, uint64_t& tau, uint32_t L) {
     const uint32_t lane = lane_id();
     const uint32_t n = min(cand_n, (uint32_t)kWaveCand);
     const uint32_t P2 = next_pow2(max(n, 2u));
@@ -855,8 +862,8 @@ __device__ void wave_flush(WaveSmem<W, LEAN>& S, uint32_t& cand_n, uint64_t& tau
 
 // calcScore (nGramSearch.hpp:310-341) over the survivor list: term -> (key, weight) pairs,
 // max(w*s, 0), exact-match promotion, into the running top-L.
-template <int W, bool LEAN>
-__device__ void wave_emit(WaveSmem<W, LEAN>& S, const DevIndex& X, const SearchParams& P, uint32_t m, uint32_t L,
+template <class SM>
+__device__ void wave_emit(SM& S, const DevIndex& X, const SearchParams& P, uint32_t m, uint32_t L,
                           float sc_long, float sc_short, uint32_t& surv_n, uint32_t& cand_n, uint64_t& tau) {
     const uint32_t lane = lane_id();
     S.surv_total += surv_n;
@@ -1205,7 +1212,7 @@ __device__ __forceinline__ uint32_t part_sketch(WaveSmem<W, LEAN>& S, const uint
 // exact-count pass, no mid-loop calcScore and no short search, which keeps the kernel within 96
 // VGPRs (5 waves per SIMD); a query that needs any of those is appended to fb[] untouched and
 // rerun from scratch by the full kernel (tier 1b).
-template <int W, bool LEAN>
+template <int W, bool LEAN, bool DEFER = false>
 __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t q, const DevIndex& X, const SearchParams& P,
                                            const uint8_t* __restrict__ qnorm, const uint64_t* __restrict__ qoff,
                                            const uint32_t* __restrict__ qm, uint32_t* __restrict__ out_n,
@@ -1260,6 +1267,21 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
     grp_sync<W>();
     uint32_t cand_n = 0, surv_n = 0;
     uint64_t tau = kNoCand;
+    // tier 1a with DEFER: the survivor list goes to this query's kEmitCap slots in HBM
+    // (spilled of them written so far); false if they are full (the query is handed over)
+    uint32_t spilled = 0;
+    auto spill = [&]() -> bool {
+        if (spilled + surv_n > kEmitCap) return false;
+        uint32_t* et = P.est + (size_t)q * kEmitCap + spilled;
+        uint8_t* ec = P.esc + (size_t)q * kEmitCap + spilled;
+        for (uint32_t i = lane; i < surv_n; i += 64) {
+            et[i] = S.surv_t[i];
+            ec[i] = S.surv_c[i];
+        }
+        spilled += surv_n;
+        surv_n = 0;
+        return true;
+    };
     unsigned* err = &stats->errors;
     // lane c holds the fp32 score of c hits: (float)c / n (hpp:300) and (float)c / m (hpp:244)
     const float sc_long = lane <= n ? (float)lane / (float)n : 0.0f;
@@ -1267,8 +1289,8 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
     // the smallest hit count whose score passes the threshold (hpp:300,315)
     const unsigned long long pm = __ballot(lane <= n && lane > 0 && !(sc_long < P.thr));
     const uint32_t cmin = pm ? (uint32_t)(__ffsll((long long)pm) - 1) : 1000u;
-    // the queries heavy_query() lists in k_prep are tier 1b's (same test, same cmin)
-    if (LEAN && (cmin <= kHeavyCmin || (m < X.short_query_len && X.n_short))) return;
+    // the queries heavy_class() lists in k_prep run in launches of their own (same test, same cmin)
+    if (LEAN && !P.lean_all && (cmin <= kHeavyCmin || (m < X.short_query_len && X.n_short))) return;
 
     // ---- searchShort over shortLib (nGramSearch.hpp:262-270), 4 <= m < 9, wave 0 ----
     if constexpr (LEAN) {
@@ -1324,7 +1346,7 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
     // sketch counting for 2 <= cmin <= 15; at cmin 2 two colliding entries already make a false
     // candidate, so those parts are cut at half the size
     const bool sketch = cmin >= kSketchMinCmin && cmin <= kSketchMax;
-    const uint32_t shrink = cmin == 2 ? kShrink2 : 0u;
+    const uint32_t shrink = cmin == 2 ? (LEAN ? kLeanShrink2 : kShrink2) : 0u;
     // part cap: a sketch part holds twice the entries of an exact pass (u8 vs u32 cells)
     const uint32_t kChunks = ((sketch ? (uint32_t)kWaveChunks : (uint32_t)kExactChunks) * W) >> shrink;
     WSTAMP(1);
@@ -1466,7 +1488,10 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
             // ---- count part i while part i+1 is in flight ----
             if (have_c && !(P.dbg & 1u)) {  // dbg 1: load only, no counting
                 if (wid == 0 && surv_n + 64 > (uint32_t)kWaveSurv) {
-                    if constexpr (LEAN && kLeanCandInTable) { bail(); return; }
+                    if constexpr (LEAN && DEFER) {
+                        if (!spill()) { bail(); return; }
+                        wave_sync();  // the list is read before it is refilled
+                    } else if constexpr (LEAN && kLeanCandInTable) { bail(); return; }
                     else wave_emit(S, X, P, m, L, sc_long, sc_short, surv_n, cand_n, tau);
                 }
                 const uint32_t nc = sketch ? part_sketch(S, cv, c_vm, c_mt, cmin, X.n_short, X.n_terms, surv_n, P.dbg) : 65u;
@@ -1518,6 +1543,18 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
     }
     WSTAMP(7);
     if (wid != 0) return;
+    if constexpr (LEAN && DEFER) {  // calcScore + top-L in k_emit
+        if (!spill()) { bail(); return; }
+        if (lane == 0) P.esn[q] = spilled | (P.lean_all ? kEmitHeavy : 0u);
+        if (lane == 0 && !(P.dbg & 32u)) {
+            DevStats* sl = stats + (q & (kStatSlots - 1));
+            atomicAdd(&sl->postings, (unsigned long long)p_total);
+            atomicAdd(&sl->lists, (unsigned long long)ng);
+            atomicAdd(&sl->fast, 1ull);
+            atomicAdd(&sl->survivors, (unsigned long long)spilled);
+        }
+        return;
+    }
     if (surv_n) wave_emit(S, X, P, m, L, sc_long, sc_short, surv_n, cand_n, tau);
     WSTAMP(8);
     wave_flush(S, cand_n, tau, L);
@@ -1573,7 +1610,9 @@ __global__ __launch_bounds__(64 * W, kWaveWavesPerSimd) void k_wave(DevIndex X, 
     }
 }
 
-// Tier 1a: the lean wave kernel over every query.
+// Tier 1a: the lean wave kernel over every query (qlist == nullptr), or over the heavy list.
+// DEFER: survivors spill to HBM for k_emit (the heavy launch always; the main one if kDeferEmit).
+template <bool DEFER>
 __global__ __launch_bounds__(64, kLeanWavesPerSimd) void k_wave_lean(DevIndex X, SearchParams P,
                                                                     const uint8_t* __restrict__ qnorm,
                                                                     const uint64_t* __restrict__ qoff,
@@ -1584,9 +1623,78 @@ __global__ __launch_bounds__(64, kLeanWavesPerSimd) void k_wave_lean(DevIndex X,
                                                                     uint32_t* __restrict__ list2,
                                                                     uint32_t* __restrict__ count2,
                                                                     DevStats* __restrict__ stats,
-                                                                    uint32_t* __restrict__ fb, uint32_t* __restrict__ fbc) {
+                                                                    uint32_t* __restrict__ fb, uint32_t* __restrict__ fbc,
+                                                                    const uint32_t* __restrict__ qlist,
+                                                                    const uint32_t* __restrict__ qcount) {
     __shared__ WaveSmem<1, true> S;
-    wave_query<1, true>(S, blockIdx.x, X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats, fb, fbc);
+    if (!qlist) {
+        wave_query<1, true, DEFER>(S, blockIdx.x, X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats,
+                                   fb, fbc);
+        return;
+    }
+    const uint32_t cnt = *qcount;  // the heavy list, grid-stride
+    for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
+        wave_query<1, true, DEFER>(S, qlist[i], X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats,
+                                   fb, fbc);
+        wave_sync();
+    }
+}
+
+// Tier 1a's calcScore (nGramSearch.hpp:310-341) and top-L (hpp:397-401), one wave per query
+// over the survivor list k_wave_lean left in HBM (DEFER), for every query or the heavy list: the
+// same wave_emit / wave_flush
+// as the fused path, in 5 KB of LDS.
+struct EmitSmem {
+    uint64_t cand_own[kWaveCand];
+    __device__ __forceinline__ uint64_t* cand() { return cand_own; }
+    uint32_t surv_t[kEmitCap];
+    uint8_t surv_c[kEmitCap];
+    uint32_t q[kWaveMaxGrams + 8];
+    uint32_t surv_total;
+};
+
+__global__ __launch_bounds__(64) void k_emit(DevIndex X, SearchParams P, const uint8_t* __restrict__ qnorm,
+                                             const uint64_t* __restrict__ qoff, const uint32_t* __restrict__ qm,
+                                             uint32_t* __restrict__ out_n, uint32_t* __restrict__ out_k,
+                                             float* __restrict__ out_s, DevStats* __restrict__ stats,
+                                             const uint32_t* __restrict__ qlist, const uint32_t* __restrict__ qcount) {
+    __shared__ EmitSmem S;
+    const uint32_t lane = threadIdx.x;
+    if (qlist && blockIdx.x >= *qcount) return;
+    const uint32_t q = qlist ? qlist[blockIdx.x] : blockIdx.x;
+    uint32_t sn = P.esn[q];
+    if (sn == kNoEmit) return;  // tier 1a did not finish this query
+    // the main launch leaves the heavy launch's queries to the heavy list's k_emit
+    if (!qlist && (sn & kEmitHeavy)) return;
+    sn &= ~kEmitHeavy;
+    const uint32_t m = qm[q], n = m - X.gsz + 1, L = P.limit;
+    const uint8_t* qg = qnorm + qoff[q];
+    for (uint32_t i = lane; i < m; i += 64) S.q[i] = char_at(qg, i, X.csize);
+    const uint32_t* et = P.est + (size_t)q * kEmitCap;
+    const uint8_t* ec = P.esc + (size_t)q * kEmitCap;
+    for (uint32_t i = lane; i < sn; i += 64) {
+        S.surv_t[i] = et[i];
+        S.surv_c[i] = ec[i];
+    }
+    if (lane == 0) S.surv_total = 0;
+    const float sc_long = lane <= n ? (float)lane / (float)n : 0.0f;  // as wave_query
+    const float sc_short = lane <= m ? (float)lane / (float)m : 0.0f;
+    uint32_t surv_n = sn, cand_n = 0;
+    uint64_t tau = kNoCand;
+    wave_sync();
+    if (surv_n) wave_emit(S, X, P, m, L, sc_long, sc_short, surv_n, cand_n, tau);
+    wave_flush(S, cand_n, tau, L);
+    const size_t ob = (size_t)q * P.out_stride;
+    for (uint32_t i = lane; i < cand_n; i += 64) {
+        const uint64_t r = S.cand()[i];
+        const uint32_t enc = ~(uint32_t)(r >> 32);
+        out_k[ob + i] = (uint32_t)r;
+        out_s[ob + i] = enc == kPromoted ? 100.0f : __uint_as_float(enc - 1u);
+    }
+    if (lane == 0) {
+        out_n[q] = cand_n;
+        if (!(P.dbg & 32u)) atomicAdd(&stats[q & (kStatSlots - 1)].results, (unsigned long long)cand_n);
+    }
 }
 
 // ---------------------------------------------------------------- general path -------
@@ -1738,43 +1846,63 @@ int phase_stats(unsigned long long* out, int n, bool reset) {
 
 hipError_t launch_prep(const uint8_t* raw, const uint64_t* off, uint32_t B, const SearchParams& P, uint8_t* qnorm,
                        uint32_t* qm, uint32_t cs, const DevIndex& X, uint32_t* heavy, uint32_t* hcount,
-                       hipStream_t s) {
+                       uint32_t* full, uint32_t* fcount, hipStream_t s) {
     if (!B) return hipSuccess;
     hipLaunchKernelGGL(k_prep, dim3(B), dim3(64), 0, s, raw, off, B, P, qnorm, qm, cs, X,
-                       P.waves == 0 ? heavy : nullptr, hcount);
+                       P.waves == 0 ? heavy : nullptr, hcount, full, fcount);
     return hipGetLastError();
 }
 
 hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* qnorm, const uint64_t* off,
                        const uint32_t* qm, uint32_t* out_n, uint32_t* out_k, float* out_s, uint32_t* list2,
-                       uint32_t* count2, uint32_t* fb, uint32_t* fbc, const uint32_t* heavy,
-                       const uint32_t* hcount, uint32_t* glist, uint32_t* gcount, DevStats* stats, hipStream_t s,
-                       hipStream_t side, hipEvent_t fork, hipEvent_t join) {
+                       uint32_t* count2, uint32_t* fb, uint32_t* fbc, uint32_t* fb2, uint32_t* fbc2,
+                       const uint32_t* heavy, const uint32_t* hcount, const uint32_t* full,
+                       const uint32_t* fcount, uint32_t* glist, uint32_t* gcount, DevStats* stats, hipStream_t s,
+                       hipStream_t side, hipStream_t side2, hipEvent_t fork, hipEvent_t join, hipEvent_t join2) {
     if (!P.n_queries) return hipSuccess;
     hipError_t e = hipSuccess;
     switch (P.waves) {  // waves per query (SearchParams.waves, NGS_WAVES; 0 = tier 1a + 1b)
         case 0: {
-            // tier 1b on the prep kernel's heavy list, on the side stream beside tier 1a
+            // beside tier 1a: the heavy list through the lean kernel, k_emit and tier 1b on its
+            // hand-overs (side), and the full list through tier 1b (side2)
             const uint32_t g1b = std::min<uint32_t>(P.n_queries, 4096);  // grid-stride over the list
             const uint32_t gh = std::min<uint32_t>(P.n_queries, P.heavy_grid ? P.heavy_grid : 4096);
-            if ((e = hipEventRecord(fork, s)) != hipSuccess || (e = hipStreamWaitEvent(side, fork, 0)) != hipSuccess)
+            if ((e = hipMemsetAsync(P.esn, 0xFF, sizeof(uint32_t) * P.n_queries, s)) != hipSuccess ||
+                (e = hipEventRecord(fork, s)) != hipSuccess || (e = hipStreamWaitEvent(side, fork, 0)) != hipSuccess ||
+                (e = hipStreamWaitEvent(side2, fork, 0)) != hipSuccess)
                 return e;
             if (P.heavy_waves == 4)
-                hipLaunchKernelGGL(k_wave<4>, dim3(gh), dim3(256), 0, side, X, P, qnorm, off, qm, out_n, out_k,
-                                   out_s, list2, count2, stats, heavy, hcount);
+                hipLaunchKernelGGL(k_wave<4>, dim3(gh), dim3(256), 0, side2, X, P, qnorm, off, qm, out_n, out_k,
+                                   out_s, list2, count2, stats, full, fcount);
             else if (P.heavy_waves == 2)
-                hipLaunchKernelGGL(k_wave<2>, dim3(gh), dim3(128), 0, side, X, P, qnorm, off, qm, out_n, out_k,
-                                   out_s, list2, count2, stats, heavy, hcount);
+                hipLaunchKernelGGL(k_wave<2>, dim3(gh), dim3(128), 0, side2, X, P, qnorm, off, qm, out_n, out_k,
+                                   out_s, list2, count2, stats, full, fcount);
             else
-                hipLaunchKernelGGL(k_wave<1>, dim3(gh), dim3(64), 0, side, X, P, qnorm, off, qm, out_n, out_k,
-                                   out_s, list2, count2, stats, heavy, hcount);
+                hipLaunchKernelGGL(k_wave<1>, dim3(gh), dim3(64), 0, side2, X, P, qnorm, off, qm, out_n, out_k,
+                                   out_s, list2, count2, stats, full, fcount);
+            if ((e = hipEventRecord(join2, side2)) != hipSuccess) return e;
+            if (kHeavyLean) {
+                SearchParams PH = P;
+                PH.lean_all = 1;
+                hipLaunchKernelGGL(k_wave_lean<true>, dim3(gh), dim3(64), 0, side, X, PH, qnorm, off, qm, out_n,
+                                   out_k, out_s, list2, count2, stats, fb2, fbc2, heavy, hcount);
+                hipLaunchKernelGGL(k_emit, dim3(gh), dim3(64), 0, side, X, PH, qnorm, off, qm, out_n, out_k, out_s,
+                                   stats, heavy, hcount);
+                hipLaunchKernelGGL(k_wave<1>, dim3(g1b), dim3(64), 0, side, X, P, qnorm, off, qm, out_n, out_k,
+                                   out_s, list2, count2, stats, (const uint32_t*)fb2, (const uint32_t*)fbc2);
+            }
             if ((e = hipEventRecord(join, side)) != hipSuccess) return e;
-            hipLaunchKernelGGL(k_wave_lean, dim3(P.n_queries), dim3(64), 0, s, X, P, qnorm, off, qm, out_n, out_k,
-                               out_s, list2, count2, stats, fb, fbc);
+            hipLaunchKernelGGL(k_wave_lean<kDeferEmit>, dim3(P.n_queries), dim3(64), 0, s, X, P, qnorm, off, qm,
+                               out_n, out_k, out_s, list2, count2, stats, fb, fbc, (const uint32_t*)nullptr,
+                               (const uint32_t*)nullptr);
+            if (kDeferEmit)
+                hipLaunchKernelGGL(k_emit, dim3(P.n_queries), dim3(64), 0, s, X, P, qnorm, off, qm, out_n, out_k,
+                                   out_s, stats, (const uint32_t*)nullptr, (const uint32_t*)nullptr);
             // tier 1b over the queries tier 1a handed over
             hipLaunchKernelGGL(k_wave<1>, dim3(g1b), dim3(64), 0, s, X, P, qnorm, off, qm, out_n, out_k, out_s,
                                list2, count2, stats, (const uint32_t*)fb, (const uint32_t*)fbc);
-            if ((e = hipStreamWaitEvent(s, join, 0)) != hipSuccess) return e;
+            if ((e = hipStreamWaitEvent(s, join, 0)) != hipSuccess || (e = hipStreamWaitEvent(s, join2, 0)) != hipSuccess)
+                return e;
             break;
         }
         case 1:
