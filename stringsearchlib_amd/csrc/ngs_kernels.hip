@@ -1642,15 +1642,11 @@ __global__ __launch_bounds__(64, kLeanWavesPerSimd) void k_wave_lean(DevIndex X,
 
 // Tier 1a's calcScore (nGramSearch.hpp:310-341) and top-L (hpp:397-401), one wave per query
 // over the survivor list k_wave_lean left in HBM (DEFER), for every query or the heavy list: the
-// same wave_emit / wave_flush
-// as the fused path, in 5 KB of LDS.
+// fused path's wave_emit (reading the survivors from HBM) and wave_flush, in 2.3 KB of LDS.
 struct EmitSmem {
     uint64_t cand_own[kWaveCand];
     __device__ __forceinline__ uint64_t* cand() { return cand_own; }
-    uint32_t surv_t[kEmitCap];
-    uint8_t surv_c[kEmitCap];
     uint32_t q[kWaveMaxGrams + 8];
-    uint32_t surv_total;
 };
 
 __global__ __launch_bounds__(64) void k_emit(DevIndex X, SearchParams P, const uint8_t* __restrict__ qnorm,
@@ -1662,6 +1658,10 @@ __global__ __launch_bounds__(64) void k_emit(DevIndex X, SearchParams P, const u
     const uint32_t lane = threadIdx.x;
     if (qlist && blockIdx.x >= *qcount) return;
     const uint32_t q = qlist ? qlist[blockIdx.x] : blockIdx.x;
+    const uint32_t* et = P.est + (size_t)q * kEmitCap;
+    const uint8_t* ec = P.esc + (size_t)q * kEmitCap;
+    // the first 64 survivors load beside the count (the slots always exist): one round trip less
+    uint32_t t = et[lane], code = ec[lane];
     uint32_t sn = P.esn[q];
     if (sn == kNoEmit) return;  // tier 1a did not finish this query
     // the main launch leaves the heavy launch's queries to the heavy list's k_emit
@@ -1670,19 +1670,40 @@ __global__ __launch_bounds__(64) void k_emit(DevIndex X, SearchParams P, const u
     const uint32_t m = qm[q], n = m - X.gsz + 1, L = P.limit;
     const uint8_t* qg = qnorm + qoff[q];
     for (uint32_t i = lane; i < m; i += 64) S.q[i] = char_at(qg, i, X.csize);
-    const uint32_t* et = P.est + (size_t)q * kEmitCap;
-    const uint8_t* ec = P.esc + (size_t)q * kEmitCap;
-    for (uint32_t i = lane; i < sn; i += 64) {
-        S.surv_t[i] = et[i];
-        S.surv_c[i] = ec[i];
-    }
-    if (lane == 0) S.surv_total = 0;
     const float sc_long = lane <= n ? (float)lane / (float)n : 0.0f;  // as wave_query
     const float sc_short = lane <= m ? (float)lane / (float)m : 0.0f;
-    uint32_t surv_n = sn, cand_n = 0;
+    uint32_t cand_n = 0;
     uint64_t tau = kNoCand;
     wave_sync();
-    if (surv_n) wave_emit(S, X, P, m, L, sc_long, sc_short, surv_n, cand_n, tau);
+    // wave_emit over the survivors in HBM
+    for (uint32_t base = 0; base < sn; base += 64) {
+        const uint32_t i = base + lane;
+        if (base) {
+            t = i < sn ? et[i] : 0u;
+            code = i < sn ? ec[i] : 0u;
+        }
+        uint32_t p = 0, pe = 0;
+        if (i < sn) {
+            p = X.tk_off[t];
+            pe = X.tk_off[t + 1];
+        }
+        const float s_l = __shfl(sc_long, (int)(code & 63u)), s_s = __shfl(sc_short, (int)(code & 63u));
+        const float s = (code & 0x80u) ? s_s : s_l;
+        const bool promo = (double)s > 0.999;  // nGramSearch.hpp:328
+        while (__ballot(p < pe)) {
+            uint64_t rec = kNoCand;
+            if (p < pe) {
+                const uint2 kw = X.tk[p++];
+                const uint32_t enc = pair_enc(kw, s, promo, X, S.q, 4u, m, P.valid);
+                rec = ((uint64_t)(~enc) << 32) | kw.x;
+            }
+            if (cand_n + 64 > (uint32_t)kWaveCand) wave_flush(S, cand_n, tau, L);
+            const bool want = rec < tau;
+            const unsigned long long bw = __ballot(want);
+            if (want) S.cand()[cand_n + rank_below(bw)] = rec;
+            cand_n += __popcll(bw);
+        }
+    }
     wave_flush(S, cand_n, tau, L);
     const size_t ob = (size_t)q * P.out_stride;
     for (uint32_t i = lane; i < cand_n; i += 64) {

@@ -1,0 +1,57 @@
+"""Heavy queries (match-count threshold cmin 2) through the lean kernel's spill path, exact vs the
+oracle. At cmin 2 every term sharing a 4-gram with the query survives: the survivors overflow the
+LDS survivor list and spill to HBM for k_emit (up to kEmitCap = 1024 per query), and above that
+the query is handed over to tier 1b. Both corpora use 8-character queries (6 grams, thr 0.3 ->
+cmin 2), as in nGramSearch.hpp:278-301 + 310-341."""
+import random
+
+import pytest
+
+from oracle_py import OracleIndex
+from tiecheck import bits
+
+import stringsearchlib_amd as ssl
+
+pytestmark = pytest.mark.gpu
+
+
+def _words(rng, alphabet, n, lo, hi):
+    return [bytes(rng.choice(alphabet) for _ in range(rng.randint(lo, hi))) for _ in range(n)]
+
+
+def _queries(rng, words, n, qlen=8):
+    out = []
+    for _ in range(n):
+        src = rng.choice([w for w in words if len(w) >= qlen])
+        o = rng.randrange(len(src) - qlen + 1)
+        q = bytearray(src[o:o + qlen])
+        q[rng.randrange(qlen)] = src[0]
+        out.append(bytes(q))
+    return out
+
+
+@pytest.mark.parametrize("alphabet,rows,lo,hi,expect_handover", [
+    (b"ABCDEFGHIJKL", 60000, 10, 30, False),  # a few hundred survivors: spilled, scored by k_emit
+    (b"ABCDEFGH", 40000, 6, 30, True),         # thousands: beyond kEmitCap, tier 1b
+])
+def test_cmin2_spill_parity(alphabet, rows, lo, hi, expect_handover):
+    rng = random.Random(rows + len(alphabet))
+    words = _words(rng, alphabet, rows, lo, hi)
+    wts = [0.5 + rng.random() / 2 for _ in words]
+    gi = ssl.StringIndex(words, 1, wts)
+    gi.set_timing(True)  # ngsLastStats
+    oi = OracleIndex(words, 1, wts)
+    qs = _queries(rng, words, 40)
+    for thr, limit in [(0.3, 100), (0.3, 7)]:
+        got = gi.score_batch(qs, thr, limit)
+        st = gi.last_stats()
+        for q, g in zip(qs, got):
+            ref = oi.score(q, thr, limit)
+            assert len(g) == len(ref), f"q={q!r} thr={thr} limit={limit}: {len(g)} vs {len(ref)}"
+            for i, ((k1, s1), (k2, s2)) in enumerate(zip(g, ref)):
+                assert k1 == k2 and bits(s1) == bits(s2), f"q={q!r} #{i}: {k1!r}|{s1} vs {k2!r}|{s2}"
+        if expect_handover:
+            assert st["handover_queries"] > 0, st
+        else:  # most finish in the lean kernel (a part with > 64 sketch candidates hands over)
+            assert st["handover_queries"] < len(qs) // 4 and st["survivors"] / len(qs) > 128, st
+    gi.dispose()
