@@ -54,4 +54,9 @@ def test_cmin2_spill_parity(alphabet, rows, lo, hi, expect_handover):
             assert st["handover_queries"] > 0, st
         else:  # most finish in the lean kernel (a part with > 64 sketch candidates hands over)
             assert st["handover_queries"] < len(qs) // 4 and st["survivors"] / len(qs) > 128, st
+    # a heavy list longer than the side launches' grids (4096): grid-stride in every stage
+    small = gi.score_batch(qs, 0.3, 100)
+    big = gi.score_batch(qs * 128, 0.3, 100)
+    for i, g in enumerate(big):
+        assert g == small[i % len(qs)], f"batch of {len(big)}: q#{i} differs"
     gi.dispose()
