@@ -274,7 +274,7 @@ def main():
                    "parallelism": f"query-shard x{world}" + (" + RCCL gather of top-k" if world > 1 else "")},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(args.config),
-                     "kernel": "tier-1 phase: k_wave_lean + concurrent k_wave on the heavy list + hand-over k_wave + k_fast (HIP events on the call stream)", "kernel_ms": round(fast_ms, 4), "alg_bytes_per_launch": alg_bytes,
+                     "kernel": "tier-1 phase: k_wave_lean over the batch + k_emit, beside it k_wave_lean + k_emit on the heavy list and k_wave on the full list (side streams), hand-over k_wave, k_fast (HIP events on the call stream)", "kernel_ms": round(fast_ms, 4), "alg_bytes_per_launch": alg_bytes,
                      "postings_per_query": round(st.postings / max(1, st.fast_queries), 1)},
         "detail": {"prep_ms": round(sum(k[1] for k in ktimes) / len(ktimes), 4),
                    "general_ms": round(sum(k[2] for k in ktimes) / len(ktimes), 4),

@@ -77,7 +77,8 @@ struct Context {
     uint32_t* d_est = nullptr;     // kEmitCap terms and
     uint8_t* d_esc = nullptr;      // kEmitCap hit counts per query
     uint32_t* d_group = nullptr;
-    DevStats* d_stats = nullptr;
+    DevStats* d_stats = nullptr;   // kStatSlots slots, then one holding d_gcount (one memset, one read-back)
+    DevStats* h_stats = nullptr;   // pinned host copy of the same
     uint32_t* d_n = nullptr;
     uint32_t* d_k = nullptr;
     float* d_s = nullptr;
@@ -87,11 +88,12 @@ struct Context {
 
     ~Context() {
         hipSetDevice(device);
-        for (void* p : {(void*)d_raw, (void*)d_off, (void*)d_norm, (void*)d_qm, (void*)d_glist, (void*)d_list2, (void*)d_fb, (void*)d_fb2, (void*)d_heavy, (void*)d_full, (void*)d_gcount,
+        for (void* p : {(void*)d_raw, (void*)d_off, (void*)d_norm, (void*)d_qm, (void*)d_glist, (void*)d_list2, (void*)d_fb, (void*)d_fb2, (void*)d_heavy, (void*)d_full,
                         (void*)d_esn, (void*)d_est, (void*)d_esc,
                         (void*)d_group, (void*)d_stats, (void*)d_n, (void*)d_k, (void*)d_s, (void*)gen.cnt,
                         (void*)gen.kenc, (void*)gen.list, (void*)gen.sorted, (void*)gen.lcount, gen.temp})
             if (p) hipFree(p);
+        if (h_stats) hipHostFree(h_stats);
         for (hipEvent_t e : ev)
             if (e) hipEventDestroy(e);
         for (hipEvent_t e : {fork, join, join2})
@@ -158,7 +160,11 @@ struct Library {
             return nullptr;
         for (hipEvent_t& e : c->ev)
             if (!HIP_CHECK(hipEventCreate(&e))) return nullptr;
-        if (!dev_alloc(&c->d_gcount, 6) || !dev_alloc(&c->d_group, 64) || !dev_alloc(&c->d_stats, kStatSlots)) return nullptr;
+        if (!dev_alloc(&c->d_group, 64) || !dev_alloc(&c->d_stats, kStatSlots + 1) ||
+            !HIP_CHECK(hipHostMalloc((void**)&c->h_stats, sizeof(DevStats) * (kStatSlots + 1), hipHostMallocDefault)))
+            return nullptr;
+        c->d_gcount = reinterpret_cast<uint32_t*>(c->d_stats + kStatSlots);
+        static_assert(sizeof(DevStats) >= 6 * sizeof(uint32_t), "the path counts fit one stats slot");
         return c;
     }
     void give_back(std::unique_ptr<Context> c) {
@@ -371,8 +377,7 @@ int device_search(Library& L, Context& c, const uint8_t* d_raw, const uint64_t* 
     const bool timing = L.timing.load();
     ngs_stats st{};
     st.queries = B;
-    if (!HIP_CHECK(hipMemsetAsync(c.d_stats, 0, sizeof(DevStats) * kStatSlots, s))) return -4;
-    if (!HIP_CHECK(hipMemsetAsync(c.d_gcount, 0, 6 * sizeof(uint32_t), s))) return -4;
+    if (!HIP_CHECK(hipMemsetAsync(c.d_stats, 0, sizeof(DevStats) * (kStatSlots + 1), s))) return -4;  // + gcount
     if (timing) HIP_CHECK(hipEventRecord(c.ev[0], s));
     if (!HIP_CHECK(launch_prep(d_raw, d_off, B, P, c.d_norm, c.d_qm, L.dev.csize, L.dev, c.d_heavy, c.d_gcount + 3,
                                c.d_full, c.d_gcount + 5, s)))
@@ -385,10 +390,13 @@ int device_search(Library& L, Context& c, const uint8_t* d_raw, const uint64_t* 
                                c.join2)))
         return -4;
     if (timing) HIP_CHECK(hipEventRecord(c.ev[3], s));
-    uint32_t counts3[6] = {};  // general, tier 2, tier 1a hand-overs, heavy, heavy hand-overs, full
-    if (!HIP_CHECK(hipMemcpyAsync(counts3, c.d_gcount, sizeof(counts3), hipMemcpyDeviceToHost, s)) ||
+    // the statistics and the path counts in one read-back (the general path adds no statistics)
+    if (!HIP_CHECK(hipMemcpyAsync(c.h_stats, c.d_stats, sizeof(DevStats) * (kStatSlots + 1), hipMemcpyDeviceToHost,
+                                  s)) ||
         !HIP_CHECK(hipStreamSynchronize(s)))
         return -4;
+    // general, tier 2, tier 1a hand-overs, heavy, heavy hand-overs, full
+    const uint32_t* counts3 = reinterpret_cast<const uint32_t*>(c.h_stats + kStatSlots);
     const uint32_t ngen = counts3[0];
     if (ngen) {
         std::vector<uint32_t> gl(ngen);
@@ -408,11 +416,9 @@ int device_search(Library& L, Context& c, const uint8_t* d_raw, const uint64_t* 
         }
         if (timing) HIP_CHECK(hipEventRecord(c.ev[5], s));
     }
-    DevStats slots[kStatSlots], ds{};
-    if (!HIP_CHECK(hipMemcpyAsync(slots, c.d_stats, sizeof(slots), hipMemcpyDeviceToHost, s)) ||
-        !HIP_CHECK(hipStreamSynchronize(s)))
-        return -4;
-    for (const DevStats& x : slots) {
+    DevStats ds{};
+    for (uint32_t i = 0; i < kStatSlots; ++i) {
+        const DevStats& x = c.h_stats[i];
         ds.postings += x.postings;
         ds.lists += x.lists;
         ds.results += x.results;

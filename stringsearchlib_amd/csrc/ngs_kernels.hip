@@ -88,6 +88,7 @@ __global__ __launch_bounds__(64) void k_prep(const uint8_t* __restrict__ raw, co
     const uint32_t q = blockIdx.x;
     if (q >= B) return;
     const uint32_t lane = threadIdx.x;
+    if (lane == 0 && P.esn) P.esn[q] = kNoEmit;  // set by tier 1a when it finishes the query (DEFER)
     const uint8_t* rq = raw + off[q];        // query q: characters of cs bytes from byte offset off[q]
     uint8_t* nq = qnorm + off[q];
     const uint64_t n = (off[q + 1] - off[q]) / cs;
@@ -1911,8 +1912,8 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
             // hand-overs (side), and the full list through tier 1b (side2)
             const uint32_t g1b = std::min<uint32_t>(P.n_queries, 4096);  // grid-stride over the list
             const uint32_t gh = std::min<uint32_t>(P.n_queries, P.heavy_grid ? P.heavy_grid : 4096);
-            if ((e = hipMemsetAsync(P.esn, 0xFF, sizeof(uint32_t) * P.n_queries, s)) != hipSuccess ||
-                (e = hipEventRecord(fork, s)) != hipSuccess || (e = hipStreamWaitEvent(side, fork, 0)) != hipSuccess ||
+            // (esn[] was reset by k_prep)
+            if ((e = hipEventRecord(fork, s)) != hipSuccess || (e = hipStreamWaitEvent(side, fork, 0)) != hipSuccess ||
                 (e = hipStreamWaitEvent(side2, fork, 0)) != hipSuccess)
                 return e;
             if (P.heavy_waves == 4)

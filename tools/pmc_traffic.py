@@ -17,25 +17,30 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def main(src, cfg, kernel="k_wave_lean"):
-    """HBM bytes of one search call's tier-1 phase: every k_wave* / k_fast dispatch of the pass
-    (tier 1a, tier 1b on the heavy list and on hand-overs, tier 2), divided by the number of
-    tier-1a dispatches (one per call)."""
+    """HBM bytes of one search call's tier-1 phase: every k_wave* / k_emit / k_fast dispatch of
+    the pass (tier 1a over the batch and over the heavy list, k_emit, tier 1b on the full list
+    and on hand-overs, tier 2), divided by the number of main tier-1a dispatches (one per call:
+    the k_wave_lean dispatches with the largest grid)."""
     fetch = defaultdict(float)
-    names = {}
+    names, grid = {}, {}
     files = glob.glob(os.path.join(src, "**", "run_counter_collection.csv"), recursive=True)
     for f in files:
         with open(f) as fh:
             for r in csv.DictReader(fh):
-                if r["Counter_Name"] == "FETCH_SIZE" and ("k_wave" in r["Kernel_Name"] or "k_fast" in r["Kernel_Name"]):
+                nm = r["Kernel_Name"]
+                if r["Counter_Name"] == "FETCH_SIZE" and ("k_wave" in nm or "k_fast" in nm or "k_emit" in nm):
                     fetch[(f, r["Dispatch_Id"])] += float(r["Counter_Value"])
-                    names[(f, r["Dispatch_Id"])] = r["Kernel_Name"]
-    calls = sum(1 for k in fetch if kernel in names[k])
+                    names[(f, r["Dispatch_Id"])] = nm
+                    grid[(f, r["Dispatch_Id"])] = int(r["Grid_Size"])
+    main_grid = max((grid[k] for k in fetch if kernel in names[k]), default=0)
+    calls = sum(1 for k in fetch if kernel in names[k] and grid[k] == main_grid)
     if not calls:
         raise SystemExit(f"no FETCH_SIZE rows for {kernel} under {src}")
     kib = sum(fetch.values()) / calls
-    lean = sorted(v for k, v in fetch.items() if kernel in names[k])
+    lean = sorted(v for k, v in fetch.items() if kernel in names[k] and grid[k] == main_grid)
     out = {
-        "kernel": "tier-1 phase (k_wave_lean + k_wave heavy + k_wave hand-over + k_fast)",
+        "kernel": "tier-1 phase (k_wave_lean over the batch and the heavy list, k_emit, k_wave on the full "
+                  "list and hand-overs, k_fast)",
         "calls": calls,
         "fetch_size_kib_per_call": kib,
         "fetch_size_kib_k_wave_lean_median": lean[len(lean) // 2],
