@@ -73,11 +73,15 @@ struct Context {
     uint32_t* d_fb2 = nullptr;     // ... from the heavy list (side stream)
     uint32_t* d_heavy = nullptr;   // queries the prep kernel listed as heavy (cmin 2)
     uint32_t* d_full = nullptr;    // ... for tier 1b (cmin 1, short search)
+    uint32_t* d_lslots = nullptr;  // k_prep's slot lists of both (2 * kListSlots * ceil(B / kListSlots))
     uint32_t* d_esn = nullptr;     // tier 1a survivor lists for k_emit: count per query,
     uint32_t* d_est = nullptr;     // kEmitCap terms and
     uint8_t* d_esc = nullptr;      // kEmitCap hit counts per query
     uint32_t* d_group = nullptr;
-    DevStats* d_stats = nullptr;   // kStatSlots slots, then one holding d_gcount (one memset, one read-back)
+    // kStatSlots slots, then one holding d_gcount (one memset, one read-back), then the
+    // 2 * kListSlots counter lines of k_prep's slot lists (d_lctr; same memset, not read back)
+    DevStats* d_stats = nullptr;
+    uint32_t* d_lctr = nullptr;
     DevStats* h_stats = nullptr;   // pinned host copy of the same
     uint32_t* d_n = nullptr;
     uint32_t* d_k = nullptr;
@@ -88,7 +92,7 @@ struct Context {
 
     ~Context() {
         hipSetDevice(device);
-        for (void* p : {(void*)d_raw, (void*)d_off, (void*)d_norm, (void*)d_qm, (void*)d_glist, (void*)d_list2, (void*)d_fb, (void*)d_fb2, (void*)d_heavy, (void*)d_full,
+        for (void* p : {(void*)d_raw, (void*)d_off, (void*)d_norm, (void*)d_qm, (void*)d_glist, (void*)d_list2, (void*)d_fb, (void*)d_fb2, (void*)d_heavy, (void*)d_full, (void*)d_lslots,
                         (void*)d_esn, (void*)d_est, (void*)d_esc,
                         (void*)d_group, (void*)d_stats, (void*)d_n, (void*)d_k, (void*)d_s, (void*)gen.cnt,
                         (void*)gen.kenc, (void*)gen.list, (void*)gen.sorted, (void*)gen.lcount, gen.temp})
@@ -160,10 +164,12 @@ struct Library {
             return nullptr;
         for (hipEvent_t& e : c->ev)
             if (!HIP_CHECK(hipEventCreate(&e))) return nullptr;
-        if (!dev_alloc(&c->d_group, 64) || !dev_alloc(&c->d_stats, kStatSlots + 1) ||
+        if (!dev_alloc(&c->d_group, 64) || !dev_alloc(&c->d_stats, kStatSlots + 1 + 2 * kListSlots) ||
             !HIP_CHECK(hipHostMalloc((void**)&c->h_stats, sizeof(DevStats) * (kStatSlots + 1), hipHostMallocDefault)))
             return nullptr;
         c->d_gcount = reinterpret_cast<uint32_t*>(c->d_stats + kStatSlots);
+        c->d_lctr = reinterpret_cast<uint32_t*>(c->d_stats + kStatSlots + 1);
+        static_assert(sizeof(DevStats) == 16 * sizeof(uint32_t), "k_prep's counters are 16 words apart");
         static_assert(sizeof(DevStats) >= 6 * sizeof(uint32_t), "the path counts fit one stats slot");
         return c;
     }
@@ -283,11 +289,12 @@ bool upload(Library& L) {
 bool ensure_queries(Context& c, size_t B, size_t bytes) {
     if (B > c.bcap) {
         for (void** p : {(void**)&c.d_off, (void**)&c.d_qm, (void**)&c.d_glist, (void**)&c.d_list2, (void**)&c.d_fb,
-                         (void**)&c.d_fb2, (void**)&c.d_heavy, (void**)&c.d_full, (void**)&c.d_esn, (void**)&c.d_est, (void**)&c.d_esc})
+                         (void**)&c.d_fb2, (void**)&c.d_heavy, (void**)&c.d_full, (void**)&c.d_lslots, (void**)&c.d_esn, (void**)&c.d_est, (void**)&c.d_esc})
             if (*p) { hipFree(*p); *p = nullptr; }
         size_t nb = std::max<size_t>(B, 1024);
         if (!dev_alloc(&c.d_off, nb + 1) || !dev_alloc(&c.d_qm, nb) || !dev_alloc(&c.d_glist, nb) ||
             !dev_alloc(&c.d_list2, nb) || !dev_alloc(&c.d_fb, nb) || !dev_alloc(&c.d_fb2, nb) || !dev_alloc(&c.d_heavy, nb) || !dev_alloc(&c.d_full, nb) ||
+            !dev_alloc(&c.d_lslots, 2 * (nb + kListSlots)) ||
             !dev_alloc(&c.d_esn, nb) || !dev_alloc(&c.d_est, nb * kEmitCap) || !dev_alloc(&c.d_esc, nb * kEmitCap))
             return false;
         c.bcap = nb;
@@ -377,10 +384,11 @@ int device_search(Library& L, Context& c, const uint8_t* d_raw, const uint64_t* 
     const bool timing = L.timing.load();
     ngs_stats st{};
     st.queries = B;
-    if (!HIP_CHECK(hipMemsetAsync(c.d_stats, 0, sizeof(DevStats) * (kStatSlots + 1), s))) return -4;  // + gcount
+    // statistics, path counts and list counters
+    if (!HIP_CHECK(hipMemsetAsync(c.d_stats, 0, sizeof(DevStats) * (kStatSlots + 1 + 2 * kListSlots), s))) return -4;
     if (timing) HIP_CHECK(hipEventRecord(c.ev[0], s));
     if (!HIP_CHECK(launch_prep(d_raw, d_off, B, P, c.d_norm, c.d_qm, L.dev.csize, L.dev, c.d_heavy, c.d_gcount + 3,
-                               c.d_full, c.d_gcount + 5, s)))
+                               c.d_full, c.d_gcount + 5, c.d_lslots, c.d_lctr, s)))
         return -4;
     if (timing) HIP_CHECK(hipEventRecord(c.ev[1], s));
     if (timing) HIP_CHECK(hipEventRecord(c.ev[2], s));

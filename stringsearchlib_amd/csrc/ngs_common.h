@@ -110,6 +110,7 @@ constexpr bool kLeanCandInTable = NGS_LEAN_CAND_IN_TABLE != 0;
 // per query afterwards: the dependent term -> key loads and the sorts leave the occupancy-bound
 // counting kernel (SearchParams.esn / est / esc)
 constexpr bool kDeferEmit = NGS_DEFER_EMIT != 0;
+constexpr uint32_t kListSlots = 64;             // slot lists per routing list in k_prep
 constexpr uint32_t kNoEmit = 0xFFFFFFFFu;       // esn[q]: query not finished by tier 1a
 constexpr uint32_t kEmitHeavy = 0x80000000u;    // esn[q] flag: finished by the heavy-list launch
 #ifndef NGS_HEAVY_CMIN

@@ -9,9 +9,13 @@ namespace ngs {
 
 // Normalise every query (escapeBlank -> trim -> toUpper, nGramSearch.hpp:372-376) into
 // qnorm (same offsets as the raw bytes) and its length into qm (kQueryWildcard for ""/"*").
+// The heavy and full lists (tier-1 routing) go through 2 x kListSlots slot lists: `slots` holds
+// 2 * kListSlots * ceil(B / kListSlots) entries, `ctr` 2 * kListSlots counters 16 words apart
+// (zeroed by the caller).
 hipError_t launch_prep(const uint8_t* raw, const uint64_t* off, uint32_t B, const SearchParams& P,
                        uint8_t* qnorm, uint32_t* qm, uint32_t cs, const DevIndex& X, uint32_t* heavy,
-                       uint32_t* hcount, uint32_t* full, uint32_t* fcount, hipStream_t s);
+                       uint32_t* hcount, uint32_t* full, uint32_t* fcount, uint32_t* slots, uint32_t* ctr,
+                       hipStream_t s);
 
 // Fused per-query kernel: short Levenshtein scan of shortLib (4 <= m < 9), 3-gram posting
 // count in an LDS hash table per term-id part, threshold, term->key weighting, per-key max

@@ -79,51 +79,73 @@ __device__ __forceinline__ uint32_t heavy_class(const DevIndex& X, const SearchP
 }
 
 // ---------------------------------------------------------------- normalisation ------
-// One wave per query: ballots find the first / last byte that survives escape + trim.
+// Four queries per wave, 16 lanes each (one query per wave spent 50 us on 65,536 waves of a few
+// dependent loads): 16-lane windows of the wave's ballots find the first / last character that
+// survives escape + trim; the window loops run while any query of the wave still searches.
 __global__ __launch_bounds__(64) void k_prep(const uint8_t* __restrict__ raw, const uint64_t* __restrict__ off,
                                              uint32_t B, SearchParams P, uint8_t* __restrict__ qnorm,
                                              uint32_t* __restrict__ qm, uint32_t cs, DevIndex X,
-                                             uint32_t* __restrict__ heavy, uint32_t* __restrict__ hcount,
-                                             uint32_t* __restrict__ full, uint32_t* __restrict__ fcount) {
-    const uint32_t q = blockIdx.x;
-    if (q >= B) return;
-    const uint32_t lane = threadIdx.x;
-    if (lane == 0 && P.esn) P.esn[q] = kNoEmit;  // set by tier 1a when it finishes the query (DEFER)
-    const uint8_t* rq = raw + off[q];        // query q: characters of cs bytes from byte offset off[q]
-    uint8_t* nq = qnorm + off[q];
-    const uint64_t n = (off[q + 1] - off[q]) / cs;
-    if (n == 0 || (n == 1 && char_at(rq, 0, cs) == '*')) {  // wildcard, nGramSearch.hpp:356
-        if (lane == 0) qm[q] = kQueryWildcard;
-        return;
+                                             uint32_t* __restrict__ slots, uint32_t* __restrict__ ctr, uint32_t cap) {
+    const uint32_t lane = threadIdx.x, gl = lane & 15u, sh = lane & 48u;
+    const uint32_t q = blockIdx.x * 4 + (lane >> 4);
+    const bool live = q < B;
+    const uint8_t* rq = raw;  // query q: characters of cs bytes from byte offset off[q]
+    uint8_t* nq = qnorm;
+    uint64_t n = 0;
+    if (live) {
+        rq = raw + off[q];
+        nq = qnorm + off[q];
+        n = (off[q + 1] - off[q]) / cs;
+        if (gl == 0 && P.esn) P.esn[q] = kNoEmit;  // set by tier 1a when it finishes the query (DEFER)
     }
+    const bool wild = live && (n == 0 || (n == 1 && char_at(rq, 0, cs) == '*'));  // nGramSearch.hpp:356
     uint64_t first = n, last = 0;
-    for (uint64_t base = 0; base < n; base += 64) {
-        const uint64_t i = base + lane;
-        const bool keep = i < n && !dev_space(esc_cs(P.valid, char_at(rq, i, cs), cs));
-        const unsigned long long bal = __ballot(keep);
-        if (bal) { first = base + __ffsll((long long)bal) - 1; break; }
+    bool seek = live && !wild;
+    for (uint64_t base = 0; __ballot(seek); base += 16) {
+        const uint64_t i = base + gl;
+        const bool keep = seek && i < n && !dev_space(esc_cs(P.valid, char_at(rq, i, cs), cs));
+        const uint32_t bal = (uint32_t)(__ballot(keep) >> sh) & 0xFFFFu;
+        if (seek && bal) {
+            first = base + __ffs(bal) - 1;
+            seek = false;
+        } else if (base + 16 >= n) {
+            seek = false;
+        }
     }
-    if (first == n) {  // nothing left after escape + trim, nGramSearch.hpp:374-375
-        if (lane == 0) qm[q] = 0;
-        return;
+    const bool empty = live && !wild && first == n;  // nothing left after escape + trim, hpp:374-375
+    seek = live && !wild && !empty;
+    for (uint64_t base = 0; __ballot(seek); base += 16) {
+        const uint64_t i = n - 1 - (base + gl);
+        const bool keep = seek && base + gl < n && !dev_space(esc_cs(P.valid, char_at(rq, i, cs), cs));
+        const uint32_t bal = (uint32_t)(__ballot(keep) >> sh) & 0xFFFFu;
+        if (seek && bal) {
+            last = n - 1 - (base + __ffs(bal) - 1);
+            seek = false;
+        } else if (base + 16 >= n) {
+            seek = false;
+        }
     }
-    for (uint64_t base = 0; base < n; base += 64) {
-        const uint64_t i = n - 1 - (base + lane);
-        const bool keep = base + lane < n && !dev_space(esc_cs(P.valid, char_at(rq, i, cs), cs));
-        const unsigned long long bal = __ballot(keep);
-        if (bal) { last = n - 1 - (base + __ffsll((long long)bal) - 1); break; }
-    }
-    const uint64_t m = last - first + 1;
-    for (uint64_t i = lane; i < m; i += 64) {
+    const uint64_t m = live && !wild && !empty ? last - first + 1 : 0;
+    for (uint64_t i = gl; i < m; i += 16) {
         const uint32_t c = dev_upper(esc_cs(P.valid, char_at(rq, first + i, cs), cs));
         if (cs == 4) reinterpret_cast<uint32_t*>(nq)[i] = c; else nq[i] = (uint8_t)c;
     }
-    const uint32_t mq = (uint32_t)(m > 0xFFFFFFF0ull ? 0xFFFFFFF0ull : m);
-    if (lane == 0) {
-        qm[q] = mq;
-        const uint32_t hk = heavy ? heavy_class(X, P, mq) : 0u;
-        if (hk == 1) heavy[atomicAdd(hcount, 1u)] = q;
-        if (hk == 2) full[atomicAdd(fcount, 1u)] = q;
+    if (live && gl == 0) {
+        if (wild) {
+            qm[q] = kQueryWildcard;
+        } else if (empty) {
+            qm[q] = 0;
+        } else {
+            const uint32_t mq = (uint32_t)(m > 0xFFFFFFF0ull ? 0xFFFFFFF0ull : m);
+            qm[q] = mq;
+            // heavy / full lists: 64 slot lists with a counter line each (one counter for the
+            // whole batch serialised 3,900 atomics at one address: 57 against 15 us), merged by k_lists
+            const uint32_t hk = slots ? heavy_class(X, P, mq) : 0u;
+            if (hk) {
+                const uint32_t sl = (hk - 1) * kListSlots + (q & (kListSlots - 1));
+                slots[(size_t)sl * cap + atomicAdd(&ctr[16 * sl], 1u)] = q;
+            }
+        }
     }
 }
 
@@ -1889,12 +1911,39 @@ int phase_stats(unsigned long long* out, int n, bool reset) {
 #endif
 }
 
+// The heavy and full lists from k_prep's slot lists: per list, a scan of the 64 slot counts,
+// then the slots' entries copied behind each other (slot order: the lists' order does not matter).
+__global__ __launch_bounds__(256) void k_lists(const uint32_t* __restrict__ slots, const uint32_t* __restrict__ ctr,
+                                               uint32_t cap, uint32_t* __restrict__ heavy, uint32_t* __restrict__ hcount,
+                                               uint32_t* __restrict__ full, uint32_t* __restrict__ fcount) {
+    __shared__ uint32_t base[2 * kListSlots + 2];
+    const uint32_t t = threadIdx.x, lane = t & 63u;
+    if (t < 128) {  // wave 0: heavy slots, wave 1: full slots
+        const uint32_t L = t >> 6, c = ctr[16 * (L * kListSlots + lane)];
+        const uint32_t incl = wave_incl_scan(c);
+        base[L * (kListSlots + 1) + lane + 1] = incl;
+        if (lane == 0) base[L * (kListSlots + 1)] = 0;
+        if (lane == 63) *(L ? fcount : hcount) = incl;
+    }
+    __syncthreads();
+    for (uint32_t sl = t >> 6; sl < 2 * kListSlots; sl += 4) {
+        const uint32_t L = sl / kListSlots, k = sl % kListSlots;
+        const uint32_t b0 = base[L * (kListSlots + 1) + k], n = base[L * (kListSlots + 1) + k + 1] - b0;
+        const uint32_t* src = slots + (size_t)sl * cap;
+        uint32_t* dst = (L ? full : heavy) + b0;
+        for (uint32_t i = lane; i < n; i += 64) dst[i] = src[i];
+    }
+}
+
 hipError_t launch_prep(const uint8_t* raw, const uint64_t* off, uint32_t B, const SearchParams& P, uint8_t* qnorm,
                        uint32_t* qm, uint32_t cs, const DevIndex& X, uint32_t* heavy, uint32_t* hcount,
-                       uint32_t* full, uint32_t* fcount, hipStream_t s) {
+                       uint32_t* full, uint32_t* fcount, uint32_t* slots, uint32_t* ctr, hipStream_t s) {
     if (!B) return hipSuccess;
-    hipLaunchKernelGGL(k_prep, dim3(B), dim3(64), 0, s, raw, off, B, P, qnorm, qm, cs, X,
-                       P.waves == 0 ? heavy : nullptr, hcount, full, fcount);
+    const uint32_t cap = (B + kListSlots - 1) / kListSlots;
+    const bool lists = P.waves == 0;
+    hipLaunchKernelGGL(k_prep, dim3((B + 3) / 4), dim3(64), 0, s, raw, off, B, P, qnorm, qm, cs, X,
+                       lists ? slots : nullptr, ctr, cap);
+    if (lists) hipLaunchKernelGGL(k_lists, dim3(1), dim3(256), 0, s, slots, ctr, cap, heavy, hcount, full, fcount);
     return hipGetLastError();
 }
 
