@@ -110,6 +110,10 @@ constexpr bool kLeanCandInTable = NGS_LEAN_CAND_IN_TABLE != 0;
 // per query afterwards: the dependent term -> key loads and the sorts leave the occupancy-bound
 // counting kernel (SearchParams.esn / est / esc)
 constexpr bool kDeferEmit = NGS_DEFER_EMIT != 0;
+#ifndef NGS_MAIN_FIRST
+#define NGS_MAIN_FIRST 1
+#endif
+constexpr bool kMainFirst = NGS_MAIN_FIRST != 0;  // queue the main tier-1a launch before the side streams'
 constexpr uint32_t kListSlots = 64;             // slot lists per routing list in k_prep
 constexpr uint32_t kNoEmit = 0xFFFFFFFFu;       // esn[q]: query not finished by tier 1a
 constexpr uint32_t kEmitHeavy = 0x80000000u;    // esn[q] flag: finished by the heavy-list launch

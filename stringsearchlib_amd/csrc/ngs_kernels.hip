@@ -1962,8 +1962,16 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
             const uint32_t g1b = std::min<uint32_t>(P.n_queries, 4096);  // grid-stride over the list
             const uint32_t gh = std::min<uint32_t>(P.n_queries, P.heavy_grid ? P.heavy_grid : 4096);
             // (esn[] was reset by k_prep)
-            if ((e = hipEventRecord(fork, s)) != hipSuccess || (e = hipStreamWaitEvent(side, fork, 0)) != hipSuccess ||
-                (e = hipStreamWaitEvent(side2, fork, 0)) != hipSuccess)
+            auto main_lean = [&]() {
+                hipLaunchKernelGGL(k_wave_lean<kDeferEmit>, dim3(P.n_queries), dim3(64), 0, s, X, P, qnorm, off, qm,
+                                   out_n, out_k, out_s, list2, count2, stats, fb, fbc, (const uint32_t*)nullptr,
+                                   (const uint32_t*)nullptr);
+            };
+            if ((e = hipEventRecord(fork, s)) != hipSuccess) return e;
+            // the main launch is queued first: the GPU idled ~35 us while the host queued the side
+            // streams' launches ahead of it
+            if (kMainFirst) main_lean();
+            if ((e = hipStreamWaitEvent(side, fork, 0)) != hipSuccess || (e = hipStreamWaitEvent(side2, fork, 0)) != hipSuccess)
                 return e;
             if (P.heavy_waves == 4)
                 hipLaunchKernelGGL(k_wave<4>, dim3(gh), dim3(256), 0, side2, X, P, qnorm, off, qm, out_n, out_k,
@@ -1986,9 +1994,7 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
                                    out_s, list2, count2, stats, (const uint32_t*)fb2, (const uint32_t*)fbc2);
             }
             if ((e = hipEventRecord(join, side)) != hipSuccess) return e;
-            hipLaunchKernelGGL(k_wave_lean<kDeferEmit>, dim3(P.n_queries), dim3(64), 0, s, X, P, qnorm, off, qm,
-                               out_n, out_k, out_s, list2, count2, stats, fb, fbc, (const uint32_t*)nullptr,
-                               (const uint32_t*)nullptr);
+            if (!kMainFirst) main_lean();
             if (kDeferEmit)
                 hipLaunchKernelGGL(k_emit, dim3((P.n_queries + kEmitWaves - 1) / kEmitWaves), dim3(64 * kEmitWaves), 0,
                                    s, X, P, qnorm, off, qm, out_n, out_k, out_s, stats, (const uint32_t*)nullptr,
