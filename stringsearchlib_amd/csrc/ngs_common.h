@@ -114,6 +114,10 @@ constexpr bool kDeferEmit = NGS_DEFER_EMIT != 0;
 #define NGS_MAIN_FIRST 1
 #endif
 constexpr bool kMainFirst = NGS_MAIN_FIRST != 0;  // queue the main tier-1a launch before the side streams'
+#ifndef NGS_SKIP_COLD
+#define NGS_SKIP_COLD 1
+#endif
+constexpr bool kSkipCold = NGS_SKIP_COLD != 0;  // skip the sketch candidate pass when no cell reached cmin
 constexpr uint32_t kListSlots = 64;             // slot lists per routing list in k_prep
 constexpr uint32_t kNoEmit = 0xFFFFFFFFu;       // esn[q]: query not finished by tier 1a
 constexpr uint32_t kEmitHeavy = 0x80000000u;    // esn[q] flag: finished by the heavy-list launch

@@ -1138,7 +1138,9 @@ __device__ __forceinline__ uint32_t part_sketch(WaveSmem<W, LEAN>& S, const uint
                                                 uint32_t& surv_n, uint32_t dbg) {
     const uint32_t lane = lane_id(), wid = W == 1 ? 0u : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     mt = __builtin_amdgcn_readfirstlane(mt);
-    bool ovf = false;
+    // ovf: a counter wrapped; hot: an add took a cell from cmin - 1 to cmin (every cell that ends
+    // at >= cmin had exactly one such add in this part: the table starts clear and adds are 0/1)
+    bool ovf = false, hot = false;
 #pragma unroll
     for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) {
         if (64 * r < mt) {
@@ -1150,12 +1152,16 @@ __device__ __forceinline__ uint32_t part_sketch(WaveSmem<W, LEAN>& S, const uint
                 const uint32_t c = sketch_cell<W, LEAN>(t[e]);
                 const uint32_t sh = (c & 7u) << 2;
                 const uint32_t old = atomicAdd(&S.table[c >> 3], ((vmask >> (4 * r + e)) & 1u) << sh);
-                ovf |= ((old >> sh) & kSketchMax) == kSketchMax;
+                const uint32_t on = (old >> sh) & kSketchMax;
+                ovf |= on == kSketchMax;
+                if constexpr (kSkipCold && W == 1) hot |= on + 1u == cmin;
             }
         }
     }
     grp_sync<W>();
-    if (dbg & 2u) {  // ablation: add pass only (table cleared, no candidates)
+    bool cold = false;  // no cell reached cmin: no candidates, skip the candidate pass
+    if constexpr (kSkipCold && W == 1) cold = !__ballot(hot || ovf);
+    if ((dbg & 2u) || cold) {  // (dbg 2, ablation: add pass only)
         uint4* T4 = reinterpret_cast<uint4*>(S.table) + wid * (TableGeom<LEAN>::kSlots / 4);
         for (uint32_t i = lane; i < (uint32_t)TableGeom<LEAN>::kSlots / 4; i += 64) T4[i] = make_uint4(0, 0, 0, 0);
         grp_sync<W>();
