@@ -1582,6 +1582,10 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
             atomicAdd(&sl->fast, 1ull);
             atomicAdd(&sl->survivors, (unsigned long long)spilled);
         }
+#ifdef NGS_PHASE_STAMPS
+        if (lane == 0)
+            for (int i = 0; i < 16; ++i) atomicAdd(&g_phase[16 + i], wacc_[i]);
+#endif
         return;
     }
     if (surv_n) wave_emit(S, X, P, m, L, sc_long, sc_short, surv_n, cand_n, tau);
