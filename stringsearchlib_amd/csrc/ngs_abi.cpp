@@ -198,6 +198,14 @@ bool upload(Library& L) {
     X.n_terms = H.n_terms;
     X.n_short = H.n_short;
     X.n_keys = H.n_keys;
+    {
+        std::vector<uint8_t> seen(H.n_keys, 0);
+        X.keys_unique = 1;
+        for (const uint2& kw : H.tk) {
+            if (seen[kw.x]) { X.keys_unique = 0; break; }
+            seen[kw.x] = 1;
+        }
+    }
     std::vector<uint8_t> kb(H.key_bytes.begin(), H.key_bytes.end());
     uint64_t *gram_off, *term_off, *key_off;
     uint32_t *post, *tk_off, *wild_key, *gram_row, *skip;

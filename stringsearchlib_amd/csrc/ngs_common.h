@@ -171,7 +171,9 @@ struct DevIndex {  // passed by value to kernels; all pointers are device pointe
     const uint8_t* key_bytes;
     const uint32_t* wild_key;   // wildcard answer, pre-sorted (hpp:356-369)
     const float* wild_score;
-    uint32_t n_terms, n_short, n_keys, pad;
+    uint32_t n_terms, n_short, n_keys;
+    uint32_t keys_unique;       // 1: every key has one (term, key) pair, so a query's records never
+                                // share a key and the top-L needs no key dedup pass
     // gram size and character width (indexG / indexW extensions; 3 and 1 for indexN)
     uint32_t gsz, csize, gram_mode;         // gram_mode 1: grams via the dictionary below
     uint32_t short_query_len, full_scan_len; // 3g and g (nGramSearch.hpp:381, :247)

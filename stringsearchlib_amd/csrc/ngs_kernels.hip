@@ -835,17 +835,18 @@ __device__ __forceinline__ uint32_t wave_incl_max_scan(uint32_t v) {
 }
 
 // Wave-local running top-L over the candidate buffer (same algorithm as flush()).
+// unique: no two records share a key (DevIndex.keys_unique): only the second pass runs.
 template <class SM>
-__device__ void wave_flush(SM& S, uint32_t& cand_n, uint64_t& tau, uint32_t L) {
+__device__ void wave_flush(SM& S, uint32_t& cand_n, uint64_t& tau, uint32_t L, bool unique = false) {
     const uint32_t lane = lane_id();
     const uint32_t n = min(cand_n, (uint32_t)kWaveCand);
     const uint32_t P2 = next_pow2(max(n, 2u));
     for (uint32_t i = lane; i < P2; i += 64) {
         const uint64_t r = i < n ? S.cand()[i] : kNoCand;
-        S.cand()[i] = i < n ? ((r << 32) | (r >> 32)) : kNoCand;  // key-major for the dedup
+        S.cand()[i] = i < n ? (unique ? r : ((r << 32) | (r >> 32))) : kNoCand;  // key-major for the dedup
     }
     wave_sync();
-    for (int pass = 0; pass < 2; ++pass) {
+    for (int pass = unique ? 1 : 0; pass < 2; ++pass) {
         for (uint32_t k = 2; k <= P2; k <<= 1) {
             for (uint32_t j = k >> 1; j > 0; j >>= 1) {
                 for (uint32_t p = lane; p < P2 / 2; p += 64) {
@@ -910,7 +911,7 @@ __device__ void wave_emit(SM& S, const DevIndex& X, const SearchParams& P, uint3
                 const uint32_t enc = pair_enc(kw, s, promo, X, S.q, 4u, m, P.valid);
                 rec = ((uint64_t)(~enc) << 32) | kw.x;
             }
-            if (cand_n + 64 > (uint32_t)kWaveCand) wave_flush(S, cand_n, tau, L);
+            if (cand_n + 64 > (uint32_t)kWaveCand) wave_flush(S, cand_n, tau, L, X.keys_unique != 0);
             const bool want = rec < tau;
             const unsigned long long b = __ballot(want);
             if (want) S.cand()[cand_n + rank_below(b)] = rec;
@@ -1590,7 +1591,7 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
     }
     if (surv_n) wave_emit(S, X, P, m, L, sc_long, sc_short, surv_n, cand_n, tau);
     WSTAMP(8);
-    wave_flush(S, cand_n, tau, L);
+    wave_flush(S, cand_n, tau, L, X.keys_unique != 0);
     WSTAMP(9);
     for (uint32_t i = lane; i < cand_n; i += 64) {
         const uint64_t r = S.cand()[i];
@@ -1731,14 +1732,14 @@ __device__ __forceinline__ void emit_query(EmitSmem& S, const uint32_t q, const 
                 const uint32_t enc = pair_enc(kw, s, promo, X, S.q, 4u, m, P.valid);
                 rec = ((uint64_t)(~enc) << 32) | kw.x;
             }
-            if (cand_n + 64 > (uint32_t)kWaveCand) wave_flush(S, cand_n, tau, L);
+            if (cand_n + 64 > (uint32_t)kWaveCand) wave_flush(S, cand_n, tau, L, X.keys_unique != 0);
             const bool want = rec < tau;
             const unsigned long long bw = __ballot(want);
             if (want) S.cand()[cand_n + rank_below(bw)] = rec;
             cand_n += __popcll(bw);
         }
     }
-    wave_flush(S, cand_n, tau, L);
+    wave_flush(S, cand_n, tau, L, X.keys_unique != 0);
     const size_t ob = (size_t)q * P.out_stride;
     for (uint32_t i = lane; i < cand_n; i += 64) {
         const uint64_t r = S.cand()[i];
