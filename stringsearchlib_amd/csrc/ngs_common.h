@@ -83,8 +83,12 @@ constexpr int kSketchCellBits = 4;              // sketch counters: u4, 8 per ta
 constexpr uint32_t kSketchMax = (1u << kSketchCellBits) - 1u;
 constexpr int kSketchCap = NGS_SKETCH_CAP;      // entries per sketch part (<= 1/8 of the cells)
 static_assert(kSketchCap * 8 <= kWaveSlots * (32 / kSketchCellBits), "sketch load");
-constexpr int kWaveCand = 256;                  // candidate buffer per query
-constexpr uint32_t kWaveMaxLimit = kWaveCand / 2;
+#ifndef NGS_WAVE_CAND
+#define NGS_WAVE_CAND 256
+#endif
+constexpr int kWaveCand = NGS_WAVE_CAND;        // candidate buffer per query
+constexpr uint32_t kWaveMaxLimit = 128;         // tier 1 limits (<= kWaveCand / 2)
+static_assert(kWaveMaxLimit * 2 <= (uint32_t)kWaveCand, "a flush keeps at most half the buffer");
 constexpr int kWaveChunks = kSketchCap / 4;     // 16-byte chunks per part and wave (sketch parts)
 constexpr int kExactChunks = (kWaveCap < kSketchCap ? kWaveCap : kSketchCap) / 4;  // ... parts counted exactly (cmin <= 2)
 constexpr int kDmaRounds = kWaveChunks / 64;    // dwordx4 loads per lane for one part
