@@ -103,9 +103,10 @@ constexpr int kLeanWavesPerSimd = NGS_LEAN_WPS; // tier 1a: 6 -> <= 80 VGPRs (LD
 #ifndef NGS_LEAN_CAND_IN_TABLE
 #define NGS_LEAN_CAND_IN_TABLE 1
 #endif
-// tier 1a keeps its candidate buffer over the sketch table (no calcScore until the part loop
-// ends; a query with more survivors than the survivor list holds goes to tier 1b), or in its
-// own 2 KB (calcScore mid-loop like tier 1b, 8 KB of LDS)
+// Only without kDeferEmit (NGS_DEFER_EMIT=0, tier 1a scoring its own survivors): tier 1a keeps
+// its candidate buffer over the sketch table (no calcScore until the part loop ends; a query
+// with more survivors than the survivor list holds goes to tier 1b), or in its own 2 KB
+// (calcScore mid-loop like tier 1b, 8 KB of LDS)
 constexpr bool kLeanCandInTable = NGS_LEAN_CAND_IN_TABLE != 0;
 #ifndef NGS_DEFER_EMIT
 #define NGS_DEFER_EMIT 1
