@@ -175,8 +175,8 @@ def pmc_traffic(cfg_name: str):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--rows", type=int, default=None, help="override corpus rows (debug only)")
     ap.add_argument("--batch", type=int, default=None, help="override per-GPU batch (debug only)")
@@ -279,7 +279,8 @@ def main():
         "detail": {"prep_ms": round(sum(k[1] for k in ktimes) / len(ktimes), 4),
                    "general_ms": round(sum(k[2] for k in ktimes) / len(ktimes), 4),
                    "general_queries": int(st.general_queries), "results_per_query": round(st.results / B, 2),
-                   "survivors_per_query": round(st.survivors / B, 2), "index_build_s": round(index_s, 1)},
+                   "survivors_per_query": round(st.survivors / B, 2), "index_build_s": round(index_s, 1),
+                   "library": L.ngsVersion().decode()},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(corpus, cfg, raw, offs)

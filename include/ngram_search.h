@@ -136,8 +136,9 @@ NGS_API uint32_t ngsGramSize(uint32_t handle);
  * dQueryBytes[dQueryOffsets[i] .. dQueryOffsets[i+1]) (no NUL needed; for an indexW handle
  * the bytes are UTF-32 characters and the offsets multiples of 4). Writes, for query i,
  * dCounts[i] results to dKeys/dScores[i*outStride ...]; outStride must be >=
- * min(limit ? limit : 2^31-1, ngsNumKeys). `stream` is a hipStream_t (NULL = the handle's
- * own stream); the call returns when the results are complete on that stream.
+ * min(limit ? limit : 2^31-1, ngsNumKeys). `stream` is the caller's hipStream_t (NULL = the
+ * null stream): the call's kernels are ordered after the work already queued on it, and the
+ * call returns when the results are complete.
  * Returns 0, or a negative error (-1 bad handle, -2 un-built index, -3 bad argument,
  * -4 HIP failure, -5 internal error flagged by a kernel, e.g. an exhausted LDS table). */
 NGS_API int ngsSearchDevice(uint32_t handle, const uint8_t* dQueryBytes, const uint64_t* dQueryOffsets,
@@ -158,6 +159,8 @@ typedef struct {
     double general_ms;         /* general path time (all its kernels) */
     uint64_t handover_queries; /* queries the lean tier-1a kernel handed to the full tier-1b kernel */
     uint64_t tier2_queries;    /* queries routed to the block-per-query tier-2 kernel */
+    uint64_t heavy_queries;    /* listed by the prep kernel as heavy (cmin 2: lean kernel on a side stream) */
+    uint64_t full_queries;     /* listed by the prep kernel for tier 1b from the start (cmin 1, short search) */
 } ngs_stats;
 NGS_API int ngsSetTiming(uint32_t handle, int enable);
 NGS_API int ngsLastStats(uint32_t handle, ngs_stats* out);
@@ -168,7 +171,8 @@ NGS_API int ngsLastStats(uint32_t handle, ngs_stats* out);
  * span. Returns 8, -1 (bad handle), -3 (dictionary index), -4 (HIP error). */
 NGS_API int ngsIndexDigest(uint32_t handle, uint64_t* out, int n);
 
-/* Library build identification (e.g. "gfx950 ngram_search 0.1"). */
+/* Library build identification: "ngram_search <version> gfx950 src=<hash>", where <hash> is the
+ * first 16 hex digits of the SHA-256 of the sources the library was compiled from. */
 NGS_API const char* ngsVersion(void);
 
 /* Diagnostics: per-phase time of the LDS kernels (s_memtime shader-clock ticks, summed over

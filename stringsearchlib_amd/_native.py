@@ -7,6 +7,8 @@ missing or no GPU is usable the calls fail loudly.
 from __future__ import annotations
 
 import ctypes as C
+import glob
+import hashlib
 import os
 import re
 import subprocess
@@ -27,7 +29,8 @@ class NgsStats(C.Structure):
     _fields_ = [("queries", C.c_uint64), ("fast_queries", C.c_uint64), ("general_queries", C.c_uint64),
                 ("postings", C.c_uint64), ("lists", C.c_uint64), ("results", C.c_uint64), ("survivors", C.c_uint64),
                 ("fast_kernel_ms", C.c_double), ("prep_kernel_ms", C.c_double), ("general_ms", C.c_double),
-                ("handover_queries", C.c_uint64), ("tier2_queries", C.c_uint64)]
+                ("handover_queries", C.c_uint64), ("tier2_queries", C.c_uint64),
+                ("heavy_queries", C.c_uint64), ("full_queries", C.c_uint64)]
 
 
 def build(jobs: int = 4) -> None:
@@ -37,6 +40,18 @@ def build(jobs: int = 4) -> None:
 
 _lib = None
 _synth = None
+
+
+def source_hash() -> str:
+    """The stamp the Makefile bakes into ngsVersion(): SHA-256 (16 hex digits) of the library's
+    sources (csrc/*.h, *.hip, *.cpp in byte order, then include/ngram_search.h)."""
+    files = sorted(glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(CSRC, "*.hip")) +
+                   glob.glob(os.path.join(CSRC, "*.cpp"))) + [HEADER]
+    h = hashlib.sha256()
+    for f in files:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
 
 
 def lib():
@@ -120,6 +135,11 @@ def lib():
     L.ngsVersion.argtypes = []
     L.ngsPhaseStats.restype = C.c_int
     L.ngsPhaseStats.argtypes = [C.POINTER(C.c_uint64), C.c_int, C.c_int]
+    version = L.ngsVersion().decode()
+    want = source_hash()
+    if not version.endswith(f"src={want}"):
+        raise RuntimeError(f"{LIB_PATH} ({version!r}) was not built from this tree's sources (src={want}): "
+                           f"rebuild it with `make -C {CSRC}`")
     _lib = L
     return L
 

@@ -431,6 +431,9 @@ int device_search(Library& L, Context& c, const uint8_t* d_raw, const uint64_t* 
                 return -4;
         }
         if (timing) HIP_CHECK(hipEventRecord(c.ev[5], s));
+        // the last group's k_gen_write still reads c.gen: complete before the context goes back
+        // to the pool (and before the call returns, as the ABI promises)
+        if (!HIP_CHECK(hipStreamSynchronize(s))) return -4;
     }
     DevStats ds{};
     for (uint32_t i = 0; i < kStatSlots; ++i) {
@@ -453,6 +456,8 @@ int device_search(Library& L, Context& c, const uint8_t* d_raw, const uint64_t* 
         st.tier2_queries = counts3[1];
         // queries tier 1b ran: hand-overs of both lean launches and the full list
         st.handover_queries = counts3[2] + counts3[4] + counts3[5];
+        st.heavy_queries = counts3[3];
+        st.full_queries = counts3[5];
         st.postings = ds.postings;
         st.lists = ds.lists;
         st.results = ds.results;
@@ -587,10 +592,6 @@ uint32_t batch_query(uint32_t handle, const CharT* const* queries, uint32_t nq, 
 }  // namespace ngs
 
 using namespace ngs;
-
-extern "C" {
-
-}  // extern "C"
 
 namespace ngs {
 namespace {
@@ -790,7 +791,6 @@ NGS_API int ngsSearchDevice(uint32_t handle, const uint8_t* dQueryBytes, const u
     }
     std::unique_ptr<Context> c = L->acquire();
     if (!c) return -4;
-    if (!s) s = c->stream;
     uint64_t qbytes = 0;
     int rc = 0;
     if (nQueries &&
@@ -820,7 +820,10 @@ NGS_API int ngsLastStats(uint32_t handle, ngs_stats* out) {
     return 0;
 }
 
-NGS_API const char* ngsVersion(void) { return "ngram_search 0.1 gfx950"; }
+#ifndef NGS_SRC_HASH
+#define NGS_SRC_HASH "unknown"
+#endif
+NGS_API const char* ngsVersion(void) { return "ngram_search 0.2 gfx950 src=" NGS_SRC_HASH; }
 
 NGS_API int ngsIndexDigest(uint32_t handle, uint64_t* out, int n) {
     std::shared_lock<std::shared_mutex> lk(g_lock);
