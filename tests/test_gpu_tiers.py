@@ -88,15 +88,17 @@ def test_tier2_by_gram_count(bench20k, thr):
 
 
 def test_tier2_gram_count_edges(bench20k):
-    """65 bytes (63 grams) stays in tier 1; 66 and 257 go to tier 2; 258 goes to the general path."""
+    """65 bytes (63 grams) stays in tier 1; 66 and 257 go to tier 2 and finish there; 258 is
+    listed for tier 2 by tier 1 (> 63 grams) and passed on by k_fast to the general path."""
     words, gi, oi = bench20k
     rng = random.Random(7)
-    for length, tier2, general in [(65, 0, 0), (66, 1, 0), (257, 1, 0), (258, 0, 1)]:
+    for length, tier2, general in [(65, 0, 0), (66, 1, 0), (257, 1, 0), (258, 1, 1)]:
         qs = _long_queries(rng, words, 3, lo=length, hi=length)
         assert all(len(q) == length for q in qs)
         st = _check(gi, oi, qs, 0.3, 100, f"edge-{length}")
         assert st["tier2_queries"] == tier2 * len(qs), (length, st)
         assert st["general_queries"] == general * len(qs), (length, st)
+        assert st["fast_queries"] == (1 - general) * len(qs), (length, st)
 
 
 @pytest.mark.parametrize("limit", [129, 500, 1024])
@@ -124,9 +126,9 @@ def test_tier2_other_corpora(kind, thr, limit):
     if kind == "short":
         qs += [w[:rng.randint(4, 8)] for w in rng.sample([w for w in live if len(w) >= 4], 8)]
     st = _check(gi, oi, qs, thr, limit, f"{kind}")
+    assert st["fast_queries"] + st["general_queries"] == len(qs), st
     if limit > 128:
-        assert st["tier2_queries"] + st["general_queries"] == len(qs), st
-        assert st["tier2_queries"] >= len(qs) - 8, st  # (the short scan over every term goes general)
+        assert st["tier2_queries"] == len(qs) and st["general_queries"] == 0, st
     else:
         assert st["tier2_queries"] >= 8, st  # the long queries
     gi.dispose()
