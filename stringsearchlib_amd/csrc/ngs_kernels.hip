@@ -744,6 +744,7 @@ struct alignas(16) WaveSmem {
     }
     uint2 segtab[W][64];             // staging, per wave: per list {first chunk - position, first | end entry << 16}
     uint8_t mark[W][kWaveChunks];    // staging, per wave: list index + 1 at the (wave-local) position of its first chunk
+    unsigned long long lstart[kDmaRounds];  // tier 1a staging: bit (pre - 1) per list start, 64 chunk positions a word
     uint32_t surv_t[kWaveSurv];      // survivor terms
     uint32_t cbuf[64];               // sketch candidates (terms)
     uint8_t surv_c[kWaveSurv];       // hit count, | 0x80 for a Levenshtein (short search) match count
@@ -960,9 +961,12 @@ __device__ __forceinline__ uint32_t wave_insert_slot(uint32_t* T, uint32_t rel, 
 
 // sketch cell of a term: full-rate shift/xor (v_mul_lo_u32 is quarter rate). Term ids of a part
 // are spread over a range much wider than the table, and consecutive ids get distinct cells.
+// Tier 1a (NGS_LEAN_CELL_XOR=0) takes the low bits alone: its parts are contiguous term-id ranges
+// whose few hundred entries are spread over an id span far wider than the table.
 template <int W, bool LEAN>
 __device__ __forceinline__ uint32_t sketch_cell(uint32_t t) {  // u4 counter index: 8 per table word
     constexpr uint32_t kBits = TableGeom<LEAN>::kBits + 3 + (W == 4 ? 2 : W == 2 ? 1 : 0);
+    if constexpr (LEAN && !NGS_LEAN_CELL_XOR) return t & ((1u << kBits) - 1u);
     return (t ^ (t >> kBits)) & ((1u << kBits) - 1u);
 }
 
@@ -1133,8 +1137,8 @@ __device__ __forceinline__ void part_exact(WaveSmem<W, LEAN>& S, uint4 (&v)[kDma
 // other. Returns the number of candidate entries; above 64 the caller counts the part exactly
 // (the table is clean again). (u16 counters with no-return adds were measured: the 4x fewer
 // cells per KB cost more in false candidates than the returns cost in waits.)
-template <int W, bool LEAN>
-__device__ __forceinline__ uint32_t part_sketch(WaveSmem<W, LEAN>& S, const uint4 (&v)[kDmaRounds], uint32_t vmask,
+template <int W, bool LEAN, int NR = kDmaRounds>
+__device__ __forceinline__ uint32_t part_sketch(WaveSmem<W, LEAN>& S, const uint4 (&v)[NR], uint32_t vmask,
                                                 uint32_t mt, uint32_t cmin, uint32_t n_short, uint32_t n_terms,
                                                 uint32_t& surv_n, uint32_t dbg) {
     const uint32_t lane = lane_id(), wid = W == 1 ? 0u : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1143,7 +1147,7 @@ __device__ __forceinline__ uint32_t part_sketch(WaveSmem<W, LEAN>& S, const uint
     // at >= cmin had exactly one such add in this part: the table starts clear and adds are 0/1)
     bool ovf = false, hot = false;
 #pragma unroll
-    for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) {
+    for (uint32_t r = 0; r < (uint32_t)NR; ++r) {
         if (64 * r < mt) {
             const uint32_t t[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
             // (issuing the four returning adds together, one wait, was measured no faster: the
@@ -1172,7 +1176,7 @@ __device__ __forceinline__ uint32_t part_sketch(WaveSmem<W, LEAN>& S, const uint
     // at offsets from one prefix sum instead of compacting every entry slot by ballot
     uint32_t cm = 0;
 #pragma unroll
-    for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) {
+    for (uint32_t r = 0; r < (uint32_t)NR; ++r) {
         if (64 * r < mt) {
             const uint32_t t[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
             uint32_t w[4];
@@ -1204,7 +1208,7 @@ __device__ __forceinline__ uint32_t part_sketch(WaveSmem<W, LEAN>& S, const uint
             bits &= bits - 1u;
             uint32_t t = 0;
 #pragma unroll
-            for (uint32_t j = 0; j < 4 * (uint32_t)kDmaRounds; ++j) {
+            for (uint32_t j = 0; j < 4 * (uint32_t)NR; ++j) {
                 const uint32_t x = (j & 3) == 0 ? v[j >> 2].x : (j & 3) == 1 ? v[j >> 2].y : (j & 3) == 2 ? v[j >> 2].z : v[j >> 2].w;
                 t = j == k ? x : t;
             }
@@ -1615,6 +1619,311 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
 #endif
 }
 
+// Tier 1a's staging of one part into registers (W = 1). Lane g < ng brings entries [cur, cur + len)
+// of its list: nch 16-byte chunks from position pre = incl - nch of the part's packed chunk
+// numbering on (incl: the planner's inclusive prefix sum, mt chunks in all). Lane l loads chunks
+// l, 64 + l, ... . A chunk finds its list by counting the list starts below it: every non-empty
+// list but the first sets bit (pre - 1) of a 192-bit map, so the ordinal of chunk c's list is the
+// map's bits below lane l in word c / 64 (v_mbcnt_lo/hi) plus those of the earlier words; the
+// non-empty lists' {first chunk - pre, entry bounds} sit in segtab by ordinal. (stage_part, the
+// full kernel's staging, spends a marker array and a max-scan per round on the same lookup.)
+__device__ __forceinline__ void lean_stage(WaveSmem<1, true>& S, const uint4* __restrict__ post4, uint64_t gbase,
+                                           uint32_t a0, uint32_t cur, uint32_t len, uint32_t nch, uint32_t incl,
+                                           uint32_t mt, uint4 (&v)[kDmaRounds], uint32_t& vmask) {
+    const uint32_t lane = lane_id();
+    const uint32_t head = (a0 + cur) & 3u;
+    const uint32_t pre = incl - nch;
+    const uint32_t ord = rank_below(__ballot(nch != 0));
+    mt = __builtin_amdgcn_readfirstlane(mt);
+    if (lane < (uint32_t)kDmaRounds) S.lstart[lane] = 0;
+    wave_sync();
+    if (nch) {
+        if (pre) atomicOr(&S.lstart[(pre - 1) >> 6], 1ull << ((pre - 1) & 63u));
+        const uint32_t first = (uint32_t)((gbase + cur) >> 2);
+        S.segtab[0][ord] = make_uint2(first - pre, (4 * pre + head) | ((4 * pre + head + len) << 16));
+    }
+    wave_sync();
+    uint32_t below = 0;  // list starts in the earlier words
+    vmask = 0;
+#pragma unroll
+    for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) {
+        if (64 * r < mt) {
+            const unsigned long long wd = S.lstart[r];
+            const uint32_t wlo = __builtin_amdgcn_readfirstlane((uint32_t)wd);
+            const uint32_t whi = __builtin_amdgcn_readfirstlane((uint32_t)(wd >> 32));
+            const uint32_t idx = __builtin_amdgcn_mbcnt_hi(whi, __builtin_amdgcn_mbcnt_lo(wlo, below));
+            below += (uint32_t)__popc(wlo) + (uint32_t)__popc(whi);
+            const uint32_t c = 64 * r + lane;
+            const bool ok = c < mt;
+            const uint2 seg = S.segtab[0][idx & 63u];
+            if (ok) v[r] = post4[seg.x + c];  // inactive lanes load nothing
+            // entries [lo_e, hi_e) of this chunk are in the list segment [y, z)
+            const int y = (int)(seg.y & 0xFFFFu), z = (int)(seg.y >> 16);
+            const uint32_t lo_e = (uint32_t)min(max(y - (int)(4 * c), 0), 4);
+            const uint32_t hi_e = (uint32_t)min(max(z - (int)(4 * c), 0), 4);
+            const uint32_t bits = ((1u << hi_e) - 1u) & ~((1u << lo_e) - 1u);
+            vmask |= (ok ? bits : 0u) << (4 * r);
+        }
+    }
+}
+
+// Tier 1a (LEAN, DEFER): one wave per query, sketch counting only, survivors spilled to HBM for
+// k_emit. The full kernel's part loop (bucket groups, term-id sub-parts, loads one part ahead)
+// with its own staging (lean_stage) and the sketch counter part_sketch; a query that needs exact
+// counting, a short search or more than kEmitCap survivor slots is handed to tier 1b untouched.
+__device__ __forceinline__ void lean_query(WaveSmem<1, true>& S, const uint32_t q, const DevIndex& X,
+                                           const SearchParams& P, const uint8_t* __restrict__ qnorm,
+                                           const uint64_t* __restrict__ qoff, const uint32_t* __restrict__ qm,
+                                           uint32_t* __restrict__ out_n, uint32_t* __restrict__ out_k,
+                                           float* __restrict__ out_s, uint32_t* __restrict__ list2,
+                                           uint32_t* __restrict__ count2, DevStats* __restrict__ stats,
+                                           uint32_t* __restrict__ fb, uint32_t* __restrict__ fbc) {
+    const uint32_t lane = lane_id();
+    auto bail = [&]() {  // hand the query to tier 1b (nothing of it was written yet)
+        if (lane == 0) fb[atomicAdd(fbc, 1u)] = q;
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    };
+    const uint32_t m = qm[q];
+    const uint32_t L = P.limit;
+    if (m == kQueryWildcard) {  // nGramSearch.hpp:356-369, answer precomputed at index time
+        const uint32_t nk = min(L, X.n_keys);
+        const size_t ob = (size_t)q * P.out_stride;
+        for (uint32_t i = lane; i < nk; i += 64) {
+            out_k[ob + i] = X.wild_key[i];
+            out_s[ob + i] = X.wild_score[i];
+        }
+        if (lane == 0) out_n[q] = nk;
+        return;
+    }
+    if (m == 0) {  // nothing left after normalisation, nGramSearch.hpp:374-375
+        if (lane == 0) out_n[q] = 0;
+        return;
+    }
+    if (m <= X.full_scan_len || m - X.gsz + 1 > kWaveMaxGrams || L > kWaveMaxLimit) {
+        if (lane == 0) list2[atomicAdd(count2, 1u)] = q;  // tier 2 / library-wide path
+        return;
+    }
+    const uint32_t n = m - X.gsz + 1;  // grams of the query (hpp:29-36)
+    const uint32_t n_long = X.n_terms - X.n_short;
+#ifdef NGS_PHASE_STAMPS
+    unsigned long long wt_ = __builtin_amdgcn_s_memtime();
+    unsigned long long wacc_[16] = {};
+#endif
+    // lane c holds the fp32 score of c hits, (float)c / n (hpp:300); the smallest passing count
+    const float sc_long = lane <= n ? (float)lane / (float)n : 0.0f;
+    const unsigned long long pm = __ballot(lane <= n && lane > 0 && !(sc_long < P.thr));
+    const uint32_t cmin = pm ? (uint32_t)(__ffsll((long long)pm) - 1) : 1000u;
+    // heavy_class() lists these for launches of their own (same test, same cmin)
+    if (!P.lean_all && (cmin <= kHeavyCmin || (m < X.short_query_len && X.n_short))) return;
+    if (m < X.short_query_len && X.n_short) { bail(); return; }  // short search: tier 1b
+    const uint8_t* qg = qnorm + qoff[q];
+    for (uint32_t i = lane; i < m; i += 64) S.q[i] = char_at(qg, i, X.csize);
+    {
+        uint4* T4 = reinterpret_cast<uint4*>(S.table);
+        for (uint32_t i = lane; i < (uint32_t)kWaveSlots / 4; i += 64) T4[i] = make_uint4(0, 0, 0, 0);
+    }
+    wave_sync();
+    // ---- searchLong (nGramSearch.hpp:278-301): lanes 0..ng-1 own the gram occurrences with
+    // postings (a gram repeated k times owns k lanes: counts with multiplicity) ----
+    uint64_t gbase = 0;
+    uint32_t glen = 0, grow = 0;
+    bool have = false;
+    if (lane < n) {
+        const uint32_t code = gram_at(X, [&](uint32_t i) { return S.q[i]; }, lane);
+        if (code != UINT32_MAX) {
+            gbase = X.gram_off[code];
+            glen = (uint32_t)(X.gram_off[code + 1] - gbase);
+            grow = X.gram_row[code];
+            have = glen != 0;
+        }
+    }
+    const unsigned long long hb = __ballot(have);
+    const uint32_t ng = __popcll(hb);
+    {
+        uint32_t src = 0;
+        unsigned long long rest = hb;
+        for (uint32_t k = 0; k <= lane && rest; ++k) {  // lane k takes the k-th set bit
+            src = __ffsll((long long)rest) - 1;
+            rest &= rest - 1;
+        }
+        const uint64_t b2 = __shfl(gbase, (int)src);
+        const uint32_t l2 = __shfl(glen, (int)src), r2 = __shfl(grow, (int)src);
+        gbase = lane < ng ? b2 : 0;
+        glen = lane < ng ? l2 : 0;
+        grow = lane < ng ? r2 : 0;
+    }
+    const uint64_t p_total = wave_sum((uint64_t)glen);
+    WSTAMP(0);
+    const bool sketch = cmin >= kSketchMinCmin && cmin <= kSketchMax;
+    if (p_total && cmin <= n && !sketch) { bail(); return; }  // exact counting: tier 1b
+    uint32_t surv_n = 0, spilled = 0;
+    // the LDS survivor list to this query's kEmitCap slots in HBM; false if they are full
+    auto spill = [&]() -> bool {
+        if (spilled + surv_n > kEmitCap) return false;
+        uint32_t* et = P.est + (size_t)q * kEmitCap + spilled;
+        uint8_t* ec = P.esc + (size_t)q * kEmitCap + spilled;
+        for (uint32_t i = lane; i < surv_n; i += 64) {
+            et[i] = S.surv_t[i];
+            ec[i] = S.surv_c[i];
+        }
+        spilled += surv_n;
+        surv_n = 0;
+        return true;
+    };
+    if (p_total && cmin <= n) {
+        // cmin 2: every colliding pair is a false candidate, so those parts are cut at half the size
+        const uint32_t shrink = cmin == 2 ? kLeanShrink2 : 0u;
+        const uint32_t kChunks = (uint32_t)kWaveChunks >> shrink;  // part cap in 16-byte chunks
+        const uint32_t K = X.n_buckets, span = X.bucket_span;
+        const uint32_t wmax = (uint32_t)max64(1, min64(K, kMaxPartSpan / max(span, 1u)));
+        const uint32_t w = (uint32_t)max64(1, min64(wmax, (uint64_t)K * (kSketchTarget >> shrink) / p_total));
+        const uint32_t* sk = X.skip + (size_t)grow * (K + 1);
+        const uint4* post4 = reinterpret_cast<const uint4*>(X.post);
+        const uint32_t a0 = (uint32_t)gbase & 3u;  // list start within its 16-byte chunk
+        // entries [s, e) of this lane's list cover 16-byte chunks [(a0 + s) / 4, (a0 + e + 3) / 4)
+        auto chunks = [a0](uint32_t s, uint32_t e) -> uint32_t { return e > s ? ((a0 + e + 3) >> 2) - ((a0 + s) >> 2) : 0u; };
+        // end of the next bucket group: skip[row][min(K, bn + w)]; idle lanes load nothing
+        auto next_end = [&](uint32_t bn) -> uint32_t { return sk[min(K, bn + w)]; };
+        uint32_t cur = 0, bnext = 0;
+        uint32_t e_pre = lane < ng ? next_end(0) : 0u;
+        uint32_t in_sub = 0, sub_lo = 0, hi_lim = 0, sub_end = 0, sub_bnext = 0, step = 1;
+        // software pipeline in registers: part i+1's loads are in flight while part i is counted
+        uint4 pv[kDmaRounds];
+        uint32_t p_vm = 0, p_mt = 0;
+        bool have_p = false;
+#pragma unroll
+        for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) pv[r] = make_uint4(0, 0, 0, 0);
+        unsigned* err = &stats->errors;
+        WSTAMP(1);
+        for (uint32_t guard = 0;;) {
+            uint4 cv[kDmaRounds];
+#pragma unroll
+            for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) cv[r] = pv[r];
+            const uint32_t c_vm = p_vm, c_mt = p_mt;
+            const bool have_c = have_p;
+            // ---- next part: per list lane the segment [cur, cur + len) ----
+            uint32_t len = 0, nch = 0, incl = 0, tot = 0;  // the part's per-list chunks, their prefix sum, total
+            have_p = false;
+            in_sub = __builtin_amdgcn_readfirstlane(in_sub);
+            bnext = __builtin_amdgcn_readfirstlane(bnext);
+            bool fast = false;
+            if (!in_sub && bnext < K) {  // common case, straight-line: the next bucket group fits
+                const uint32_t e = lane < ng ? e_pre : cur;
+                nch = chunks(cur, e);
+                incl = wave_incl_scan(nch);
+                tot = __builtin_amdgcn_readlane(incl, 63);
+                if (tot && tot <= kChunks) {
+                    len = e - cur;
+                    bnext = min(K, bnext + w);
+                    if (lane < ng) e_pre = next_end(bnext);
+                    have_p = true;
+                    fast = true;
+                }
+            }
+            WSTAMP(2);
+            for (; !fast;) {
+                WCOUNT(12, 1);
+                guard = __builtin_amdgcn_readfirstlane(guard);
+                bnext = __builtin_amdgcn_readfirstlane(bnext);
+                sub_lo = __builtin_amdgcn_readfirstlane(sub_lo);
+                step = __builtin_amdgcn_readfirstlane(step);
+                if (++guard > 8u * K + 4096u) {
+                    atomicOr(err, 4u);  // every lane (idempotent)
+                    break;
+                }
+                if (!in_sub) {
+                    if (bnext >= K) break;
+                    const uint32_t bhi = min(K, bnext + w), e = lane < ng ? e_pre : cur;
+                    nch = chunks(cur, e);
+                    incl = wave_incl_scan(nch);
+                    tot = __builtin_amdgcn_readlane(incl, 63);
+                    if (tot <= kChunks) {
+                        len = e - cur;
+                        bnext = bhi;
+                        if (lane < ng) e_pre = next_end(bnext);
+                        if (tot) { have_p = true; break; }
+                        continue;
+                    }
+                    in_sub = 1;  // the group is over the cap: term-id sub-ranges of it
+                    sub_lo = bnext * span;
+                    hi_lim = (uint32_t)min64((uint64_t)bhi * span, n_long);
+                    sub_end = e;
+                    sub_bnext = bhi;
+                    step = (uint32_t)max64(1, min64((uint64_t)(hi_lim - sub_lo) * (kChunks * 3 / 4) / max(tot, 1u),
+                                                    kMaxPartSpan));
+                }
+                const uint32_t hi = (uint32_t)min64(hi_lim, (uint64_t)sub_lo + step);
+                // lower_bound(list, hi) per lane, as a ballot-controlled (uniform) loop
+                uint32_t a = cur, b = lane < ng ? sub_end : cur;
+                while (__ballot(a < b)) {
+                    const bool act = a < b;
+                    const uint32_t mid = (a + b) >> 1;
+                    uint32_t pvv = 0;
+                    if (act) pvv = X.post[gbase + mid];
+                    const bool below = pvv < hi;
+                    a = act && below ? mid + 1 : a;
+                    b = act && !below ? mid : b;
+                }
+                nch = lane < ng ? chunks(cur, a) : 0u;
+                incl = wave_incl_scan(nch);
+                const uint32_t t2 = __builtin_amdgcn_readlane(incl, 63);
+                tot = t2;
+                if (t2 > kChunks && hi - sub_lo > 1) {
+                    step = max(1u, (uint32_t)((uint64_t)(hi - sub_lo) * (kChunks * 3 / 4) / t2));
+                    continue;
+                }
+                len = lane < ng ? a - cur : 0u;
+                sub_lo = hi;
+                if (sub_lo >= hi_lim) {
+                    in_sub = 0;
+                    bnext = sub_bnext;
+                    if (lane < ng) e_pre = next_end(bnext);
+                }
+                if (t2) { have_p = true; break; }
+                cur = a;
+            }
+            WSTAMP(3);
+            have_p = __builtin_amdgcn_readfirstlane(have_p ? 1u : 0u) != 0;
+            // ---- part i+1: issue this wave's loads ----
+            if (have_p) {
+                lean_stage(S, post4, gbase, a0, cur, len, nch, incl, tot, pv, p_vm);
+                p_mt = tot;
+                cur += len;
+            }
+            WSTAMP(4);
+            // ---- count part i while part i+1 is in flight ----
+            if (have_c) {
+                if (surv_n + 64 > (uint32_t)kWaveSurv) {
+                    if (!spill()) { bail(); return; }
+                    wave_sync();  // the list is read before it is refilled
+                }
+                const uint32_t nc = part_sketch(S, cv, c_vm, c_mt, cmin, X.n_short, X.n_terms, surv_n, P.dbg);
+                WCOUNT(11, 1);
+                WCOUNT(13, (c_mt + 63) / 64);
+                WCOUNT(14, nc);
+                WCOUNT(15, nc == 0 ? 1 : 0);
+                WSTAMP(5);
+                if (nc > 64) { bail(); return; }  // wrapped counter or too many candidates: tier 1b
+            }
+            if (!have_p) break;
+        }
+    }
+    if (!spill()) { bail(); return; }
+    WSTAMP(6);
+#ifdef NGS_PHASE_STAMPS
+    if (lane == 0)
+        for (int i = 0; i < 16; ++i) atomicAdd(&g_phase[16 + i], wacc_[i]);
+#endif
+    if (lane == 0) P.esn[q] = spilled | (P.lean_all ? kEmitHeavy : 0u);
+    if (lane == 0 && !(P.dbg & 32u)) {
+        DevStats* sl = stats + (q & (kStatSlots - 1));
+        atomicAdd(&sl->postings, (unsigned long long)p_total);
+        atomicAdd(&sl->lists, (unsigned long long)ng);
+        atomicAdd(&sl->fast, 1ull);
+        atomicAdd(&sl->survivors, (unsigned long long)spilled);
+    }
+}
+
 // Tier 1b / experiments: the full wave kernel, over every query (qlist == nullptr) or over the
 // queries tier 1a handed over (qlist[0 .. *qcount), grid-stride).
 template <int W>
@@ -1662,14 +1971,12 @@ __global__ __launch_bounds__(64, kLeanWavesPerSimd) void k_wave_lean(DevIndex X,
                                                                     const uint32_t* __restrict__ qcount) {
     __shared__ WaveSmem<1, true> S;
     if (!qlist) {
-        wave_query<1, true, DEFER>(S, blockIdx.x, X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats,
-                                   fb, fbc);
+        lean_query(S, blockIdx.x, X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats, fb, fbc);
         return;
     }
     const uint32_t cnt = *qcount;  // the heavy list, grid-stride
     for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
-        wave_query<1, true, DEFER>(S, qlist[i], X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats,
-                                   fb, fbc);
+        lean_query(S, qlist[i], X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats, fb, fbc);
         wave_sync();
     }
 }
