@@ -40,6 +40,16 @@ __device__ unsigned long long g_phase[32];
 #define WSTAMP(i)
 #endif
 
+// a global (address space 1) pointer: keeps global_load addressing where a pointer passes through
+// inline asm, which hides the address space the compiler inferred from the kernel argument
+#if defined(__HIP_DEVICE_COMPILE__)
+template <class T>
+using gptr = const T __attribute__((address_space(1)))*;
+#else  // the host pass parses the device code only
+template <class T>
+using gptr = const T*;
+#endif
+
 __device__ __forceinline__ uint64_t min64(uint64_t a, uint64_t b) { return a < b ? a : b; }
 __device__ __forceinline__ uint64_t max64(uint64_t a, uint64_t b) { return a > b ? a : b; }
 __device__ __forceinline__ bool dev_space(unsigned c) { return c == 32u || (c >= 9u && c <= 13u); }
@@ -969,6 +979,24 @@ __device__ __forceinline__ uint32_t sketch_cell(uint32_t t) {  // u4 counter ind
     if constexpr (LEAN && !NGS_LEAN_CELL_XOR) return t & ((1u << kBits) - 1u);
     return (t ^ (t >> kBits)) & ((1u << kBits) - 1u);
 }
+// the table word holding t's cell; tier 1a's low-bit cells address it as the byte offset
+// (t >> 1) & 0xffc, two instructions (the word index form takes three)
+template <int W, bool LEAN>
+__device__ __forceinline__ uint32_t* sketch_word(uint32_t* table, uint32_t t) {
+    constexpr uint32_t kBits = TableGeom<LEAN>::kBits + 3 + (W == 4 ? 2 : W == 2 ? 1 : 0);
+    if constexpr (LEAN && !NGS_LEAN_CELL_XOR)
+        return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(table) + ((t >> 1) & (((1u << kBits) - 1u) >> 1 & ~3u)));
+    return table + (sketch_cell<W, LEAN>(t) >> 3);
+}
+// (sketch_cell(t) & 7) * 4 in the low 5 bits, higher bits arbitrary: v_lshlrev and v_bfe_u32 read
+// only the low 5 bits of a shift / offset, so the mask is never materialised (the tier-1a kernel
+// is VALU-issue bound)
+template <int W, bool LEAN>
+__device__ __forceinline__ uint32_t sketch_sh4(uint32_t t) {
+    constexpr uint32_t kBits = TableGeom<LEAN>::kBits + 3 + (W == 4 ? 2 : W == 2 ? 1 : 0);
+    if constexpr (LEAN && !NGS_LEAN_CELL_XOR) return t << 2;
+    return (t ^ (t >> kBits)) << 2;
+}
 
 // Loads this wave's share of one part into registers. Lane g < ng contributes entries
 // [cur, cur + len) of its list (list base gbase, a0 = gbase % 4); the part's 16-byte chunks are
@@ -1146,6 +1174,7 @@ __device__ __forceinline__ uint32_t part_sketch(WaveSmem<W, LEAN>& S, const uint
     // ovf: a counter wrapped; hot: an add took a cell from cmin - 1 to cmin (every cell that ends
     // at >= cmin had exactly one such add in this part: the table starts clear and adds are 0/1)
     bool ovf = false, hot = false;
+    const uint32_t cm1 = __builtin_amdgcn_readfirstlane(cmin - 1u);
 #pragma unroll
     for (uint32_t r = 0; r < (uint32_t)NR; ++r) {
         if (64 * r < mt) {
@@ -1154,12 +1183,11 @@ __device__ __forceinline__ uint32_t part_sketch(WaveSmem<W, LEAN>& S, const uint
             // other waves of the SIMD already cover the LDS latency)
 #pragma unroll
             for (uint32_t e = 0; e < 4; ++e) {
-                const uint32_t c = sketch_cell<W, LEAN>(t[e]);
-                const uint32_t sh = (c & 7u) << 2;
-                const uint32_t old = atomicAdd(&S.table[c >> 3], ((vmask >> (4 * r + e)) & 1u) << sh);
-                const uint32_t on = (old >> sh) & kSketchMax;
+                const uint32_t sh4 = sketch_sh4<W, LEAN>(t[e]);
+                const uint32_t old = atomicAdd(sketch_word<W, LEAN>(S.table, t[e]), ((vmask >> (4 * r + e)) & 1u) << (sh4 & 31u));
+                const uint32_t on = __builtin_amdgcn_ubfe(old, sh4, 4u);
                 ovf |= on == kSketchMax;
-                if constexpr (kSkipCold && W == 1) hot |= on + 1u == cmin;
+                if constexpr (kSkipCold && W == 1) hot |= on == cm1;
             }
         }
     }
@@ -1181,11 +1209,10 @@ __device__ __forceinline__ uint32_t part_sketch(WaveSmem<W, LEAN>& S, const uint
             const uint32_t t[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
             uint32_t w[4];
 #pragma unroll
-            for (uint32_t e = 0; e < 4; ++e) w[e] = S.table[sketch_cell<W, LEAN>(t[e]) >> 3];
+            for (uint32_t e = 0; e < 4; ++e) w[e] = *sketch_word<W, LEAN>(S.table, t[e]);
 #pragma unroll
             for (uint32_t e = 0; e < 4; ++e) {
-                const uint32_t c = sketch_cell<W, LEAN>(t[e]);
-                cm |= (((w[e] >> ((c & 7u) << 2)) & kSketchMax) >= cmin ? 1u : 0u) << (4 * r + e);
+                cm |= (__builtin_amdgcn_ubfe(w[e], sketch_sh4<W, LEAN>(t[e]), 4u) >= cmin ? 1u : 0u) << (4 * r + e);
             }
         }
     }
@@ -1627,7 +1654,7 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
 // map's bits below lane l in word c / 64 (v_mbcnt_lo/hi) plus those of the earlier words; the
 // non-empty lists' {first chunk - pre, entry bounds} sit in segtab by ordinal. (stage_part, the
 // full kernel's staging, spends a marker array and a max-scan per round on the same lookup.)
-__device__ __forceinline__ void lean_stage(WaveSmem<1, true>& S, const uint4* __restrict__ post4, uint64_t gbase,
+__device__ __forceinline__ void lean_stage(WaveSmem<1, true>& S, gptr<uint4> post4, uint64_t gbase,
                                            uint32_t a0, uint32_t cur, uint32_t len, uint32_t nch, uint32_t incl,
                                            uint32_t mt, uint4 (&v)[kDmaRounds], uint32_t& vmask) {
     const uint32_t lane = lane_id();
@@ -1778,7 +1805,10 @@ __device__ __forceinline__ void lean_query(WaveSmem<1, true>& S, const uint32_t 
         const uint32_t wmax = (uint32_t)max64(1, min64(K, kMaxPartSpan / max(span, 1u)));
         const uint32_t w = (uint32_t)max64(1, min64(wmax, (uint64_t)K * (kSketchTarget >> shrink) / p_total));
         const uint32_t* sk = X.skip + (size_t)grow * (K + 1);
-        const uint4* post4 = reinterpret_cast<const uint4*>(X.post);
+        // an opaque SGPR pair: otherwise the compiler keeps it inside the 8-dword kernarg tuple it
+        // loaded it with and reloads all 8 dwords from VGPR lanes (v_readlane, VALU) every round
+        gptr<uint4> post4 = (gptr<uint4>)reinterpret_cast<const uint4*>(X.post);
+        asm volatile("" : "+s"(post4));
         const uint32_t a0 = (uint32_t)gbase & 3u;  // list start within its 16-byte chunk
         // entries [s, e) of this lane's list cover 16-byte chunks [(a0 + s) / 4, (a0 + e + 3) / 4)
         auto chunks = [a0](uint32_t s, uint32_t e) -> uint32_t { return e > s ? ((a0 + e + 3) >> 2) - ((a0 + s) >> 2) : 0u; };
