@@ -44,11 +44,16 @@ CONFIGS = {
                workload="C2: 1M-row ASCII corpus, gSize=3, weight=NULL, batch=4096/GPU, threshold=0, limit=100"),
     # BASELINE.json configs[3] (our indexW/gSize extension, parity unpinned). With gSize 2 over the
     # 37-symbol alphabet a list holds ~440k postings and a 12-character query reads ~4.7M (19 MB),
-    # 180x a C3 query, so the default batch is 16,384 queries rather than 65,536.
-    "c4": dict(rows=10_000_000, batch=16384, threshold=0.3, limit=100, weights=False, row_size=4, gram=2,
+    # 180x a C3 query: one step is ~0.7 s, so run it with a few --steps.
+    "c4": dict(rows=10_000_000, batch=65536, threshold=0.3, limit=100, weights=False, row_size=4, gram=2,
                wide=True,
                workload="C4: 10M-row UTF-32 corpus via indexW, gSize=2, rowSize=4 (key + 3 aliases), weight=NULL, "
-                        "batch=16384/GPU, threshold=0.3, limit=100"),
+                        "batch=65536/GPU, threshold=0.3, limit=100"),
+    # BASELINE.json configs[4]: 2^20 queries over 8 GPUs = 131,072 per GPU on a 50M-row library
+    # (weight=NULL: the config names none). At N=1 this is the per-GPU slice.
+    "c5": dict(rows=50_000_000, batch=131072, threshold=0.3, limit=100, weights=False,
+               workload="C5: 50M-row ASCII corpus, gSize=3, rowSize=1, weight=NULL, batch=131072/GPU "
+                        "(2^20 over 8 GPUs), threshold=0.3, limit=100"),
 }
 
 
@@ -160,6 +165,53 @@ def cpu_baseline(corpus: Corpus, cfg: dict, raw: bytes, offs: list, target_s: fl
                       f"host threads; index build {build_s:.1f}s not timed"}
 
 
+def dropin_path(L, h, cfg: dict, raw: bytes, offs: list, n_batches: int = 3, n_single: int = 300):
+    """The reference's own entry points on the bench index: scoreBatch over the whole batch (host
+    strings in, new[]'d char** / float* out, released) and single-query score() latency."""
+    B = len(offs) - 1
+    qs = [raw[offs[i]:offs[i + 1]] for i in range(B)]
+    arr = (C.c_char_p * B)(*qs)
+    counts = (C.c_uint32 * B)()
+    res, sc = C.POINTER(C.POINTER(C.c_char))(), C.POINTER(C.c_float)()
+    L.scoreBatch(h, arr, B, cfg["threshold"], cfg["limit"], counts, C.byref(res), C.byref(sc))  # warm
+    L.release(h, res, sc)
+    t = time.perf_counter()
+    for _ in range(n_batches):
+        L.scoreBatch(h, arr, B, cfg["threshold"], cfg["limit"], counts, C.byref(res), C.byref(sc))
+        L.release(h, res, sc)
+    batch_s = (time.perf_counter() - t) / n_batches
+    lat = []
+    for i in range(n_single + 10):
+        t = time.perf_counter()
+        L.score(h, qs[i % B], C.byref(res), C.byref(sc), cfg["threshold"], cfg["limit"])
+        lat.append(time.perf_counter() - t)
+        L.release(h, res, sc)
+    lat = sorted(lat[10:])
+    return {"scorebatch_mqs": round(B / batch_s / 1e6, 4), "scorebatch_ms": round(batch_s * 1e3, 3),
+            "score_us_mean": round(sum(lat) / len(lat) * 1e6, 1), "score_us_p50": round(lat[len(lat) // 2] * 1e6, 1)}
+
+
+def c1_latency(device: int, n: int = 2000):
+    """BASELINE configs[0] shape: 1k-row ASCII corpus, gSize 3, rowSize 1, one query per score()
+    call (the reference's SearchTest harness measures 14.7 us per query on its CPU DLL)."""
+    L = _native.lib()
+    corpus = Corpus(1000, seed=1)
+    h = build_index(corpus, False, device)
+    raw, offs = corpus.queries(256)
+    qs = [raw[offs[i]:offs[i + 1]] for i in range(256)]
+    res, sc = C.POINTER(C.POINTER(C.c_char))(), C.POINTER(C.c_float)()
+    lat = []
+    for i in range(n + 20):
+        t = time.perf_counter()
+        L.score(h, qs[i % 256], C.byref(res), C.byref(sc), 0.3, 100)
+        lat.append(time.perf_counter() - t)
+        L.release(h, res, sc)
+    L.dispose(h)
+    corpus.free()
+    lat = sorted(lat[20:])
+    return {"c1_score_us_mean": round(sum(lat) / len(lat) * 1e6, 1), "c1_score_us_p50": round(lat[len(lat) // 2] * 1e6, 1)}
+
+
 def pmc_traffic(cfg_name: str):
     """HBM bytes per fused-kernel launch from a committed rocprofv3 PMC pass, if any."""
     p = os.path.join(ROOT, "profiles", f"pmc_{cfg_name}.json")
@@ -181,6 +233,7 @@ def main():
     ap.add_argument("--rows", type=int, default=None, help="override corpus rows (debug only)")
     ap.add_argument("--batch", type=int, default=None, help="override per-GPU batch (debug only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-dropin", action="store_true", help="skip the scoreBatch / score() latency lines")
     args = ap.parse_args()
     cfg = dict(CONFIGS[args.config])
     if args.rows:
@@ -216,28 +269,33 @@ def main():
         d_raw = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(dev)
         d_off = torch.tensor(offs, dtype=torch.int64, device=dev)
     stride = min(cfg["limit"], n_keys)
-    d_cnt = torch.zeros(B, dtype=torch.int32, device=dev)
-    d_key = torch.zeros(B * stride, dtype=torch.int32, device=dev)
-    d_sc = torch.zeros(B * stride, dtype=torch.float32, device=dev)
+    # results go straight into the fused gather buffers (shard.GatherBuffer); two of them in turn,
+    # so step i writes one while step i-1's gather still reads the other
+    gbs = [shard.GatherBuffer(B, stride, B, dev) for _ in range(2 if world > 1 else 1)]
     stream = torch.cuda.current_stream(dev).cuda_stream
     L.ngsSetTiming(h, 1)
     st = _native.NgsStats()
+    pending = {}  # buffer index -> in-flight top-k gather (N > 1)
+    nstep = [0]
 
     def step():
+        i = nstep[0] % len(gbs)
+        nstep[0] += 1
+        if i in pending:  # the gather that last read this buffer: ordered before it is rewritten
+            pending.pop(i).complete()
+        gb = gbs[i]
         rc = L.ngsSearchDevice(h, d_raw.data_ptr(), d_off.data_ptr(), B, cfg["threshold"], cfg["limit"], stride,
-                               d_cnt.data_ptr(), d_key.data_ptr(), d_sc.data_ptr(), stream)
+                               gb.counts.data_ptr(), gb.keys.data_ptr(), gb.scores.data_ptr(), stream)
         if rc:
             raise RuntimeError(f"ngsSearchDevice -> {rc}")
         L.ngsLastStats(h, C.byref(st))
-        if world > 1:
-            c, k, s = shard.compact(d_cnt, d_key, d_sc, stride)
-            pending.append(shard.gather_to_root(c, k, s, async_op=True))  # overlaps the next batch
+        if world > 1:  # no size exchange, no host read-back: fixed-size buffers
+            pending[i] = shard.gather_to_root(gb, async_op=True)  # overlaps the next batch
         return st.fast_kernel_ms, st.prep_kernel_ms, st.general_ms
 
-    pending = []  # in-flight top-k gathers (N > 1)
     for _ in range(args.warmup):
         step()
-    for p in pending:
+    for p in pending.values():
         p.complete()
     pending.clear()
     if world > 1:
@@ -247,7 +305,7 @@ def main():
     ktimes = []
     for _ in range(args.steps):
         ktimes.append(step())
-    for p in pending:  # every gather of the timed steps completes inside the timed region
+    for p in pending.values():  # every gather of the timed steps completes inside the timed region
         p.complete()
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -280,8 +338,16 @@ def main():
                    "general_ms": round(sum(k[2] for k in ktimes) / len(ktimes), 4),
                    "general_queries": int(st.general_queries), "results_per_query": round(st.results / B, 2),
                    "survivors_per_query": round(st.survivors / B, 2), "index_build_s": round(index_s, 1),
+                   "paths": {"tier1a_finished": int(st.fast_queries), "heavy_listed": int(st.heavy_queries),
+                             "full_listed": int(st.full_queries), "tier1b_handovers": int(st.handover_queries),
+                             "tier2": int(st.tier2_queries), "general": int(st.general_queries)},
                    "library": L.ngsVersion().decode()},
     }
+    if rank == 0 and world == 1 and not args.no_dropin and not corpus.wide:
+        out["detail"]["dropin"] = dropin_path(L, h, cfg, raw, offs)
+        out["detail"]["dropin"].update(c1_latency(local))
+        out["detail"]["dropin"]["note"] = ("scoreBatch: host strings in, new[]'d char**/float* out (released), "
+                                           "PCIe both ways, whole batch; score(): one query per call")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(corpus, cfg, raw, offs)
     else:

@@ -118,8 +118,18 @@ NGS_API uint64_t getLibSizeW(uint32_t handle);
  * ------------------------------------------------------------------------------------ */
 
 /* Selects the HIP device that the calling thread's next indexN builds on (default: the
- * current HIP device). Returns 0, or a negative HIP error code. */
+ * current HIP device). Same as ngsSetDevices(&device, 1). Returns 0, or a negative HIP error code. */
 NGS_API int ngsSetDevice(int device);
+/* Multi-GPU (BASELINE north_star: "one-shard-per-GPU across the node"): the calling thread's next
+ * indexN / indexG / indexW places one replica of the index on each of the n devices (repeats
+ * allowed; n = 0 restores the default). score/search/scoreBatch/searchBatch on such a handle
+ * split a batch of at least 4,096 queries per replica into contiguous slices, one per replica,
+ * scored concurrently (one host thread and stream each) and joined in query order: the results
+ * are those of one device. ngsSearchDevice uses the replica on the caller's current device.
+ * Returns 0, or a negative HIP error code (nothing changed). */
+NGS_API int ngsSetDevices(const int* devices, int n);
+/* Replicas of the index (devices it was placed on); -1 for an unknown handle. */
+NGS_API int ngsReplicaCount(uint32_t handle);
 NGS_API int ngsDeviceCount(void);
 
 /* Number of master keys; key ids used by ngsSearchDevice are 0..n-1. */

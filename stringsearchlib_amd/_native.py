@@ -116,6 +116,10 @@ def lib():
     L.ngsGramSize.argtypes = [u32]
     L.ngsSetDevice.restype = C.c_int
     L.ngsSetDevice.argtypes = [C.c_int]
+    L.ngsSetDevices.restype = C.c_int
+    L.ngsSetDevices.argtypes = [C.POINTER(C.c_int), C.c_int]
+    L.ngsReplicaCount.restype = C.c_int
+    L.ngsReplicaCount.argtypes = [u32]
     L.ngsDeviceCount.restype = C.c_int
     L.ngsDeviceCount.argtypes = []
     L.ngsNumKeys.restype = u32

@@ -16,6 +16,7 @@
 #include <memory>
 #include <mutex>
 #include <shared_mutex>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -31,6 +32,8 @@ constexpr char kDefaultValid[] = ".%$ @0123456789abcdefghijklmnopqrstuvwxyzABCDE
 constexpr uint32_t kInt32Max = (uint32_t)std::numeric_limits<int32_t>::max();
 constexpr size_t kOutBudget = size_t(1) << 30;       // bytes of (key, score) output per chunk
 constexpr size_t kGeneralBudget = size_t(2) << 30;   // bytes of dense general-path state
+constexpr uint32_t kSmallBatch = 16;                 // host batches up to this many queries take the latency path
+constexpr size_t kSmallBlock = size_t(1) << 20;      // ... if their output block is at most this many bytes
 
 bool hip_ok(hipError_t e, const char* what) {
     if (e == hipSuccess) return true;
@@ -52,6 +55,28 @@ bool dev_upload(T** p, const std::vector<T>& v, std::vector<void*>& owned, size_
     if (pad && !HIP_CHECK(hipMemset(*p + v.size(), 0, pad * sizeof(T)))) return false;
     return v.empty() || HIP_CHECK(hipMemcpy(*p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
 }
+
+// A page-locked host buffer, grown geometrically: the host entry points stage queries and
+// results through these (asynchronous DMA at full PCIe rate instead of pageable bounce copies).
+struct Pinned {
+    void* p = nullptr;
+    size_t cap = 0;
+    bool grow(size_t bytes) {
+        if (bytes <= cap) return true;
+        const size_t nb = std::max<size_t>(bytes, cap * 2);
+        if (p) hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        if (!HIP_CHECK(hipHostMalloc(&p, std::max<size_t>(nb, 64), hipHostMallocDefault))) return false;
+        cap = nb;
+        return true;
+    }
+    template <class T>
+    T* as() const { return static_cast<T*>(p); }
+    ~Pinned() {
+        if (p) hipHostFree(p);
+    }
+};
 
 struct Context {
     int device = 0;
@@ -83,18 +108,26 @@ struct Context {
     DevStats* d_stats = nullptr;
     uint32_t* d_lctr = nullptr;
     DevStats* h_stats = nullptr;   // pinned host copy of the same
+    // host-path outputs, one block holding [n (B + 1) | k (B * stride) | s (B * stride)] for the
+    // call's B and stride, so that a small batch reads all of it back in one copy; packed copies
+    // (launch_pack) for large batches
+    uint32_t* d_out = nullptr;
     uint32_t* d_n = nullptr;
     uint32_t* d_k = nullptr;
     float* d_s = nullptr;
+    uint32_t* d_pos = nullptr;  // [ncap + 1] packed offsets
+    uint32_t* d_pk = nullptr;   // [ocap] packed keys
+    float* d_ps = nullptr;      // [ocap] packed scores
+    void* d_ptemp = nullptr;    // scan scratch
+    size_t ptemp_bytes = 0;
     GeneralBuffers gen;
-    std::vector<uint8_t> h_raw;
-    std::vector<uint64_t> h_off;
+    Pinned h_off, h_raw, h_res;  // queries in; results out
 
     ~Context() {
         hipSetDevice(device);
         for (void* p : {(void*)d_raw, (void*)d_off, (void*)d_norm, (void*)d_qm, (void*)d_glist, (void*)d_list2, (void*)d_fb, (void*)d_fb2, (void*)d_heavy, (void*)d_full, (void*)d_lslots,
                         (void*)d_esn, (void*)d_est, (void*)d_esc,
-                        (void*)d_group, (void*)d_stats, (void*)d_n, (void*)d_k, (void*)d_s, (void*)gen.cnt,
+                        (void*)d_group, (void*)d_stats, (void*)d_out, (void*)d_pos, (void*)d_pk, (void*)d_ps, d_ptemp, (void*)gen.cnt,
                         (void*)gen.kenc, (void*)gen.list, (void*)gen.sorted, (void*)gen.lcount, gen.temp})
             if (p) hipFree(p);
         if (h_stats) hipHostFree(h_stats);
@@ -123,26 +156,19 @@ hipError_t make_side_stream(hipStream_t* s) {
     return hipStreamCreateWithPriority(s, hipStreamNonBlocking, hi);
 }
 
-struct Library {
-    HostIndex host;
+// One copy of the index in one device's HBM, with its pool of per-call contexts. An index built
+// after ngsSetDevices has one replica per listed device; batches are split across them.
+struct Replica {
     int device = 0;
-    bool on_device = false;
     DevIndex dev{};
     std::vector<void*> owned;
-    std::mutex valid_mu;
-    uint32_t valid[8] = {};
     std::mutex pool_mu;
     std::vector<std::unique_ptr<Context>> pool;
-    std::atomic<bool> timing{false};
-    std::mutex stats_mu;
-    ngs_stats last{};
 
-    ~Library() {
+    ~Replica() {
         pool.clear();
-        if (on_device) {
-            hipSetDevice(device);
-            for (void* p : owned) hipFree(p);
-        }
+        hipSetDevice(device);
+        for (void* p : owned) hipFree(p);
     }
 
     std::unique_ptr<Context> acquire() {
@@ -179,44 +205,56 @@ struct Library {
     }
 };
 
+struct Library {
+    HostIndex host;
+    int device = 0;                              // first replica's device (or the build device)
+    std::vector<std::unique_ptr<Replica>> reps;  // empty until the index is on a GPU
+    std::mutex valid_mu;
+    uint32_t valid[8] = {};
+    std::atomic<bool> timing{false};
+    std::mutex stats_mu;
+    ngs_stats last{};
+
+    ~Library() { reps.clear(); }
+    // the replica on `dev`, else the first
+    Replica& replica_on(int dev) {
+        for (auto& r : reps)
+            if (r->device == dev) return *r;
+        return *reps.front();
+    }
+};
+
 std::shared_mutex g_lock;                                        // dllmain.cpp:22
 std::unordered_map<uint32_t, std::unique_ptr<Library>> g_libs;   // dllmain.cpp:24
-thread_local int t_device = -1;
+thread_local std::vector<int> t_devices;                          // ngsSetDevice(s): this thread's next builds
 
 Library* find_lib(uint32_t h) {
     auto it = g_libs.find(h);
     return it == g_libs.end() ? nullptr : it->second.get();
 }
 
-bool upload(Library& L) {
-    int dev = t_device;
-    if (dev < 0 && !HIP_CHECK(hipGetDevice(&dev))) return false;
-    if (!HIP_CHECK(hipSetDevice(dev))) return false;
-    L.device = dev;
+// Places one copy of the host-built index on device R.device. The host arrays stay until every
+// replica is uploaded (free_uploaded).
+bool upload_replica(Library& L, Replica& R, bool keys_unique) {
+    if (!HIP_CHECK(hipSetDevice(R.device))) return false;
     HostIndex& H = L.host;
-    DevIndex& X = L.dev;
+    DevIndex& X = R.dev;
     X.n_terms = H.n_terms;
     X.n_short = H.n_short;
     X.n_keys = H.n_keys;
-    {
-        std::vector<uint8_t> seen(H.n_keys, 0);
-        X.keys_unique = 1;
-        for (const uint2& kw : H.tk) {
-            if (seen[kw.x]) { X.keys_unique = 0; break; }
-            seen[kw.x] = 1;
-        }
-    }
-    std::vector<uint8_t> kb(H.key_bytes.begin(), H.key_bytes.end());
+    X.keys_unique = keys_unique ? 1u : 0u;
+    const std::vector<char>& kb = H.key_bytes;
     uint64_t *gram_off, *term_off, *key_off;
     uint32_t *post, *tk_off, *wild_key, *gram_row, *skip;
-    uint8_t *term_bytes, *key_bytes;
+    uint8_t* term_bytes;
+    char* key_bytes;
     uint2* tk;
     float *wild_w, *wild_score;
-    L.on_device = true;  // from here on the destructor frees what was allocated
-    bool ok = dev_upload(&term_off, H.term_off, L.owned) && dev_upload(&term_bytes, H.term_bytes, L.owned) &&
-              dev_upload(&tk_off, H.tk_off, L.owned) && dev_upload(&tk, H.tk, L.owned) &&
-              dev_upload(&key_off, H.key_off, L.owned) && dev_upload(&key_bytes, kb, L.owned) &&
-              dev_upload(&wild_w, H.wild_w, L.owned);
+    // from here on the replica's destructor frees what was allocated
+    bool ok = dev_upload(&term_off, H.term_off, R.owned) && dev_upload(&term_bytes, H.term_bytes, R.owned) &&
+              dev_upload(&tk_off, H.tk_off, R.owned) && dev_upload(&tk, H.tk, R.owned) &&
+              dev_upload(&key_off, H.key_off, R.owned) && dev_upload(&key_bytes, kb, R.owned) &&
+              dev_upload(&wild_w, H.wild_w, R.owned);
     if (!ok) return false;
     bool dev_built = false;
     if (!H.grams_built) {
@@ -229,7 +267,7 @@ bool upload(Library& L) {
             std::fprintf(stderr, "[ngs build] %-22s %8.3f s\n", "gram CSR + skip (GPU)",
                          std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
         if (e == hipSuccess) {
-            for (void* p : {(void*)dg.gram_off, (void*)dg.post, (void*)dg.gram_row, (void*)dg.skip}) L.owned.push_back(p);
+            for (void* p : {(void*)dg.gram_off, (void*)dg.post, (void*)dg.gram_row, (void*)dg.skip}) R.owned.push_back(p);
             gram_off = dg.gram_off;
             post = dg.post;
             gram_row = dg.gram_row;
@@ -245,12 +283,12 @@ bool upload(Library& L) {
         }
     }
     if (!dev_built)  // host-built gram CSR (dictionary indexes, NGS_HOST_GRAMS, device-build failure)
-        ok = dev_upload(&gram_off, H.gram_off, L.owned) && dev_upload(&post, H.post, L.owned, 4) /* k_wave stages whole 16-byte chunks */ &&
-             dev_upload(&gram_row, H.gram_row, L.owned) && dev_upload(&skip, H.skip, L.owned);
+        ok = dev_upload(&gram_off, H.gram_off, R.owned) && dev_upload(&post, H.post, R.owned, 4) /* k_wave stages whole 16-byte chunks */ &&
+             dev_upload(&gram_row, H.gram_row, R.owned) && dev_upload(&skip, H.skip, R.owned);
     if (!ok) return false;
     uint64_t* ghash_key = nullptr;
     uint32_t* ghash_val = nullptr;
-    if (H.gram_mode == 1 && !(dev_upload(&ghash_key, H.ghash_key, L.owned) && dev_upload(&ghash_val, H.ghash_val, L.owned)))
+    if (H.gram_mode == 1 && !(dev_upload(&ghash_key, H.ghash_key, R.owned) && dev_upload(&ghash_val, H.ghash_val, R.owned)))
         return false;
     X.gsz = H.gsz;
     X.csize = H.csize;
@@ -261,9 +299,9 @@ bool upload(Library& L) {
     X.ghash_key = ghash_key;
     X.ghash_val = ghash_val;
     if (!dev_alloc(&wild_key, H.n_keys)) return false;
-    L.owned.push_back(wild_key);
+    R.owned.push_back(wild_key);
     if (!dev_alloc(&wild_score, H.n_keys)) return false;
-    L.owned.push_back(wild_score);
+    R.owned.push_back(wild_score);
     if (!HIP_CHECK(build_wildcard(wild_w, H.n_keys, wild_key, wild_score, nullptr))) return false;
     X.gram_off = gram_off;
     X.post = post;
@@ -276,10 +314,15 @@ bool upload(Library& L) {
     X.tk_off = tk_off;
     X.tk = tk;
     X.key_off = key_off;
-    X.key_bytes = key_bytes;
+    X.key_bytes = reinterpret_cast<const uint8_t*>(key_bytes);
     X.wild_key = wild_key;
     X.wild_score = wild_score;
-    // the device copy is authoritative for the search; keep only what marshalling needs
+    // the build's null-stream work completes before any search stream (non-blocking) reads it
+    return HIP_CHECK(hipDeviceSynchronize());
+}
+
+// The device copies are authoritative for the search; keep only what marshalling needs.
+void free_uploaded(HostIndex& H) {
     std::vector<uint64_t>().swap(H.gram_off);
     std::vector<uint32_t>().swap(H.post);
     std::vector<uint32_t>().swap(H.gram_row);
@@ -291,6 +334,27 @@ bool upload(Library& L) {
     std::vector<float>().swap(H.wild_w);
     std::vector<uint64_t>().swap(H.ghash_key);
     std::vector<uint32_t>().swap(H.ghash_val);
+}
+
+// One replica per device in `devs` (repeats allowed: several replicas on one device split a batch
+// like several devices do, which the one-GPU tests use).
+bool upload(Library& L, const std::vector<int>& devs) {
+    const HostIndex& H = L.host;
+    bool keys_unique = true;
+    {
+        std::vector<uint8_t> seen(H.n_keys, 0);
+        for (const uint2& kw : H.tk) {
+            if (seen[kw.x]) { keys_unique = false; break; }
+            seen[kw.x] = 1;
+        }
+    }
+    for (int d : devs) {
+        L.reps.push_back(std::make_unique<Replica>());
+        L.reps.back()->device = d;
+        if (!upload_replica(L, *L.reps.back(), keys_unique)) return false;
+    }
+    L.device = devs.front();
+    free_uploaded(L.host);
     return true;
 }
 
@@ -319,19 +383,30 @@ bool ensure_queries(Context& c, size_t B, size_t bytes) {
 
 bool ensure_outputs(Context& c, size_t B, size_t stride) {
     const size_t need = B * stride;
-    if (!c.d_n || B > c.ncap || need > c.ocap) {
-        for (void** p : {(void**)&c.d_n, (void**)&c.d_k, (void**)&c.d_s})
+    if (!c.d_out || B > c.ncap || need > c.ocap) {
+        for (void** p : {(void**)&c.d_out, (void**)&c.d_pos, (void**)&c.d_pk, (void**)&c.d_ps, &c.d_ptemp})
             if (*p) { hipFree(*p); *p = nullptr; }
-        if (!dev_alloc(&c.d_n, B) || !dev_alloc(&c.d_k, need) || !dev_alloc(&c.d_s, need)) return false;
-        c.ncap = B;
-        c.ocap = need;
+        c.d_n = c.d_k = nullptr;
+        c.d_s = nullptr;
+        const size_t nb = std::max(B, c.ncap), ob = std::max(need, c.ocap);
+        if (!dev_alloc(&c.d_out, nb + 1 + 2 * ob) || !dev_alloc(&c.d_pos, nb + 1) || !dev_alloc(&c.d_pk, ob) ||
+            !dev_alloc(&c.d_ps, ob))
+            return false;
+        c.ptemp_bytes = pack_temp_bytes((uint32_t)nb);
+        if (!HIP_CHECK(hipMalloc(&c.d_ptemp, std::max<size_t>(c.ptemp_bytes, 1)))) return false;
+        c.ncap = nb;
+        c.ocap = ob;
     }
+    // this call's views: [n (B + 1) | k (B * stride) | s (B * stride)] from the block's start
+    c.d_n = c.d_out;
+    c.d_k = c.d_out + B + 1;
+    c.d_s = reinterpret_cast<float*>(c.d_k + need);
     return true;
 }
 
-bool ensure_general(Library& L, Context& c) {
+bool ensure_general(const Replica& R, Context& c, hipStream_t s) {
     if (c.gen.G) return true;
-    const DevIndex& X = L.dev;
+    const DevIndex& X = R.dev;
     const uint64_t n_long = X.n_terms - X.n_short;
     const uint64_t per = n_long * 4 + (uint64_t)X.n_keys * 12 + 64;
     uint32_t G = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(64, kGeneralBudget / per));
@@ -342,19 +417,24 @@ bool ensure_general(Library& L, Context& c) {
         return false;
     W.temp_bytes = general_sort_temp_bytes(X.n_keys);
     if (!HIP_CHECK(hipMalloc(&W.temp, std::max<size_t>(W.temp_bytes, 1)))) return false;
-    if (!HIP_CHECK(hipMemset(W.cnt, 0, sizeof(uint32_t) * std::max<size_t>((size_t)G * n_long, 1))) ||
-        !HIP_CHECK(hipMemset(W.kenc, 0, sizeof(uint32_t) * std::max<size_t>((size_t)G * X.n_keys, 1))))
+    // on the call's stream: a plain hipMemset runs on the null stream, which the context's
+    // non-blocking streams do not wait for (the first group's counts raced with it)
+    if (!HIP_CHECK(hipMemsetAsync(W.cnt, 0, sizeof(uint32_t) * std::max<size_t>((size_t)G * n_long, 1), s)) ||
+        !HIP_CHECK(hipMemsetAsync(W.kenc, 0, sizeof(uint32_t) * std::max<size_t>((size_t)G * X.n_keys, 1), s)))
         return false;
     W.G = G;
     return true;
 }
 
-// The search pipeline over B queries already in device memory. Returns 0 or a negative code.
-int device_search(Library& L, Context& c, const uint8_t* d_raw, const uint64_t* d_off, uint32_t B, uint64_t qbytes,
-                  float thr, uint32_t limit, uint32_t stride, uint32_t* d_n, uint32_t* d_k, float* d_s,
-                  hipStream_t s) {
-    if (!B) return 0;
-    SearchParams P{};
+// The search pipeline over B queries already in device memory, in two halves: queue_search
+// queues the normalisation, the tier kernels and the read-back of the statistics and path
+// counts; finish_search waits for them, runs the general path for the queries listed for it
+// and records the statistics. small: one kernel per tier on the call's stream (no routing
+// lists, no side streams; the latency path of score() and small batches).
+int queue_search(Library& L, Replica& R, Context& c, const uint8_t* d_raw, const uint64_t* d_off, uint32_t B,
+                 uint64_t qbytes, float thr, uint32_t limit, uint32_t stride, uint32_t* d_n, uint32_t* d_k,
+                 float* d_s, hipStream_t s, SearchParams& P, bool small) {
+    P = SearchParams{};
     P.thr = thr;
     P.limit = limit;
     P.out_stride = stride;
@@ -369,7 +449,7 @@ int device_search(Library& L, Context& c, const uint8_t* d_raw, const uint64_t* 
         const uint32_t w = e ? (uint32_t)std::strtoul(e, nullptr, 0) : kDefaultWaves;
         return w == 0 || w == 1 || w == 2 || w == 4 ? w : kDefaultWaves;
     }();
-    P.waves = waves;
+    P.waves = small ? 1u : waves;
     static const uint32_t heavy_waves = [] {
         const char* e = std::getenv("NGS_HEAVY_WAVES");
         const uint32_t w = e ? (uint32_t)std::strtoul(e, nullptr, 0) : kHeavyWaves;
@@ -390,17 +470,15 @@ int device_search(Library& L, Context& c, const uint8_t* d_raw, const uint64_t* 
     P.est = c.d_est;
     P.esc = c.d_esc;
     const bool timing = L.timing.load();
-    ngs_stats st{};
-    st.queries = B;
     // statistics, path counts and list counters
     if (!HIP_CHECK(hipMemsetAsync(c.d_stats, 0, sizeof(DevStats) * (kStatSlots + 1 + 2 * kListSlots), s))) return -4;
     if (timing) HIP_CHECK(hipEventRecord(c.ev[0], s));
-    if (!HIP_CHECK(launch_prep(d_raw, d_off, B, P, c.d_norm, c.d_qm, L.dev.csize, L.dev, c.d_heavy, c.d_gcount + 3,
+    if (!HIP_CHECK(launch_prep(d_raw, d_off, B, P, c.d_norm, c.d_qm, R.dev.csize, R.dev, c.d_heavy, c.d_gcount + 3,
                                c.d_full, c.d_gcount + 5, c.d_lslots, c.d_lctr, s)))
         return -4;
     if (timing) HIP_CHECK(hipEventRecord(c.ev[1], s));
     if (timing) HIP_CHECK(hipEventRecord(c.ev[2], s));
-    if (!HIP_CHECK(launch_fast(L.dev, P, c.d_norm, d_off, c.d_qm, d_n, d_k, d_s, c.d_list2, c.d_gcount + 1,
+    if (!HIP_CHECK(launch_fast(R.dev, P, c.d_norm, d_off, c.d_qm, d_n, d_k, d_s, c.d_list2, c.d_gcount + 1,
                                c.d_fb, c.d_gcount + 2, c.d_fb2, c.d_gcount + 4, c.d_heavy, c.d_gcount + 3, c.d_full,
                                c.d_gcount + 5, c.d_glist, c.d_gcount, c.d_stats, s, c.side, c.side2, c.fork, c.join,
                                c.join2)))
@@ -408,9 +486,17 @@ int device_search(Library& L, Context& c, const uint8_t* d_raw, const uint64_t* 
     if (timing) HIP_CHECK(hipEventRecord(c.ev[3], s));
     // the statistics and the path counts in one read-back (the general path adds no statistics)
     if (!HIP_CHECK(hipMemcpyAsync(c.h_stats, c.d_stats, sizeof(DevStats) * (kStatSlots + 1), hipMemcpyDeviceToHost,
-                                  s)) ||
-        !HIP_CHECK(hipStreamSynchronize(s)))
+                                  s)))
         return -4;
+    return 0;
+}
+
+int finish_search(Library& L, Replica& R, Context& c, uint32_t B, const SearchParams& P, const uint64_t* d_off,
+                  uint32_t* d_n, uint32_t* d_k, float* d_s, hipStream_t s) {
+    if (!HIP_CHECK(hipStreamSynchronize(s))) return -4;
+    const bool timing = L.timing.load();
+    ngs_stats st{};
+    st.queries = B;
     // general, tier 2, tier 1a hand-overs, heavy, heavy hand-overs, full
     const uint32_t* counts3 = reinterpret_cast<const uint32_t*>(c.h_stats + kStatSlots);
     const uint32_t ngen = counts3[0];
@@ -420,13 +506,13 @@ int device_search(Library& L, Context& c, const uint8_t* d_raw, const uint64_t* 
             !HIP_CHECK(hipStreamSynchronize(s)))
             return -4;
         std::sort(gl.begin(), gl.end());
-        if (!ensure_general(L, c)) return -4;
+        if (!ensure_general(R, c, s)) return -4;
         if (timing) HIP_CHECK(hipEventRecord(c.ev[4], s));
         for (uint32_t g0 = 0; g0 < ngen; g0 += c.gen.G) {
             const uint32_t G = std::min(c.gen.G, ngen - g0);
             if (!HIP_CHECK(hipMemcpyAsync(c.d_group, gl.data() + g0, sizeof(uint32_t) * G, hipMemcpyHostToDevice, s)))
                 return -4;
-            if (!HIP_CHECK(run_general(L.dev, P, c.d_norm, d_off, c.d_qm, c.d_group, gl.data() + g0, G, c.gen, d_n,
+            if (!HIP_CHECK(run_general(R.dev, P, c.d_norm, d_off, c.d_qm, c.d_group, gl.data() + g0, G, c.gen, d_n,
                                        d_k, d_s, s)))
                 return -4;
         }
@@ -471,6 +557,15 @@ int device_search(Library& L, Context& c, const uint8_t* d_raw, const uint64_t* 
     return 0;
 }
 
+int device_search(Library& L, Replica& R, Context& c, const uint8_t* d_raw, const uint64_t* d_off, uint32_t B,
+                  uint64_t qbytes, float thr, uint32_t limit, uint32_t stride, uint32_t* d_n, uint32_t* d_k,
+                  float* d_s, hipStream_t s) {
+    if (!B) return 0;
+    SearchParams P;
+    const int rc = queue_search(L, R, c, d_raw, d_off, B, qbytes, thr, limit, stride, d_n, d_k, d_s, s, P, false);
+    return rc ? rc : finish_search(L, R, c, B, P, d_off, d_n, d_k, d_s, s);
+}
+
 uint32_t effective_limit(const Library& L, uint32_t limit) {
     if (limit == 0) limit = kInt32Max;  // nGramSearch.hpp:420-421
     return std::min<uint32_t>(limit, L.host.n_keys);
@@ -483,57 +578,141 @@ size_t str_len(const CharT* p) {
     return n;
 }
 
-// Host entry: scores n queries (characters of the index's width); fills counts and flat
+// Scores n queries (characters of the index's width) on one replica; fills counts and flat
 // (key, score) vectors.
 template <typename CharT>
-bool host_search(Library& L, const CharT* const* queries, uint32_t nq, float thr, uint32_t limit,
-                 std::vector<uint32_t>& counts, std::vector<uint32_t>& keys, std::vector<float>& scores) {
+bool host_search_one(Library& L, Replica& R, const CharT* const* queries, uint32_t nq, float thr, uint32_t Lm,
+                     std::vector<uint32_t>& counts, std::vector<uint32_t>& keys, std::vector<float>& scores) {
     constexpr size_t cs = sizeof(CharT);
     counts.assign(nq, 0);
     keys.clear();
     scores.clear();
-    const uint32_t Lm = effective_limit(L, limit);
     if (Lm == 0 || nq == 0) return true;
-    if (!HIP_CHECK(hipSetDevice(L.device))) return false;
-    std::unique_ptr<Context> c = L.acquire();
+    if (!HIP_CHECK(hipSetDevice(R.device))) return false;
+    std::unique_ptr<Context> c = R.acquire();
     if (!c) return false;
     const size_t stride = Lm;
     const size_t max_chunk = std::max<size_t>(1, std::min<size_t>(1 << 20, kOutBudget / (stride * 8)));
-    std::vector<uint32_t> hk, hn;
-    std::vector<float> hs;
     bool ok = true;
     for (uint32_t q0 = 0; q0 < nq && ok; q0 += (uint32_t)max_chunk) {
         const uint32_t B = (uint32_t)std::min<size_t>(max_chunk, nq - q0);
-        c->h_off.resize(B + 1);
-        c->h_off[0] = 0;
-        for (uint32_t i = 0; i < B; ++i) c->h_off[i + 1] = c->h_off[i] + (queries[q0 + i] ? str_len(queries[q0 + i]) * cs : 0);
-        c->h_raw.resize(std::max<uint64_t>(c->h_off[B], 1));
+        // queries into pinned staging: offsets, then the bytes
+        ok = c->h_off.grow(sizeof(uint64_t) * (B + 1));
+        if (!ok) break;
+        uint64_t* ho = c->h_off.as<uint64_t>();
+        ho[0] = 0;
+        for (uint32_t i = 0; i < B; ++i) ho[i + 1] = ho[i] + (queries[q0 + i] ? str_len(queries[q0 + i]) * cs : 0);
+        ok = c->h_raw.grow(std::max<uint64_t>(ho[B], 1));
+        if (!ok) break;
         for (uint32_t i = 0; i < B; ++i)
-            if (queries[q0 + i]) std::memcpy(c->h_raw.data() + c->h_off[i], queries[q0 + i], c->h_off[i + 1] - c->h_off[i]);
-        ok = ensure_queries(*c, B, c->h_off[B]) && ensure_outputs(*c, B, stride) &&
-             HIP_CHECK(hipMemcpyAsync(c->d_raw, c->h_raw.data(), c->h_off[B], hipMemcpyHostToDevice, c->stream)) &&
-             HIP_CHECK(hipMemcpyAsync(c->d_off, c->h_off.data(), sizeof(uint64_t) * (B + 1), hipMemcpyHostToDevice,
-                                      c->stream));
+            if (queries[q0 + i]) std::memcpy(c->h_raw.as<uint8_t>() + ho[i], queries[q0 + i], ho[i + 1] - ho[i]);
+        ok = ensure_queries(*c, B, ho[B]) && ensure_outputs(*c, B, stride) &&
+             HIP_CHECK(hipMemcpyAsync(c->d_raw, c->h_raw.p, ho[B], hipMemcpyHostToDevice, c->stream)) &&
+             HIP_CHECK(hipMemcpyAsync(c->d_off, ho, sizeof(uint64_t) * (B + 1), hipMemcpyHostToDevice, c->stream));
         if (!ok) break;
-        ok = device_search(L, *c, c->d_raw, c->d_off, B, c->h_off[B], thr, Lm, (uint32_t)stride, c->d_n, c->d_k,
-                           c->d_s, c->stream) == 0;
+        // small batches: one kernel per tier on one stream, and the whole output block read back
+        // with the statistics before the one wait (score()'s latency path)
+        const size_t block = sizeof(uint32_t) * (B + 1 + 2 * (size_t)B * stride);
+        const bool small = B <= kSmallBatch && block <= kSmallBlock;
+        SearchParams P;
+        ok = queue_search(L, R, *c, c->d_raw, c->d_off, B, ho[B], thr, Lm, (uint32_t)stride, c->d_n, c->d_k, c->d_s,
+                          c->stream, P, small) == 0;
         if (!ok) break;
-        hn.resize(B);
-        hk.resize((size_t)B * stride);
-        hs.resize((size_t)B * stride);
-        ok = HIP_CHECK(hipMemcpyAsync(hn.data(), c->d_n, sizeof(uint32_t) * B, hipMemcpyDeviceToHost, c->stream)) &&
-             HIP_CHECK(hipMemcpyAsync(hk.data(), c->d_k, sizeof(uint32_t) * B * stride, hipMemcpyDeviceToHost, c->stream)) &&
-             HIP_CHECK(hipMemcpyAsync(hs.data(), c->d_s, sizeof(float) * B * stride, hipMemcpyDeviceToHost, c->stream)) &&
+        if (small) {
+            ok = c->h_res.grow(block) &&
+                 HIP_CHECK(hipMemcpyAsync(c->h_res.p, c->d_out, block, hipMemcpyDeviceToHost, c->stream));
+            if (!ok) break;
+        }
+        ok = finish_search(L, R, *c, B, P, c->d_off, c->d_n, c->d_k, c->d_s, c->stream) == 0;
+        if (!ok) break;
+        const uint32_t* counts3 = reinterpret_cast<const uint32_t*>(c->h_stats + kStatSlots);
+        if (small && counts3[0]) {  // the general path ran after the read-back: read again
+            ok = HIP_CHECK(hipMemcpyAsync(c->h_res.p, c->d_out, block, hipMemcpyDeviceToHost, c->stream)) &&
+                 HIP_CHECK(hipStreamSynchronize(c->stream));
+            if (!ok) break;
+        }
+        if (small) {
+            const uint32_t* hn = c->h_res.as<uint32_t>();
+            const uint32_t* hk = hn + B + 1;
+            const float* hs = reinterpret_cast<const float*>(hk + (size_t)B * stride);
+            for (uint32_t i = 0; i < B; ++i) {
+                counts[q0 + i] = hn[i];
+                keys.insert(keys.end(), hk + (size_t)i * stride, hk + (size_t)i * stride + hn[i]);
+                scores.insert(scores.end(), hs + (size_t)i * stride, hs + (size_t)i * stride + hn[i]);
+            }
+            continue;
+        }
+        // large batches: pack on the device (prefix sum of the counts, one copy per query), read
+        // back the offsets, then exactly the packed records
+        ok = HIP_CHECK(hipMemsetAsync(c->d_n + B, 0, sizeof(uint32_t), c->stream)) &&
+             HIP_CHECK(launch_pack(c->d_n, c->d_k, c->d_s, B, (uint32_t)stride, c->d_pos, c->d_pk, c->d_ps,
+                                   c->d_ptemp, c->ptemp_bytes, c->stream)) &&
+             c->h_res.grow(sizeof(uint32_t) * (B + 1)) &&
+             HIP_CHECK(hipMemcpyAsync(c->h_res.p, c->d_pos, sizeof(uint32_t) * (B + 1), hipMemcpyDeviceToHost,
+                                      c->stream)) &&
              HIP_CHECK(hipStreamSynchronize(c->stream));
         if (!ok) break;
-        for (uint32_t i = 0; i < B; ++i) {
-            counts[q0 + i] = hn[i];
-            keys.insert(keys.end(), hk.begin() + (size_t)i * stride, hk.begin() + (size_t)i * stride + hn[i]);
-            scores.insert(scores.end(), hs.begin() + (size_t)i * stride, hs.begin() + (size_t)i * stride + hn[i]);
-        }
+        const uint32_t total = c->h_res.as<uint32_t>()[B];
+        for (uint32_t i = 0; i < B; ++i) counts[q0 + i] = c->h_res.as<uint32_t>()[i + 1] - c->h_res.as<uint32_t>()[i];
+        const size_t k0 = keys.size();
+        keys.resize(k0 + total);
+        scores.resize(k0 + total);
+        ok = c->h_res.grow(sizeof(uint32_t) * 2 * (size_t)total) &&
+             HIP_CHECK(hipMemcpyAsync(c->h_res.p, c->d_pk, sizeof(uint32_t) * total, hipMemcpyDeviceToHost, c->stream)) &&
+             HIP_CHECK(hipMemcpyAsync(c->h_res.as<uint32_t>() + total, c->d_ps, sizeof(float) * total,
+                                      hipMemcpyDeviceToHost, c->stream)) &&
+             HIP_CHECK(hipStreamSynchronize(c->stream));
+        if (!ok) break;
+        std::memcpy(keys.data() + k0, c->h_res.p, sizeof(uint32_t) * total);
+        std::memcpy(scores.data() + k0, c->h_res.as<uint32_t>() + total, sizeof(float) * total);
     }
-    L.give_back(std::move(c));
+    R.give_back(std::move(c));
     return ok;
+}
+
+// Queries per replica below which a batch is not split (a split costs a host thread and a
+// launch sequence per replica). NGS_SPLIT_MIN overrides it (tests split small batches).
+uint32_t split_min() {
+    static const uint32_t v = [] {
+        const char* e = std::getenv("NGS_SPLIT_MIN");
+        return e ? std::max<uint32_t>(1, (uint32_t)std::strtoul(e, nullptr, 0)) : 4096u;
+    }();
+    return v;
+}
+
+// Host entry: one replica scores the batch, or (an index on several devices) contiguous slices
+// of it go to the replicas, one host thread each, and the slices' results are joined in order.
+// Queries are independent, so the joined result is the single-device result.
+template <typename CharT>
+bool host_search(Library& L, const CharT* const* queries, uint32_t nq, float thr, uint32_t limit,
+                 std::vector<uint32_t>& counts, std::vector<uint32_t>& keys, std::vector<float>& scores) {
+    const uint32_t Lm = effective_limit(L, limit);
+    const size_t nrep = L.reps.size();
+    const uint32_t parts = (uint32_t)std::min<uint64_t>(nrep, std::max<uint64_t>(1, nq / split_min()));
+    if (parts <= 1) return host_search_one(L, *L.reps.front(), queries, nq, thr, Lm, counts, keys, scores);
+    const uint32_t per = (nq + parts - 1) / parts;
+    std::vector<std::vector<uint32_t>> pc(parts), pk(parts);
+    std::vector<std::vector<float>> ps(parts);
+    std::vector<char> pok(parts, 0);
+    std::vector<std::thread> th;
+    for (uint32_t i = 0; i < parts; ++i) {
+        const uint32_t q0 = i * per, n = std::min(per, nq - std::min(nq, q0));
+        th.emplace_back([&, i, q0, n] {
+            pok[i] = host_search_one(L, *L.reps[i], queries + q0, n, thr, Lm, pc[i], pk[i], ps[i]);
+        });
+    }
+    for (auto& t : th) t.join();
+    counts.clear();
+    keys.clear();
+    scores.clear();
+    counts.reserve(nq);
+    for (uint32_t i = 0; i < parts; ++i) {
+        if (!pok[i]) return false;
+        counts.insert(counts.end(), pc[i].begin(), pc[i].end());
+        keys.insert(keys.end(), pk[i].begin(), pk[i].end());
+        scores.insert(scores.end(), ps[i].begin(), ps[i].end());
+    }
+    return true;
 }
 
 void set_valid(Library& L, const char* chars, int n) {
@@ -606,15 +785,17 @@ uint32_t new_library(Build&& build) {
     auto L = std::make_unique<Library>();
     set_valid(*L, kDefaultValid, (int)std::strlen(kDefaultValid));
     build(L->host);
-    if (L->host.indexed && !upload(*L)) {
+    std::vector<int> devs = t_devices;
+    if (devs.empty()) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+        devs.push_back(dev);
+    }
+    if (L->host.indexed && !upload(*L, devs)) {
         std::fprintf(stderr, "ngram_search: indexN could not place the index on a GPU\n");
         return 0;
     }
-    if (!L->host.indexed) {
-        int dev = t_device;
-        if (dev < 0 && hipGetDevice(&dev) != hipSuccess) dev = 0;
-        L->device = dev;
-    }
+    if (!L->host.indexed) L->device = devs.front();
     g_libs.emplace(handle, std::move(L));
     return handle;
 }
@@ -726,13 +907,23 @@ NGS_API uint64_t getSizeW(uint32_t handle) { return getSize(handle); }
 
 NGS_API uint64_t getLibSizeW(uint32_t handle) { return getLibSize(handle); }
 
-NGS_API int ngsSetDevice(int device) {
-    int n = 0;
-    hipError_t e = hipGetDeviceCount(&n);
+NGS_API int ngsSetDevices(const int* devices, int n) {
+    if (n < 0 || (n > 0 && !devices)) return -(int)hipErrorInvalidValue;
+    int nd = 0;
+    hipError_t e = hipGetDeviceCount(&nd);
     if (e != hipSuccess) return -(int)e;
-    if (device < 0 || device >= n) return -(int)hipErrorInvalidDevice;
-    t_device = device;
+    for (int i = 0; i < n; ++i)
+        if (devices[i] < 0 || devices[i] >= nd) return -(int)hipErrorInvalidDevice;
+    t_devices.assign(devices, devices + n);
     return 0;
+}
+
+NGS_API int ngsSetDevice(int device) { return ngsSetDevices(&device, 1); }
+
+NGS_API int ngsReplicaCount(uint32_t handle) {
+    std::shared_lock<std::shared_mutex> lk(g_lock);
+    Library* L = find_lib(handle);
+    return L ? (int)L->reps.size() : -1;
 }
 
 NGS_API int ngsDeviceCount(void) {
@@ -781,7 +972,11 @@ NGS_API int ngsSearchDevice(uint32_t handle, const uint8_t* dQueryBytes, const u
     if (!L->host.indexed) return -2;
     const uint32_t Lm = effective_limit(*L, limit);
     if (!dQueryOffsets || !dCounts || (nQueries && Lm && (!dKeys || !dScores || outStride < Lm))) return -3;
-    if (!HIP_CHECK(hipSetDevice(L->device))) return -4;
+    // the replica on the caller's current device (the buffers' device)
+    int cur = L->device;
+    if (!HIP_CHECK(hipGetDevice(&cur))) return -4;
+    Replica& R = L->replica_on(cur);
+    if (!HIP_CHECK(hipSetDevice(R.device))) return -4;
     hipStream_t s = (hipStream_t)stream;
     if (Lm == 0) {
         return HIP_CHECK(hipMemsetAsync(dCounts, 0, sizeof(uint32_t) * nQueries, s)) &&
@@ -789,7 +984,7 @@ NGS_API int ngsSearchDevice(uint32_t handle, const uint8_t* dQueryBytes, const u
                    ? 0
                    : -4;
     }
-    std::unique_ptr<Context> c = L->acquire();
+    std::unique_ptr<Context> c = R.acquire();
     if (!c) return -4;
     uint64_t qbytes = 0;
     int rc = 0;
@@ -797,9 +992,9 @@ NGS_API int ngsSearchDevice(uint32_t handle, const uint8_t* dQueryBytes, const u
         (!HIP_CHECK(hipMemcpyAsync(&qbytes, dQueryOffsets + nQueries, sizeof(uint64_t), hipMemcpyDeviceToHost, s)) ||
          !HIP_CHECK(hipStreamSynchronize(s))))
         rc = -4;
-    if (!rc) rc = device_search(*L, *c, dQueryBytes, dQueryOffsets, nQueries, qbytes, threshold, Lm, outStride,
+    if (!rc) rc = device_search(*L, R, *c, dQueryBytes, dQueryOffsets, nQueries, qbytes, threshold, Lm, outStride,
                                 dCounts, dKeys, dScores, s);
-    L->give_back(std::move(c));
+    R.give_back(std::move(c));
     return rc;
 }
 
@@ -828,10 +1023,11 @@ NGS_API const char* ngsVersion(void) { return "ngram_search 0.2 gfx950 src=" NGS
 NGS_API int ngsIndexDigest(uint32_t handle, uint64_t* out, int n) {
     std::shared_lock<std::shared_mutex> lk(g_lock);
     auto it = g_libs.find(handle);
-    if (it == g_libs.end() || !it->second->on_device || !out) return -1;
+    if (it == g_libs.end() || it->second->reps.empty() || !out) return -1;
     Library& L = *it->second;
-    const DevIndex& X = L.dev;
-    if (!HIP_CHECK(hipSetDevice(L.device))) return -4;
+    const Replica& R = *L.reps.front();
+    const DevIndex& X = R.dev;
+    if (!HIP_CHECK(hipSetDevice(R.device))) return -4;
     // (bytes, FNV-1a) of gram_off, post, gram_row, skip as the kernels read them
     auto digest = [](const void* d, size_t bytes, uint64_t& h) -> bool {
         std::vector<uint8_t> v(bytes);

@@ -29,6 +29,13 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
                        const uint32_t* fcount, uint32_t* glist, uint32_t* gcount, DevStats* stats, hipStream_t s,
                        hipStream_t side, hipStream_t side2, hipEvent_t fork, hipEvent_t join, hipEvent_t join2);
 
+// Result compaction for the host entry points: pos[0..B] = exclusive prefix sum of n[0..B) (n
+// holds B + 1 entries, n[B] = 0), then query q's n[q] records (k, s at q * stride) are copied to
+// pk / ps at pos[q]. The host then copies pos and the pos[B] packed records, not B * stride.
+size_t pack_temp_bytes(uint32_t B);
+hipError_t launch_pack(const uint32_t* n, const uint32_t* k, const float* s, uint32_t B, uint32_t stride,
+                       uint32_t* pos, uint32_t* pk, float* ps, void* temp, size_t temp_bytes, hipStream_t st);
+
 // Wildcard answer (nGramSearch.hpp:356-369): keys sorted by (weight desc, rank asc).
 hipError_t build_wildcard(const float* d_w, uint32_t n_keys, uint32_t* d_keys, float* d_scores, hipStream_t s);
 

@@ -2373,6 +2373,35 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
     return hipGetLastError();
 }
 
+// one wave per query: its records to the packed arrays
+__global__ __launch_bounds__(256) void k_pack(const uint32_t* __restrict__ n, const uint32_t* __restrict__ k,
+                                              const float* __restrict__ s, uint32_t B, uint32_t stride,
+                                              const uint32_t* __restrict__ pos, uint32_t* __restrict__ pk,
+                                              float* __restrict__ ps) {
+    const uint32_t q = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    if (q >= B) return;
+    const uint32_t c = n[q], o = pos[q];
+    const size_t src = (size_t)q * stride;
+    for (uint32_t i = lane; i < c; i += 64) {
+        pk[o + i] = k[src + i];
+        ps[o + i] = s[src + i];
+    }
+}
+
+size_t pack_temp_bytes(uint32_t B) {
+    size_t bytes = 0;
+    hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)B + 1);
+    return bytes;
+}
+
+hipError_t launch_pack(const uint32_t* n, const uint32_t* k, const float* s, uint32_t B, uint32_t stride,
+                       uint32_t* pos, uint32_t* pk, float* ps, void* temp, size_t temp_bytes, hipStream_t st) {
+    hipError_t e = hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, n, pos, (int)B + 1, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_pack, dim3((B + 3) / 4), dim3(256), 0, st, n, k, s, B, stride, pos, pk, ps);
+    return hipGetLastError();
+}
+
 size_t general_sort_temp_bytes(uint32_t n_keys) {
     size_t bytes = 0;
     hipcub::DeviceRadixSort::SortKeys(nullptr, bytes, (const uint64_t*)nullptr, (uint64_t*)nullptr,

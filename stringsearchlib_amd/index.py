@@ -23,9 +23,17 @@ class StringIndex:
     """One index of byte strings. gram_size 3 is the reference (indexN); 1 or 2 use the indexG
     extension (every reference threshold scaled by the gram size)."""
 
-    def __init__(self, words, row_size: int = 1, weights=None, device: int | None = None, gram_size: int = 3):
+    def __init__(self, words, row_size: int = 1, weights=None, device: int | None = None, gram_size: int = 3,
+                 devices=None):
+        """devices: a list of HIP devices to place one replica of the index on each (ngsSetDevices;
+        repeats allowed); batches are then split across the replicas."""
         L = _native.lib()
-        if device is not None:
+        if devices is not None:
+            ds = (C.c_int * max(1, len(devices)))(*devices)
+            rc = L.ngsSetDevices(ds, len(devices))
+            if rc:
+                raise RuntimeError(f"ngsSetDevices({list(devices)}) failed: {rc}")
+        elif device is not None:
             rc = L.ngsSetDevice(device)
             if rc:
                 raise RuntimeError(f"ngsSetDevice({device}) failed: {rc}")
@@ -36,6 +44,8 @@ class StringIndex:
         self._keep = self._words(words)  # alive during the build only
         self.handle = self._index(L, self._keep if n else None, n, row_size, w, gram_size)
         self._keep = None
+        if devices is not None:  # the device list applies to this build only
+            L.ngsSetDevices(None, 0)
         if not self.handle:
             raise RuntimeError(f"{self._INDEX} failed (no usable GPU, or gram_size not in 1..3?) — see stderr")
 
@@ -139,6 +149,10 @@ class StringIndex:
             raise IndexError(key_id)
         return self._string(p)
 
+    def replicas(self) -> int:
+        """Devices the index was placed on (ngsReplicaCount)."""
+        return _native.lib().ngsReplicaCount(self.handle)
+
     def gram_size(self) -> int:
         return _native.lib().ngsGramSize(self.handle)
 
@@ -189,8 +203,9 @@ class WideStringIndex(StringIndex):
     _fn = {"search": "searchW", "score": "scoreW", "release": "releaseW", "scoreBatch": "scoreBatchW",
            "key": "ngsKeyW"}
 
-    def __init__(self, words, row_size: int = 1, weights=None, device: int | None = None, gram_size: int = 2):
-        super().__init__(words, row_size, weights, device, gram_size)
+    def __init__(self, words, row_size: int = 1, weights=None, device: int | None = None, gram_size: int = 2,
+                 devices=None):
+        super().__init__(words, row_size, weights, device, gram_size, devices)
 
     @staticmethod
     def _words(words):

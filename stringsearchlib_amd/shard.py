@@ -1,9 +1,15 @@
 """Query-batch sharding across GPUs.
 
 Each rank (one process per GPU) holds a replica of the index and scores a contiguous slice
-of the batch; the only collective is the gather of the compacted top-k records to rank 0
-(RCCL over xGMI with the ``nccl`` backend; ``gloo`` in the CPU tests). Queries share no
-state, so nothing else crosses ranks.
+of the batch; the only collective is the gather of the top-k records to rank 0 (RCCL over
+xGMI with the ``nccl`` backend; ``gloo`` in the CPU tests). Queries share no state, so
+nothing else crosses ranks.
+
+The gather moves one fixed-size buffer per rank, sized from numbers every rank knows
+(the padded per-rank batch and the output stride), so no collective or host read-back is
+needed to agree on sizes and the whole exchange stays asynchronous: ngsSearchDevice writes its
+counts / keys / scores straight into a GatherBuffer's views, the gather runs on RCCL's stream
+beside the next batch, and rank 0 compacts the records after it waits.
 """
 from __future__ import annotations
 
@@ -16,59 +22,91 @@ def shard_bounds(rank: int, world: int, n: int) -> tuple[int, int]:
     return n * rank // world, n * (rank + 1) // world
 
 
+def max_shard(world: int, n: int) -> int:
+    """The largest slice shard_bounds gives any rank (the gather's padded batch)."""
+    return max(hi - lo for lo, hi in (shard_bounds(r, world, n) for r in range(world)))
+
+
 def compact(counts: torch.Tensor, keys: torch.Tensor, scores: torch.Tensor, stride: int):
-    """(counts[B], keys[B*stride], scores[B*stride]) -> counts, packed keys, packed scores."""
+    """(counts[B], keys[B*stride], scores[B*stride]) -> counts, packed keys, packed scores.
+    Boolean-mask indexing reads the packed size back to the host: rank 0 uses it after the gather."""
     B = counts.numel()
     mask = torch.arange(stride, device=counts.device).unsqueeze(0) < counts.view(B, 1).to(torch.int64)
     return counts, keys.view(B, stride)[mask], scores.view(B, stride)[mask]
+
+
+class GatherBuffer:
+    """One rank's fused int32 gather buffer: [batch, counts[pad_b], keys[pad_b*stride],
+    score bits[pad_b*stride]]. ``counts``, ``keys`` and ``scores`` (float32) are views of it in
+    ngsSearchDevice's output layout (query i's records at i*stride)."""
+
+    def __init__(self, batch: int, stride: int, pad_b: int | None = None, device=None):
+        pad_b = batch if pad_b is None else pad_b
+        if batch > pad_b:
+            raise ValueError(f"batch {batch} > padded batch {pad_b}")
+        self.batch, self.stride, self.pad_b = batch, stride, pad_b
+        self.buf = torch.zeros(1 + pad_b * (1 + 2 * stride), dtype=torch.int32, device=device)
+        self.buf[0] = batch
+        ko = 1 + pad_b
+        so = ko + pad_b * stride
+        self.counts = self.buf[1:1 + batch]
+        self.keys = self.buf[ko:ko + batch * stride]
+        self.scores = self.buf[so:so + batch * stride].view(torch.float32)
+
+    def fill(self, counts: torch.Tensor, keys: torch.Tensor, scores: torch.Tensor):
+        """Copies results written elsewhere into the views (device copies, no host sync)."""
+        self.counts.copy_(counts.to(torch.int32))
+        self.keys.copy_(keys.to(torch.int32))
+        self.scores.copy_(scores.to(torch.float32))
+        return self
+
+    @staticmethod
+    def decode(buf: torch.Tensor, stride: int, pad_b: int):
+        """(counts, packed keys, packed scores) of a gathered buffer."""
+        b = int(buf[0])
+        ko = 1 + pad_b
+        so = ko + pad_b * stride
+        return compact(buf[1:1 + b], buf[ko:ko + b * stride], buf[so:so + b * stride].view(torch.float32), stride)
 
 
 class PendingGather:
     """An in-flight gather (``gather_to_root(..., async_op=True)``): ``wait()`` returns what the
     blocking call returns (the per-rank lists on rank 0, None elsewhere)."""
 
-    def __init__(self, work, buf, bufs, o, pad_k, rank):
-        self.work, self.buf, self.bufs, self.o, self.pad_k, self.rank = work, buf, bufs, o, pad_k, rank
+    def __init__(self, work, gb: GatherBuffer, bufs, rank):
+        self.work, self.gb, self.bufs, self.rank = work, gb, bufs, rank
 
     def complete(self):
-        """Orders the current stream after the gather (no host synchronisation, no decode)."""
+        """Orders the current stream after the gather (no host synchronisation, no decode): the
+        buffer may be written again afterwards."""
         self.work.wait()
 
     def wait(self):
         self.work.wait()
         if self.rank != 0:
             return None
-        out = []
-        o, pad_k = self.o, self.pad_k
-        for b in self.bufs:
-            nk, nb = int(b[0]), int(b[1])
-            out.append((b[2:2 + nb], b[o:o + nk], b[o + pad_k:o + pad_k + nk].view(torch.float32)))
-        return out
+        return [GatherBuffer.decode(b, self.gb.stride, self.gb.pad_b) for b in self.bufs]
 
 
-def gather_to_root(counts: torch.Tensor, pkeys: torch.Tensor, pscores: torch.Tensor, group=None,
-                   async_op: bool = False):
-    """Gathers every rank's (counts, packed keys, packed scores) on rank 0.
+def gather_to_root(counts, keys=None, scores=None, stride: int | None = None, group=None, async_op: bool = False,
+                   pad_b: int | None = None):
+    """Gathers every rank's top-k records on rank 0 with one collective.
 
-    Two collectives: an all-reduce of the packed length (so every rank pads to the same
-    size) and one gather of a single fused buffer per rank. Returns the per-rank lists on
-    rank 0 and None elsewhere; with ``async_op`` the gather stays in flight (RCCL runs it on
-    its own stream, beside the next batch's kernels) and a PendingGather is returned."""
-    world = dist.get_world_size(group)
+    ``counts`` is a GatherBuffer that ngsSearchDevice wrote into, or the (counts, keys, scores)
+    tensors of its output layout with their ``stride`` (they are copied into a new buffer).
+    Every rank must use the same ``pad_b`` and stride. Returns the per-rank (counts, packed keys,
+    packed scores) on rank 0 and None elsewhere; with ``async_op`` the gather stays in flight
+    (RCCL runs it on its own stream, beside the next batch's kernels) and a PendingGather is
+    returned."""
+    if isinstance(counts, GatherBuffer):
+        gb = counts
+    else:
+        if stride is None:
+            raise ValueError("stride is required with tensor arguments")
+        gb = GatherBuffer(counts.numel(), stride, pad_b, counts.device).fill(counts, keys, scores)
     rank = dist.get_rank(group)
-    dev = counts.device
-    n = torch.tensor([pkeys.numel(), counts.numel()], dtype=torch.int64, device=dev)
-    mx = n.clone()
-    dist.all_reduce(mx, op=dist.ReduceOp.MAX, group=group)
-    pad_k, pad_b = int(mx[0]), int(mx[1])
-    buf = torch.zeros(2 + pad_b + 2 * pad_k, dtype=torch.int32, device=dev)
-    buf[0] = n[0].to(torch.int32)
-    buf[1] = n[1].to(torch.int32)
-    buf[2:2 + counts.numel()] = counts.to(torch.int32)
-    o = 2 + pad_b
-    buf[o:o + pkeys.numel()] = pkeys.to(torch.int32)
-    buf[o + pad_k:o + pad_k + pscores.numel()] = pscores.contiguous().view(torch.int32)
-    bufs = [torch.empty_like(buf) for _ in range(world)] if rank == 0 else None
-    work = dist.gather(buf, bufs, dst=0, group=group, async_op=True)
-    pending = PendingGather(work, buf, bufs, o, pad_k, rank)
+    world = dist.get_world_size(group)
+    bufs = [torch.empty_like(gb.buf) for _ in range(world)] if rank == 0 else None
+    work = dist.gather(gb.buf, bufs, dst=0, group=group, async_op=True)
+    pending = PendingGather(work, gb, bufs, rank)
     return pending if async_op else pending.wait()

@@ -46,14 +46,20 @@ def _worker(rank, world, port, result_path):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         words, wts, rng = synth.gen_corpus(3000, seed=7)
-        queries = synth.gen_queries(words, 1, 64, rng)
+        queries = synth.gen_queries(words, 1, 65, rng)  # ragged: 33 + 32
         oi = OracleIndex(words, 1, wts)
         lo, hi = shard.shard_bounds(rank, world, len(queries))
         stride = LIMIT
-        c, k, s = shard.compact(*_device_layout(oi, queries[lo:hi], stride), stride)
-        got = shard.gather_to_root(c, k, s)
-        # the in-flight form bench.py uses: same buffers once waited for
-        got_async = shard.gather_to_root(c, k, s, async_op=True).wait()
+        pad_b = shard.max_shard(world, len(queries))
+        c, k, s = _device_layout(oi, queries[lo:hi], stride)
+        got = shard.gather_to_root(c, k, s, stride, pad_b=pad_b)
+        # the in-flight form bench.py uses: results written into a GatherBuffer's views (as
+        # ngsSearchDevice does), gathered without any size exchange, decoded after wait()
+        gb = shard.GatherBuffer(hi - lo, stride, pad_b)
+        gb.counts.copy_(c)
+        gb.keys.copy_(k)
+        gb.scores.copy_(s)
+        got_async = shard.gather_to_root(gb, async_op=True).wait()
         if rank == 0:
             assert all(torch.equal(a, b) for x, y in zip(got, got_async) for a, b in zip(x, y))
         else:
@@ -82,6 +88,17 @@ def test_two_rank_gather_matches_single_batch(tmp_path):
     out = tmp_path / "result.txt"
     mp.spawn(_worker, args=(2, _free_port(), str(out)), nprocs=2, join=True)
     assert out.read_text() == "ok"
+
+
+def test_gather_buffer_layout():
+    gb = shard.GatherBuffer(3, 4, pad_b=5)
+    gb.counts.copy_(torch.tensor([2, 0, 4], dtype=torch.int32))
+    gb.keys.copy_(torch.arange(12, dtype=torch.int32))
+    gb.scores.copy_(torch.arange(12, dtype=torch.float32) / 2)
+    c, k, s = shard.GatherBuffer.decode(gb.buf, 4, 5)
+    assert c.tolist() == [2, 0, 4] and k.tolist() == [0, 1, 8, 9, 10, 11]
+    assert s.tolist() == [0.0, 0.5, 4.0, 4.5, 5.0, 5.5]
+    assert shard.max_shard(8, 65541) == 8193 and shard.max_shard(2, 64) == 32
 
 
 def test_shard_bounds_cover_batch():
