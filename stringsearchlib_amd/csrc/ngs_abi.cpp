@@ -34,6 +34,7 @@ constexpr size_t kOutBudget = size_t(1) << 30;       // bytes of (key, score) ou
 constexpr size_t kGeneralBudget = size_t(2) << 30;   // bytes of dense general-path state
 constexpr uint32_t kSmallBatch = 16;                 // host batches up to this many queries take the latency path
 constexpr size_t kSmallBlock = size_t(1) << 20;      // ... if their output block is at most this many bytes
+constexpr size_t kPartBudget = size_t(1) << 30;      // bytes of sliced tier-1b partial results per call
 
 bool hip_ok(hipError_t e, const char* what) {
     if (e == hipSuccess) return true;
@@ -102,6 +103,9 @@ struct Context {
     uint32_t* d_esn = nullptr;     // tier 1a survivor lists for k_emit: count per query,
     uint32_t* d_est = nullptr;     // kEmitCap terms and
     uint8_t* d_esc = nullptr;      // kEmitCap hit counts per query
+    uint64_t* d_prec = nullptr;    // sliced tier 1b: top-L records per (query, slice)
+    uint32_t* d_pcnt = nullptr;    // ... and their counts
+    size_t pcap = 0, pncap = 0;    // records d_prec holds, counts d_pcnt holds
     uint32_t* d_group = nullptr;
     // kStatSlots slots, then one holding d_gcount (one memset, one read-back), then the
     // 2 * kListSlots counter lines of k_prep's slot lists (d_lctr; same memset, not read back)
@@ -126,7 +130,7 @@ struct Context {
     ~Context() {
         hipSetDevice(device);
         for (void* p : {(void*)d_raw, (void*)d_off, (void*)d_norm, (void*)d_qm, (void*)d_glist, (void*)d_list2, (void*)d_fb, (void*)d_fb2, (void*)d_heavy, (void*)d_full, (void*)d_lslots,
-                        (void*)d_esn, (void*)d_est, (void*)d_esc,
+                        (void*)d_esn, (void*)d_est, (void*)d_esc, (void*)d_prec, (void*)d_pcnt,
                         (void*)d_group, (void*)d_stats, (void*)d_out, (void*)d_pos, (void*)d_pk, (void*)d_ps, d_ptemp, (void*)gen.cnt,
                         (void*)gen.kenc, (void*)gen.list, (void*)gen.sorted, (void*)gen.lcount, gen.temp})
             if (p) hipFree(p);
@@ -214,6 +218,8 @@ struct Library {
     std::atomic<bool> timing{false};
     std::mutex stats_mu;
     ngs_stats last{};
+    bool tk_identity = false;  // DevIndex.tk_identity / w_max, computed once for every replica
+    float w_max = 0.0f;
 
     ~Library() { reps.clear(); }
     // the replica on `dev`, else the first
@@ -243,6 +249,8 @@ bool upload_replica(Library& L, Replica& R, bool keys_unique) {
     X.n_short = H.n_short;
     X.n_keys = H.n_keys;
     X.keys_unique = keys_unique ? 1u : 0u;
+    X.tk_identity = L.tk_identity ? 1u : 0u;
+    X.w_max = L.w_max;
     const std::vector<char>& kb = H.key_bytes;
     uint64_t *gram_off, *term_off, *key_off;
     uint32_t *post, *tk_off, *wild_key, *gram_row, *skip;
@@ -348,6 +356,15 @@ bool upload(Library& L, const std::vector<int>& devs) {
             seen[kw.x] = 1;
         }
     }
+    // term -> pairs shape and the largest weight (term_pairs in ngs_kernels.hip)
+    L.tk_identity = H.tk_off.size() == (size_t)H.n_terms + 1;
+    for (size_t t = 0; L.tk_identity && t < H.tk_off.size(); ++t) L.tk_identity = H.tk_off[t] == t;
+    L.w_max = 0.0f;
+    for (const uint2& kw : H.tk) {
+        float w;
+        std::memcpy(&w, &kw.y, sizeof w);
+        if (w > L.w_max) L.w_max = w;  // NaN weights score +0 (pair_enc) and never raise the bound
+    }
     for (int d : devs) {
         L.reps.push_back(std::make_unique<Replica>());
         L.reps.back()->device = d;
@@ -379,6 +396,36 @@ bool ensure_queries(Context& c, size_t B, size_t bytes) {
         c.qcap = nb;
     }
     return true;
+}
+
+// Sliced tier 1b's partial results: B * slices * limit records. Within kPartBudget bytes, else the
+// call runs tier 1b unsliced (returns the slice count to use).
+uint32_t ensure_parts(Context& c, size_t B, uint32_t limit) {
+    static const uint32_t slices = [] {
+        const char* e = std::getenv("NGS_SLICES");
+        const uint32_t v = e ? (uint32_t)std::strtoul(e, nullptr, 0) : kSlices;
+        return std::max<uint32_t>(1, std::min<uint32_t>(v, 16));
+    }();
+    if (slices <= 1 || limit > kWaveMaxLimit) return 1;
+    const size_t need = B * slices * limit;
+    if (need * sizeof(uint64_t) > kPartBudget) return 1;
+    if (need > c.pcap) {
+        if (c.d_prec) hipFree(c.d_prec);
+        c.d_prec = nullptr;
+        c.pcap = 0;
+        const size_t nb = std::max<size_t>(need, 1 << 16);
+        if (!dev_alloc(&c.d_prec, nb)) return 1;
+        c.pcap = nb;
+    }
+    if (B * slices > c.pncap) {
+        if (c.d_pcnt) hipFree(c.d_pcnt);
+        c.d_pcnt = nullptr;
+        c.pncap = 0;
+        const size_t nb = std::max<size_t>(B * slices, 4096);
+        if (!dev_alloc(&c.d_pcnt, nb)) return 1;
+        c.pncap = nb;
+    }
+    return slices;
 }
 
 bool ensure_outputs(Context& c, size_t B, size_t stride) {
@@ -469,6 +516,9 @@ int queue_search(Library& L, Replica& R, Context& c, const uint8_t* d_raw, const
     P.esn = c.d_esn;
     P.est = c.d_est;
     P.esc = c.d_esc;
+    P.nslices = small ? 1u : ensure_parts(c, B, P.limit);
+    P.prec = c.d_prec;
+    P.pcnt = c.d_pcnt;
     const bool timing = L.timing.load();
     // statistics, path counts and list counters
     if (!HIP_CHECK(hipMemsetAsync(c.d_stats, 0, sizeof(DevStats) * (kStatSlots + 1 + 2 * kListSlots), s))) return -4;
@@ -592,7 +642,9 @@ bool host_search_one(Library& L, Replica& R, const CharT* const* queries, uint32
     std::unique_ptr<Context> c = R.acquire();
     if (!c) return false;
     const size_t stride = Lm;
-    const size_t max_chunk = std::max<size_t>(1, std::min<size_t>(1 << 20, kOutBudget / (stride * 8)));
+    size_t max_chunk = std::max<size_t>(1, std::min<size_t>(1 << 20, kOutBudget / (stride * 8)));
+    if (Lm <= kWaveMaxLimit)  // sliced tier 1b's partial results fit the budget
+        max_chunk = std::max<size_t>(1, std::min<size_t>(max_chunk, kPartBudget / (sizeof(uint64_t) * kSlices * Lm)));
     bool ok = true;
     for (uint32_t q0 = 0; q0 < nq && ok; q0 += (uint32_t)max_chunk) {
         const uint32_t B = (uint32_t)std::min<size_t>(max_chunk, nq - q0);

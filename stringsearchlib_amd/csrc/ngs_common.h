@@ -182,6 +182,8 @@ struct DevIndex {  // passed by value to kernels; all pointers are device pointe
     uint32_t n_terms, n_short, n_keys;
     uint32_t keys_unique;       // 1: every key has one (term, key) pair, so a query's records never
                                 // share a key and the top-L needs no key dedup pass
+    uint32_t tk_identity;       // 1: term t's pairs are exactly tk[t] (tk_off[t] == t): one load less
+    float w_max;                // largest pair weight (<= 0: none positive); bounds a term's best score
     // gram size and character width (indexG / indexW extensions; 3 and 1 for indexN)
     uint32_t gsz, csize, gram_mode;         // gram_mode 1: grams via the dictionary below
     uint32_t short_query_len, full_scan_len; // 3g and g (nGramSearch.hpp:381, :247)
@@ -208,7 +210,24 @@ struct SearchParams {
     uint32_t* esn;
     uint32_t* est;
     uint8_t* esc;
+    // sliced tier 1b (kSlices): the full list and the hand-over lists run as nslices term-id
+    // slices of each query (one wave each, bucket ranges of the skip table); slice j of query q
+    // leaves its top-L records at prec[(q * nslices + j) * limit] and their count at
+    // pcnt[q * nslices + j], merged by k_merge. nslices 1: unsliced
+    uint32_t nslices;
+    uint64_t* prec;
+    uint32_t* pcnt;
 };
+
+// Tier 1b slices per query (SearchParams.nslices): a full-list or handed-over query is a few
+// hundred to thousands of survivors in one wave; four waves on disjoint term-id ranges each keep
+// their own top-L, and k_merge joins them. The key-max merge is exact: a key among the global
+// top L is among the top L of the slice holding its best record.
+#ifndef NGS_SLICES
+#define NGS_SLICES 4
+#endif
+constexpr uint32_t kSlices = NGS_SLICES;
+constexpr uint32_t kNoPart = 0xFFFFFFFFu;  // pcnt[q * nslices]: the query was answered unsliced
 
 // per-query normalised length sentinels written by the prep kernel
 constexpr uint32_t kQueryWildcard = 0xFFFFFFFFu;

@@ -183,6 +183,30 @@ __device__ __forceinline__ uint32_t pair_enc(uint2 kw, float s, bool promo_possi
     return enc;
 }
 
+// The (key, weight) pairs [p, pe) of survivor term t (calcScore, nGramSearch.hpp:318-336), or none
+// when not even the index's largest weight lifts the term's score s into the running top-L: every
+// pair scores max(w * s, 0) <= max(w_max * s, 0) in fp32, and a record enters only below tau. (An
+// exact match, promoted to 100, is never pruned.) At threshold 0 most survivors share one gram
+// with the query and are dropped here without a load.
+__device__ __forceinline__ void term_pairs(const DevIndex& X, uint32_t t, float s, bool promo, uint64_t tau,
+                                           uint32_t& p, uint32_t& pe) {
+    if (!promo && tau != kNoCand) {
+        const float ub = X.w_max * s;
+        const uint32_t ub_enc = ub > 0.0f ? __float_as_uint(ub) + 1u : 1u;
+        if (ub_enc < ~(uint32_t)(tau >> 32)) {
+            p = pe = 0;
+            return;
+        }
+    }
+    if (X.tk_identity) {
+        p = t;
+        pe = t + 1;
+    } else {
+        p = X.tk_off[t];
+        pe = X.tk_off[t + 1];
+    }
+}
+
 // stringMatch (nGramSearch.hpp:182-222): min over source substrings of the edit distance to
 // q (m <= 8); returns m - distance. Column DP over the query held in registers.
 template <typename TT>
@@ -464,10 +488,9 @@ __device__ void long_part(FastSmem& S, const DevIndex& X, const SearchParams& P,
         const float s = (float)(v & 255u) / fn;  // nGramSearch.hpp:300
         if (s < P.thr) return 2;                 // nGramSearch.hpp:315
         ++surv;
-        st.p = X.tk_off[t];
-        st.pe = X.tk_off[t + 1];
         st.s = s;
         st.promo = (double)s > 0.999;            // nGramSearch.hpp:328
+        term_pairs(X, t, s, st.promo, S.tau, st.p, st.pe);
         return 1;
     });
     STAMP(8);
@@ -538,10 +561,9 @@ __device__ void fast_one(const uint32_t q, FastSmem& S, const DevIndex& X, const
             t += kFastThreads;
             if (s < P.thr) return 2;  // nGramSearch.hpp:315
             ++surv;
-            st.p = X.tk_off[id];
-            st.pe = X.tk_off[id + 1];
             st.s = s;
             st.promo = (double)s > 0.999;
+            term_pairs(X, id, s, st.promo, S.tau, st.p, st.pe);
             return 1;
         });
     }
@@ -905,16 +927,15 @@ __device__ void wave_emit(SM& S, const DevIndex& X, const SearchParams& P, uint3
     wave_sync();
     for (uint32_t base = 0; base < surv_n; base += 64) {
         const uint32_t i = base + lane;
-        uint32_t p = 0, pe = 0, code = 0;
+        uint32_t p = 0, pe = 0, code = 0, t = 0;
         if (i < surv_n) {
-            const uint32_t t = S.surv_t[i];
+            t = S.surv_t[i];
             code = S.surv_c[i];
-            p = X.tk_off[t];
-            pe = X.tk_off[t + 1];
         }
         const float s_l = __shfl(sc_long, (int)(code & 63u)), s_s = __shfl(sc_short, (int)(code & 63u));
         const float s = (code & 0x80u) ? s_s : s_l;
         const bool promo = (double)s > 0.999;  // nGramSearch.hpp:328
+        if (i < surv_n) term_pairs(X, t, s, promo, tau, p, pe);
         while (__ballot(p < pe)) {
             uint64_t rec = kNoCand;
             if (p < pe) {
@@ -1113,7 +1134,10 @@ __device__ __forceinline__ void part_exact(WaveSmem<W, LEAN>& S, uint4 (&v)[kDma
             uint64_t ta2 = W == 1 ? tau : S.x_tau;
             // one element slot per step (a single wave_emit call site keeps the registers out of scratch)
             for (uint32_t k = 0; k < 4 * (uint32_t)kDmaRounds && 64 * (k >> 2) < mt; ++k) {
-                if (sn + 64 > (uint32_t)kWaveSurv) wave_emit(S, X, P, m, L, sc_long, sc_short, sn, cn, ta2);
+                if (sn + 64 > (uint32_t)kWaveSurv) {
+                    if (P.dbg & 64u) sn = 0;  // dbg 64 (ablation): survivors dropped, no calcScore
+                    else wave_emit(S, X, P, m, L, sc_long, sc_short, sn, cn, ta2);
+                }
                 uint32_t x = kStray;
                 if (k < 16) {  // 16-way selects (k is uniform)
 #pragma unroll
@@ -1280,8 +1304,21 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
                                            uint32_t* __restrict__ out_k, float* __restrict__ out_s,
                                            uint32_t* __restrict__ list2, uint32_t* __restrict__ count2,
                                            DevStats* __restrict__ stats, uint32_t* __restrict__ fb,
-                                           uint32_t* __restrict__ fbc) {
+                                           uint32_t* __restrict__ fbc, const uint32_t slice = 0,
+                                           const uint32_t nsl = 1) {
     const uint32_t lane = lane_id(), tid = threadIdx.x;
+    // sliced tier 1b: this wave takes the term ids of skip-table buckets [K * slice / nsl,
+    // K * (slice + 1) / nsl) and leaves its top-L records for k_merge (SearchParams.prec)
+    const bool sliced = !LEAN && W == 1 && nsl > 1;
+    if (sliced) {  // queries answered without the long search: slice 0 answers, k_merge skips them
+        const uint32_t m0 = qm[q];
+        const bool direct = m0 == kQueryWildcard || m0 == 0 || m0 <= X.full_scan_len ||
+                            m0 - X.gsz + 1 > kWaveMaxGrams || P.limit > kWaveMaxLimit;
+        if (direct) {
+            if (slice != 0) return;
+            if (tid == 0) P.pcnt[(size_t)q * nsl] = kNoPart;
+        }
+    }
     // tier 1a hands the query over (all lanes leave together; nothing of it was written yet)
     auto bail = [&]() {
         if (lane == 0) fb[atomicAdd(fbc, 1u)] = q;
@@ -1356,7 +1393,7 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
     // ---- searchShort over shortLib (nGramSearch.hpp:262-270), 4 <= m < 9, wave 0 ----
     if constexpr (LEAN) {
         if (m < X.short_query_len && X.n_short) { bail(); return; }
-    } else if (wid == 0 && m < X.short_query_len && X.n_short) {
+    } else if (wid == 0 && slice == 0 && m < X.short_query_len && X.n_short) {
         uint32_t qc[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) qc[i] = (uint32_t)i < m ? S.q[i] : 0;
@@ -1404,6 +1441,7 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
         grow = lane < ng ? r2 : 0;
     }
     const uint64_t p_total = wave_sum((uint64_t)glen);
+    uint64_t p_stat = p_total;  // postings this wave reads (its slice's)
     // sketch counting for 2 <= cmin <= 15; at cmin 2 two colliding entries already make a false
     // candidate, so those parts are cut at half the size
     const bool sketch = cmin >= kSketchMinCmin && cmin <= kSketchMax;
@@ -1424,11 +1462,18 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
         // end of the next bucket part: skip[row][min(K, bn + w)]; idle lanes load nothing (a shared
         // row would be a hot spot). (Preloading every boundary of the query into LDS was measured
         // slower: the LDS it takes costs occupancy.)
-        auto next_end = [&](uint32_t bn) -> uint32_t { return sk[min(K, bn + w)]; };
+        // this wave's buckets [b_lo, b_hi): all of them unless sliced
+        const uint32_t b_lo = sliced ? (uint32_t)((uint64_t)K * slice / nsl) : 0u;
+        const uint32_t b_hi = sliced ? (uint32_t)((uint64_t)K * (slice + 1) / nsl) : K;
+        auto next_end = [&](uint32_t bn) -> uint32_t { return sk[min(b_hi, bn + w)]; };
         // part iterator: buckets [bnext, bnext + w) unless they exceed kChunks, then term-id sub-parts
-        uint32_t cur = 0, bnext = 0;
+        uint32_t cur = 0, bnext = b_lo;
+        if (sliced) {
+            cur = lane < ng ? sk[b_lo] : 0u;
+            p_stat = wave_sum((uint64_t)(lane < ng ? sk[b_hi] - cur : 0u));
+        }
         uint32_t e_pre = 0;
-        if (lane < ng) e_pre = next_end(0);
+        if (lane < ng) e_pre = next_end(b_lo);
         uint32_t in_sub = 0;
         uint32_t sub_lo = 0, hi_lim = 0, sub_end = 0, sub_bnext = 0, step = 1;
         // software pipeline in registers: part i+1's loads are in flight while part i is counted
@@ -1462,13 +1507,13 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
             // common case, straight-line: the next group of w buckets is non-empty and fits
             // (span * w <= kMaxPartSpan holds by the choice of w)
             bool fast = false;
-            if (!in_sub && bnext < K) {
+            if (!in_sub && bnext < b_hi) {
                 const uint32_t e = lane < ng ? e_pre : cur;
                 const uint32_t tot = wave_sum_u32(chunks(cur, e));
                 if (tot && tot <= kChunks) {
                     lo = bnext * span;
                     len = e - cur;
-                    bnext = min(K, bnext + w);
+                    bnext = min(b_hi, bnext + w);
                     hi_t = (uint32_t)min64((uint64_t)bnext * span, n_long);
                     if (lane < ng) e_pre = next_end(bnext);
                     have_p = true;
@@ -1486,8 +1531,8 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
                     break;
                 }
                 if (!in_sub) {
-                    if (bnext >= K) break;
-                    const uint32_t bhi = min(K, bnext + w), e = lane < ng ? e_pre : cur;
+                    if (bnext >= b_hi) break;
+                    const uint32_t bhi = min(b_hi, bnext + w), e = lane < ng ? e_pre : cur;
                     const uint32_t tot = wave_sum_u32(chunks(cur, e));
                     if (tot <= kChunks) {
                         lo = bnext * span;
@@ -1624,6 +1669,23 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
     WSTAMP(8);
     wave_flush(S, cand_n, tau, L, X.keys_unique != 0);
     WSTAMP(9);
+    if (sliced) {  // this slice's top-L records, in order, for k_merge
+        uint64_t* pr = P.prec + ((size_t)q * nsl + slice) * L;
+        for (uint32_t i = lane; i < cand_n; i += 64) pr[i] = S.cand()[i];
+        if (lane == 0) {
+            P.pcnt[(size_t)q * nsl + slice] = cand_n;
+            if (!(P.dbg & 32u)) {
+                DevStats* sl = stats + (q & (kStatSlots - 1));
+                atomicAdd(&sl->postings, (unsigned long long)p_stat);
+                atomicAdd(&sl->survivors, (unsigned long long)S.surv_total);
+                if (slice == 0) {
+                    atomicAdd(&sl->lists, (unsigned long long)ng);
+                    atomicAdd(&sl->fast, 1ull);
+                }
+            }
+        }
+        return;
+    }
     for (uint32_t i = lane; i < cand_n; i += 64) {
         const uint64_t r = S.cand()[i];
         const uint32_t enc = ~(uint32_t)(r >> 32);
@@ -1976,12 +2038,16 @@ __global__ __launch_bounds__(64 * W, kWaveWavesPerSimd) void k_wave(DevIndex X, 
         return;
     }
     const uint32_t cnt = *qcount;
-    for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
+    const uint32_t nsl = W == 1 && P.nslices > 1 ? P.nslices : 1u;  // sliced: k_merge follows
+    for (uint32_t t = blockIdx.x; t < cnt * nsl; t += gridDim.x) {
+        const uint32_t i = t / nsl;
         wave_query<W, false>(S, qlist[i], X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats,
-                             nullptr, nullptr);
+                             nullptr, nullptr, t - i * nsl, nsl);
         __syncthreads();
     }
 }
+
+
 
 // Tier 1a: the lean wave kernel over every query (qlist == nullptr), or over the heavy list.
 // DEFER: survivors spill to HBM for k_emit (the heavy launch always; the main one if kDeferEmit).
@@ -2055,13 +2121,10 @@ __device__ __forceinline__ void emit_query(EmitSmem& S, const uint32_t q, const 
             code = i < sn ? ec[i] : 0u;
         }
         uint32_t p = 0, pe = 0;
-        if (i < sn) {
-            p = X.tk_off[t];
-            pe = X.tk_off[t + 1];
-        }
         const float s_l = __shfl(sc_long, (int)(code & 63u)), s_s = __shfl(sc_short, (int)(code & 63u));
         const float s = (code & 0x80u) ? s_s : s_l;
         const bool promo = (double)s > 0.999;  // nGramSearch.hpp:328
+        if (i < sn) term_pairs(X, t, s, promo, tau, p, pe);
         while (__ballot(p < pe)) {
             uint64_t rec = kNoCand;
             if (p < pe) {
@@ -2108,6 +2171,49 @@ __global__ __launch_bounds__(64 * kEmitWaves) void k_emit(DevIndex X, SearchPara
     const uint32_t cnt = *qcount;
     for (uint32_t j = j0; j < cnt; j += gridDim.x * kEmitWaves) {
         emit_query(S, qlist[j], true, X, P, qnorm, qoff, qm, out_n, out_k, out_s, stats);
+        wave_sync();
+    }
+}
+
+// Joins the slices of sliced tier 1b (SearchParams.prec / pcnt): per query of the list, the
+// slices' top-L records through the running top-L (key-max dedup, tau pruning), then results.
+__global__ __launch_bounds__(64) void k_merge(DevIndex X, SearchParams P, const uint32_t* __restrict__ qlist,
+                                              const uint32_t* __restrict__ qcount, uint32_t* __restrict__ out_n,
+                                              uint32_t* __restrict__ out_k, float* __restrict__ out_s,
+                                              DevStats* __restrict__ stats) {
+    __shared__ EmitSmem S;
+    const uint32_t lane = lane_id(), nsl = P.nslices, L = P.limit;
+    const uint32_t cnt = *qcount;
+    for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
+        const uint32_t q = qlist[i];
+        const uint32_t* pc = P.pcnt + (size_t)q * nsl;
+        if (pc[0] == kNoPart) continue;  // answered by slice 0 directly
+        uint32_t cand_n = 0;
+        uint64_t tau = kNoCand;
+        for (uint32_t j = 0; j < nsl; ++j) {
+            const uint32_t nj = pc[j];
+            const uint64_t* pr = P.prec + ((size_t)q * nsl + j) * L;
+            for (uint32_t b = 0; b < nj; b += 64) {
+                const uint64_t rec = b + lane < nj ? pr[b + lane] : kNoCand;
+                if (cand_n + 64 > (uint32_t)kWaveCand) wave_flush(S, cand_n, tau, L, X.keys_unique != 0);
+                const bool want = rec < tau;
+                const unsigned long long bw = __ballot(want);
+                if (want) S.cand()[cand_n + rank_below(bw)] = rec;
+                cand_n += __popcll(bw);
+            }
+        }
+        wave_flush(S, cand_n, tau, L, X.keys_unique != 0);
+        const size_t ob = (size_t)q * P.out_stride;
+        for (uint32_t k = lane; k < cand_n; k += 64) {
+            const uint64_t r = S.cand()[k];
+            const uint32_t enc = ~(uint32_t)(r >> 32);
+            out_k[ob + k] = (uint32_t)r;
+            out_s[ob + k] = enc == kPromoted ? 100.0f : __uint_as_float(enc - 1u);
+        }
+        if (lane == 0) {
+            out_n[q] = cand_n;
+            if (!(P.dbg & 32u)) atomicAdd(&stats[q & (kStatSlots - 1)].results, (unsigned long long)cand_n);
+        }
         wave_sync();
     }
 }
@@ -2308,6 +2414,8 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
             // beside tier 1a: the heavy list through the lean kernel, k_emit and tier 1b on its
             // hand-overs (side), and the full list through tier 1b (side2)
             const uint32_t g1b = std::min<uint32_t>(P.n_queries, 4096);  // grid-stride over the list
+            // sliced tier-1b launches: a wave per (query, slice)
+            const uint32_t g1s = std::min<uint32_t>(P.n_queries * std::max<uint32_t>(P.nslices, 1u), 16384);
             const uint32_t gh = std::min<uint32_t>(P.n_queries, P.heavy_grid ? P.heavy_grid : 4096);
             // (esn[] was reset by k_prep)
             auto main_lean = [&]() {
@@ -2327,9 +2435,14 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
             else if (P.heavy_waves == 2)
                 hipLaunchKernelGGL(k_wave<2>, dim3(gh), dim3(128), 0, side2, X, P, qnorm, off, qm, out_n, out_k,
                                    out_s, list2, count2, stats, full, fcount);
-            else
-                hipLaunchKernelGGL(k_wave<1>, dim3(gh), dim3(64), 0, side2, X, P, qnorm, off, qm, out_n, out_k,
-                                   out_s, list2, count2, stats, full, fcount);
+            else {
+                // unsliced: its cmin-1 parts are all counted exactly, and four slices of a C2 query
+                // measured 17 % slower than one wave (the hand-over lists below gain from slicing)
+                SearchParams PF = P;
+                PF.nslices = 1;
+                hipLaunchKernelGGL(k_wave<1>, dim3(gh), dim3(64), 0, side2, X, PF, qnorm, off, qm, out_n, out_k, out_s,
+                                   list2, count2, stats, full, fcount);
+            }
             if ((e = hipEventRecord(join2, side2)) != hipSuccess) return e;
             if (kHeavyLean) {
                 SearchParams PH = P;
@@ -2338,8 +2451,11 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
                                    out_k, out_s, list2, count2, stats, fb2, fbc2, heavy, hcount);
                 hipLaunchKernelGGL(k_emit, dim3((gh + kEmitWaves - 1) / kEmitWaves), dim3(64 * kEmitWaves), 0, side,
                                    X, PH, qnorm, off, qm, out_n, out_k, out_s, stats, heavy, hcount);
-                hipLaunchKernelGGL(k_wave<1>, dim3(g1b), dim3(64), 0, side, X, P, qnorm, off, qm, out_n, out_k,
+                hipLaunchKernelGGL(k_wave<1>, dim3(g1s), dim3(64), 0, side, X, P, qnorm, off, qm, out_n, out_k,
                                    out_s, list2, count2, stats, (const uint32_t*)fb2, (const uint32_t*)fbc2);
+                if (P.nslices > 1)
+                    hipLaunchKernelGGL(k_merge, dim3(g1b), dim3(64), 0, side, X, P, (const uint32_t*)fb2,
+                                       (const uint32_t*)fbc2, out_n, out_k, out_s, stats);
             }
             if ((e = hipEventRecord(join, side)) != hipSuccess) return e;
             if (!kMainFirst) main_lean();
@@ -2348,8 +2464,11 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
                                    s, X, P, qnorm, off, qm, out_n, out_k, out_s, stats, (const uint32_t*)nullptr,
                                    (const uint32_t*)nullptr);
             // tier 1b over the queries tier 1a handed over
-            hipLaunchKernelGGL(k_wave<1>, dim3(g1b), dim3(64), 0, s, X, P, qnorm, off, qm, out_n, out_k, out_s,
+            hipLaunchKernelGGL(k_wave<1>, dim3(g1s), dim3(64), 0, s, X, P, qnorm, off, qm, out_n, out_k, out_s,
                                list2, count2, stats, (const uint32_t*)fb, (const uint32_t*)fbc);
+            if (P.nslices > 1)
+                hipLaunchKernelGGL(k_merge, dim3(g1b), dim3(64), 0, s, X, P, (const uint32_t*)fb, (const uint32_t*)fbc,
+                                   out_n, out_k, out_s, stats);
             if ((e = hipStreamWaitEvent(s, join, 0)) != hipSuccess || (e = hipStreamWaitEvent(s, join2, 0)) != hipSuccess)
                 return e;
             break;
