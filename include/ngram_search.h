@@ -175,10 +175,12 @@ typedef struct {
 NGS_API int ngsSetTiming(uint32_t handle, int enable);
 NGS_API int ngsLastStats(uint32_t handle, ngs_stats* out);
 
-/* Test support: digests of the gram CSR as the kernels read it, for comparing the GPU index
- * build (default for indexN) with the host build (environment NGS_HOST_GRAMS=1 at build time).
- * out[0..7] = postings, lists, skip buckets, FNV-1a of gram_off, post, gram_row, skip, bucket
- * span. Returns 8, -1 (bad handle), -3 (dictionary index), -4 (HIP error). */
+/* Test support: digests of the index as the kernels read it, for comparing the GPU index build
+ * (default) with the host build (environment NGS_HOST_GRAMS=1 / NGS_HOST_INTERN=1 at build time).
+ * out[0..7] = postings, lists, skip buckets, FNV-1a of gram_off, post, gram_row, skip, bucket span
+ * (zeros for dictionary indexes: gram sizes other than narrow 3); out[8..15] = FNV-1a of term_off,
+ * term_bytes, tk_off, tk, key_off, key_bytes, wildcard keys, wildcard scores. Returns min(n, 16),
+ * -1 (bad handle), -4 (HIP error). */
 NGS_API int ngsIndexDigest(uint32_t handle, uint64_t* out, int n);
 
 /* Library build identification: "ngram_search <version> gfx950 src=<hash>", where <hash> is the

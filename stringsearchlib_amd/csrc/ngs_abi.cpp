@@ -836,13 +836,14 @@ uint32_t new_library(Build&& build) {
     if (handle == maxVal) return 0;
     auto L = std::make_unique<Library>();
     set_valid(*L, kDefaultValid, (int)std::strlen(kDefaultValid));
-    build(L->host);
     std::vector<int> devs = t_devices;
     if (devs.empty()) {
         int dev = 0;
         if (hipGetDevice(&dev) != hipSuccess) dev = 0;
         devs.push_back(dev);
     }
+    (void)hipSetDevice(devs.front());  // the build's device kernels run on the first replica's device
+    build(L->host);
     if (L->host.indexed && !upload(*L, devs)) {
         std::fprintf(stderr, "ngram_search: indexN could not place the index on a GPU\n");
         return 0;
@@ -1088,20 +1089,39 @@ NGS_API int ngsIndexDigest(uint32_t handle, uint64_t* out, int n) {
         for (uint8_t c : v) h = (h ^ c) * 1099511628211ull;
         return true;
     };
-    uint64_t n_post = 0;
-    const size_t nspace = X.gram_mode == 0 ? kGramSpace : 0;
-    if (X.gram_mode != 0) return -3;  // dictionary indexes: host-built only
-    if (!HIP_CHECK(hipMemcpy(&n_post, X.gram_off + nspace, sizeof(uint64_t), hipMemcpyDeviceToHost))) return -4;
-    const size_t rows = L.host.n_grams;
-    const size_t sizes[4] = {sizeof(uint64_t) * (nspace + 1), sizeof(uint32_t) * n_post, sizeof(uint32_t) * nspace,
-                             sizeof(uint32_t) * rows * (X.n_buckets + 1)};
-    const void* ptrs[4] = {X.gram_off, X.post, X.gram_row, X.skip};
-    uint64_t vals[11] = {n_post, rows, X.n_buckets};
-    for (int i = 0; i < 4; ++i)
-        if (!digest(ptrs[i], sizes[i], vals[3 + i])) return -4;
-    vals[7] = X.bucket_span;
-    for (int i = 0; i < n && i < 8; ++i) out[i] = vals[i];
-    return 8;
+    uint64_t vals[16] = {};
+    if (X.gram_mode == 0) {  // the direct-indexed gram CSR (dictionary indexes: zeros)
+        uint64_t n_post = 0;
+        const size_t nspace = kGramSpace;
+        if (!HIP_CHECK(hipMemcpy(&n_post, X.gram_off + nspace, sizeof(uint64_t), hipMemcpyDeviceToHost))) return -4;
+        const size_t rows = L.host.n_grams;
+        const size_t sizes[4] = {sizeof(uint64_t) * (nspace + 1), sizeof(uint32_t) * n_post, sizeof(uint32_t) * nspace,
+                                 sizeof(uint32_t) * rows * (X.n_buckets + 1)};
+        const void* ptrs[4] = {X.gram_off, X.post, X.gram_row, X.skip};
+        vals[0] = n_post;
+        vals[1] = rows;
+        vals[2] = X.n_buckets;
+        for (int i = 0; i < 4; ++i)
+            if (!digest(ptrs[i], sizes[i], vals[3 + i])) return -4;
+        vals[7] = X.bucket_span;
+    }
+    // the interned library (ngs_intern.hip or the host build): terms, pairs, keys, wildcard answer
+    uint64_t tchars = 0;
+    uint32_t npairs = 0;
+    if (!HIP_CHECK(hipMemcpy(&tchars, X.term_off + X.n_terms, sizeof(uint64_t), hipMemcpyDeviceToHost)) ||
+        !HIP_CHECK(hipMemcpy(&npairs, X.tk_off + X.n_terms, sizeof(uint32_t), hipMemcpyDeviceToHost)))
+        return -4;
+    const uint64_t kchars = L.host.key_off[X.n_keys];
+    const size_t tsizes[8] = {sizeof(uint64_t) * (X.n_terms + 1), tchars * X.csize,
+                              sizeof(uint32_t) * (X.n_terms + 1), sizeof(uint2) * npairs,
+                              sizeof(uint64_t) * (X.n_keys + 1), kchars * X.csize,
+                              sizeof(uint32_t) * X.n_keys, sizeof(float) * X.n_keys};
+    const void* tptrs[8] = {X.term_off, X.term_bytes, X.tk_off, X.tk, X.key_off, X.key_bytes, X.wild_key, X.wild_score};
+    for (int i = 0; i < 8; ++i)
+        if (!digest(tptrs[i], tsizes[i], vals[8 + i])) return -4;
+    const int m = std::min(n, 16);
+    for (int i = 0; i < m; ++i) out[i] = vals[i];
+    return m;
 }
 
 NGS_API int ngsPhaseStats(uint64_t* out, int n, int reset) {

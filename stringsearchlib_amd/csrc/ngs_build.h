@@ -21,4 +21,14 @@ struct DeviceGrams {           // device arrays, owned by the caller after a suc
 hipError_t build_grams_device(const uint64_t* term_off, const uint8_t* term_bytes, uint32_t n_short,
                               uint32_t n_terms, DeviceGrams& out);
 
+struct HostIndex;
+
+// String interning, term ids, key ranks, the term -> key CSR and the wildcard weights of an index
+// on the current device (ngs_intern.hip), into the host index (ix.csize, short_term_len set by the
+// caller). words are char* (ix.csize 1) or UTF-32 strings (4). hipErrorNotSupported: the host
+// build must decide (a 64-bit hash collision between two strings, a NaN weight, >= 2^31 words, or
+// no pair at all); other codes are HIP failures.
+hipError_t intern_device(HostIndex& ix, const void* const* words, uint64_t size, uint16_t rowSize,
+                         const float* weight, uint32_t g);
+
 }  // namespace ngs

@@ -1,6 +1,8 @@
 // ngs_index.cpp — host index build (see ngs_index.h). Paths cited relative to /root/reference.
 #include "ngs_index.h"
 
+#include "ngs_build.h"
+
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -348,6 +350,22 @@ static void build_impl(HostIndex& ix, const CharT* const* words, uint64_t size, 
     bool valid[256] = {};
     for (const char* c = kDefaultValid; *c; ++c) valid[(uint8_t)*c] = true;
     PhaseTimer pt;
+
+    // the interning, key ranks and term -> key CSR on the GPU (ngs_intern.hip), unless
+    // NGS_HOST_INTERN is set or it defers to the host (collision, NaN weight, size); same arrays
+    if (!std::getenv("NGS_HOST_INTERN")) {
+        const hipError_t e = intern_device(ix, reinterpret_cast<const void* const*>(words), size, rowSize, weight, g);
+        if (e == hipSuccess) {
+            pt.mark("intern + CSR (GPU)");
+            ix.indexed = true;  // hpp:45
+            ix.grams_built = false;
+            if (ix.gram_mode == 0 && !std::getenv("NGS_HOST_GRAMS")) return;
+            build_grams_impl<CharT>(ix, threads, pt);
+            return;
+        }
+        (void)hipGetLastError();
+        if (e != hipErrorNotSupported) std::fprintf(stderr, "ngram_search: GPU index build failed (%s), building on the host\n", hipGetErrorString(e));
+    }
 
     constexpr uint32_t cs = sizeof(CharT);
     Interner terms, keys;  // interned as raw bytes (cs per character)
