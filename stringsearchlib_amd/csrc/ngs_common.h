@@ -92,6 +92,9 @@ static_assert(kWaveMaxLimit * 2 <= (uint32_t)kWaveCand, "a flush keeps at most h
 constexpr int kWaveChunks = kSketchCap / 4;     // 16-byte chunks per part and wave (sketch parts)
 constexpr int kExactChunks = (kWaveCap < kSketchCap ? kWaveCap : kSketchCap) / 4;  // ... parts counted exactly (cmin <= 2)
 constexpr int kDmaRounds = kWaveChunks / 64;    // dwordx4 loads per lane for one part
+#ifndef NGS_CAND_BALLOT
+#define NGS_CAND_BALLOT 1  // one-wave sketch: candidates written per entry slot through a ballot
+#endif
 #ifndef NGS_LEAN_CELL_XOR
 #define NGS_LEAN_CELL_XOR 0  // tier-1a sketch cell: 1 = (t ^ t >> 13) & mask, 0 = t & mask
 #endif

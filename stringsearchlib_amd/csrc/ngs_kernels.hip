@@ -1224,47 +1224,76 @@ __device__ __forceinline__ uint32_t part_sketch(WaveSmem<W, LEAN>& S, const uint
         grp_sync<W>();
         return 0;
     }
-    // candidates are rare (~10 of ~600 entries): flag them in a per-lane mask, then write them
-    // at offsets from one prefix sum instead of compacting every entry slot by ballot
-    uint32_t cm = 0;
+    const uint32_t ov = __ballot(ovf) ? 65u : 0u;  // a wrapped counter forces exact counting
+    uint32_t wnc = 0;
+    if constexpr (W == 1 && NGS_CAND_BALLOT) {
+        // one wave: candidates are rare (~3.5 of ~410 entries), so each entry slot is a compare
+        // into a ballot and a uniform branch, taken by the few slots holding one, which write
+        // their terms in place (no per-lane mask, prefix sum or register select)
+        uint32_t nw = 0;
 #pragma unroll
-    for (uint32_t r = 0; r < (uint32_t)NR; ++r) {
-        if (64 * r < mt) {
-            const uint32_t t[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
-            uint32_t w[4];
+        for (uint32_t r = 0; r < (uint32_t)NR; ++r) {
+            if (64 * r < mt) {
+                const uint32_t t[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
+                uint32_t w[4];
 #pragma unroll
-            for (uint32_t e = 0; e < 4; ++e) w[e] = *sketch_word<W, LEAN>(S.table, t[e]);
+                for (uint32_t e = 0; e < 4; ++e) w[e] = *sketch_word<W, LEAN>(S.table, t[e]);
 #pragma unroll
-            for (uint32_t e = 0; e < 4; ++e) {
-                cm |= (__builtin_amdgcn_ubfe(w[e], sketch_sh4<W, LEAN>(t[e]), 4u) >= cmin ? 1u : 0u) << (4 * r + e);
+                for (uint32_t e = 0; e < 4; ++e) {
+                    const bool f = ((vmask >> (4 * r + e)) & 1u) &&
+                                   __builtin_amdgcn_ubfe(w[e], sketch_sh4<W, LEAN>(t[e]), 4u) >= cmin;
+                    const unsigned long long b = __ballot(f);
+                    if (b) {
+                        const uint32_t pos = nw + rank_below(b);
+                        if (f && pos < 64u) S.cbuf[pos] = t[e];
+                        nw += (uint32_t)__popcll(b);
+                    }
+                }
             }
         }
-    }
-    cm &= vmask;
-    const uint32_t ov = __ballot(ovf) ? 65u : 0u;  // a wrapped counter forces exact counting
-    const uint32_t mine = __popc(cm);
-    const uint32_t incl = wave_incl_scan(mine);
-    const uint32_t wnc = __builtin_amdgcn_readlane(incl, 63) + ov;
-    uint32_t base = 0;
-    if constexpr (W > 1) {
-        uint32_t b0 = 0;
-        if (lane == 0 && wnc) b0 = atomicAdd(&S.ncand, wnc);
-        base = __builtin_amdgcn_readlane(b0, 0);
-    }
-    if (base + wnc <= 64 && cm) {  // the few lanes holding candidates walk their set bits
-        uint32_t pos = base + incl - mine;
-        uint32_t bits = cm;
-        do {
-            const uint32_t k = __ffs(bits) - 1u;
-            bits &= bits - 1u;
-            uint32_t t = 0;
+        wnc = nw + ov;
+    } else {
+        // candidates are rare (~10 of ~600 entries): flag them in a per-lane mask, then write them
+        // at offsets from one prefix sum instead of compacting every entry slot by ballot
+        uint32_t cm = 0;
 #pragma unroll
-            for (uint32_t j = 0; j < 4 * (uint32_t)NR; ++j) {
-                const uint32_t x = (j & 3) == 0 ? v[j >> 2].x : (j & 3) == 1 ? v[j >> 2].y : (j & 3) == 2 ? v[j >> 2].z : v[j >> 2].w;
-                t = j == k ? x : t;
+        for (uint32_t r = 0; r < (uint32_t)NR; ++r) {
+            if (64 * r < mt) {
+                const uint32_t t[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
+                uint32_t w[4];
+#pragma unroll
+                for (uint32_t e = 0; e < 4; ++e) w[e] = *sketch_word<W, LEAN>(S.table, t[e]);
+#pragma unroll
+                for (uint32_t e = 0; e < 4; ++e) {
+                    cm |= (__builtin_amdgcn_ubfe(w[e], sketch_sh4<W, LEAN>(t[e]), 4u) >= cmin ? 1u : 0u) << (4 * r + e);
+                }
             }
-            S.cbuf[pos++] = t;
-        } while (bits);
+        }
+        cm &= vmask;
+        const uint32_t mine = __popc(cm);
+        const uint32_t incl = wave_incl_scan(mine);
+        wnc = __builtin_amdgcn_readlane(incl, 63) + ov;
+        uint32_t base = 0;
+        if constexpr (W > 1) {
+            uint32_t b0 = 0;
+            if (lane == 0 && wnc) b0 = atomicAdd(&S.ncand, wnc);
+            base = __builtin_amdgcn_readlane(b0, 0);
+        }
+        if (base + wnc <= 64 && cm) {  // the few lanes holding candidates walk their set bits
+            uint32_t pos = base + incl - mine;
+            uint32_t bits = cm;
+            do {
+                const uint32_t k = __ffs(bits) - 1u;
+                bits &= bits - 1u;
+                uint32_t t = 0;
+#pragma unroll
+                for (uint32_t j = 0; j < 4 * (uint32_t)NR; ++j) {
+                    const uint32_t x = (j & 3) == 0 ? v[j >> 2].x : (j & 3) == 1 ? v[j >> 2].y : (j & 3) == 2 ? v[j >> 2].z : v[j >> 2].w;
+                    t = j == k ? x : t;
+                }
+                S.cbuf[pos++] = t;
+            } while (bits);
+        }
     }
     grp_sync<W>();
     uint32_t nc = __builtin_amdgcn_readfirstlane(W == 1 ? wnc : S.ncand);
