@@ -35,6 +35,7 @@ constexpr size_t kGeneralBudget = size_t(2) << 30;   // bytes of dense general-p
 constexpr uint32_t kSmallBatch = 16;                 // host batches up to this many queries take the latency path
 constexpr size_t kSmallBlock = size_t(1) << 20;      // ... if their output block is at most this many bytes
 constexpr size_t kPartBudget = size_t(1) << 30;      // bytes of sliced tier-1b partial results per call
+constexpr int kRetryQcap = -6;                       // finish_search: rerun with the batch's byte count
 
 bool hip_ok(hipError_t e, const char* what) {
     if (e == hipSuccess) return true;
@@ -94,7 +95,8 @@ struct Context {
     uint32_t* d_glist = nullptr;
     uint32_t* d_list2 = nullptr;
     uint32_t* d_gcount = nullptr;  // [0] general-path count, [1] tier-2 count, [2] tier-1b hand-overs, [3] heavy,
-                                   // [4] hand-overs of the heavy list's lean launch, [5] full list
+                                   // [4] hand-overs of the heavy list's lean launch, [5] full list,
+                                   // [6] k_prep: a query past the normalised-query buffer (qcap)
     uint32_t* d_fb = nullptr;      // queries tier 1a handed to tier 1b
     uint32_t* d_fb2 = nullptr;     // ... from the heavy list (side stream)
     uint32_t* d_heavy = nullptr;   // queries the prep kernel listed as heavy (cmin 2)
@@ -200,7 +202,7 @@ struct Replica {
         c->d_gcount = reinterpret_cast<uint32_t*>(c->d_stats + kStatSlots);
         c->d_lctr = reinterpret_cast<uint32_t*>(c->d_stats + kStatSlots + 1);
         static_assert(sizeof(DevStats) == 16 * sizeof(uint32_t), "k_prep's counters are 16 words apart");
-        static_assert(sizeof(DevStats) >= 6 * sizeof(uint32_t), "the path counts fit one stats slot");
+        static_assert(sizeof(DevStats) >= 7 * sizeof(uint32_t), "the path counts fit one stats slot");
         return c;
     }
     void give_back(std::unique_ptr<Context> c) {
@@ -517,6 +519,8 @@ int queue_search(Library& L, Replica& R, Context& c, const uint8_t* d_raw, const
     P.est = c.d_est;
     P.esc = c.d_esc;
     P.nslices = small ? 1u : ensure_parts(c, B, P.limit);
+    P.qcap = c.qcap;
+    P.oflow = c.d_gcount + 6;
     P.prec = c.d_prec;
     P.pcnt = c.d_pcnt;
     const bool timing = L.timing.load();
@@ -549,6 +553,7 @@ int finish_search(Library& L, Replica& R, Context& c, uint32_t B, const SearchPa
     st.queries = B;
     // general, tier 2, tier 1a hand-overs, heavy, heavy hand-overs, full
     const uint32_t* counts3 = reinterpret_cast<const uint32_t*>(c.h_stats + kStatSlots);
+    if (counts3[6]) return kRetryQcap;  // a query past the normalised-query buffer: nothing is valid
     const uint32_t ngen = counts3[0];
     if (ngen) {
         std::vector<uint32_t> gl(ngen);
@@ -1039,14 +1044,24 @@ NGS_API int ngsSearchDevice(uint32_t handle, const uint8_t* dQueryBytes, const u
     }
     std::unique_ptr<Context> c = R.acquire();
     if (!c) return -4;
-    uint64_t qbytes = 0;
+    // The batch's byte count sizes the normalised-query buffer. A context that has one already
+    // launches without reading it back (a sync before any kernel); k_prep flags a batch that
+    // does not fit and the call reruns after the read-back.
     int rc = 0;
-    if (nQueries &&
-        (!HIP_CHECK(hipMemcpyAsync(&qbytes, dQueryOffsets + nQueries, sizeof(uint64_t), hipMemcpyDeviceToHost, s)) ||
-         !HIP_CHECK(hipStreamSynchronize(s))))
-        rc = -4;
+    auto read_bytes = [&](uint64_t& qb) -> bool {
+        return HIP_CHECK(hipMemcpyAsync(&qb, dQueryOffsets + nQueries, sizeof(uint64_t), hipMemcpyDeviceToHost, s)) &&
+               HIP_CHECK(hipStreamSynchronize(s));
+    };
+    uint64_t qbytes = 0;
+    if (nQueries && !c->qcap && !read_bytes(qbytes)) rc = -4;
     if (!rc) rc = device_search(*L, R, *c, dQueryBytes, dQueryOffsets, nQueries, qbytes, threshold, Lm, outStride,
                                 dCounts, dKeys, dScores, s);
+    if (rc == kRetryQcap) {
+        rc = read_bytes(qbytes) ? device_search(*L, R, *c, dQueryBytes, dQueryOffsets, nQueries, qbytes, threshold, Lm,
+                                                outStride, dCounts, dKeys, dScores, s)
+                                : -4;
+        if (rc == kRetryQcap) rc = -5;
+    }
     R.give_back(std::move(c));
     return rc;
 }

@@ -220,6 +220,11 @@ struct SearchParams {
     uint32_t nslices;
     uint64_t* prec;
     uint32_t* pcnt;
+    // capacity (bytes) of the normalised-query buffer: k_prep flags (*oflow = 1) a query whose
+    // bytes end past it instead of writing, and the host reruns the call with a larger buffer
+    // (ngsSearchDevice does not read the batch's byte count back before launching)
+    uint64_t qcap;
+    uint32_t* oflow;
 };
 
 // Tier 1b slices per query (SearchParams.nslices): a full-list or handed-over query is a few

@@ -102,13 +102,19 @@ __global__ __launch_bounds__(64) void k_prep(const uint8_t* __restrict__ raw, co
     const uint8_t* rq = raw;  // query q: characters of cs bytes from byte offset off[q]
     uint8_t* nq = qnorm;
     uint64_t n = 0;
+    bool over = false;
     if (live) {
         rq = raw + off[q];
         nq = qnorm + off[q];
         n = (off[q + 1] - off[q]) / cs;
         if (gl == 0 && P.esn) P.esn[q] = kNoEmit;  // set by tier 1a when it finishes the query (DEFER)
+        over = off[q + 1] > P.qcap;  // the normalised bytes would not fit: the host reruns the call
+        if (over) {
+            if (gl == 0) atomicOr(P.oflow, 1u);
+            n = 0;
+        }
     }
-    const bool wild = live && (n == 0 || (n == 1 && char_at(rq, 0, cs) == '*'));  // nGramSearch.hpp:356
+    const bool wild = live && !over && (n == 0 || (n == 1 && char_at(rq, 0, cs) == '*'));  // nGramSearch.hpp:356
     uint64_t first = n, last = 0;
     bool seek = live && !wild;
     for (uint64_t base = 0; __ballot(seek); base += 16) {

@@ -168,6 +168,40 @@ def test_device_api_matches_host_api():
         assert_exact(dv, h, f"device q={qs[i]!r}")
 
 
+def test_device_api_query_buffer_grows():
+    """ngsSearchDevice launches without reading the batch's byte count back once its context has a
+    normalised-query buffer; a later, larger batch that does not fit is flagged by k_prep and the
+    call reruns with a larger buffer (same answers as the host API)."""
+    torch = pytest.importorskip("torch")
+    words, wts, rng = ssl.synth.gen_corpus(5000, seed=23)
+    gi = ssl.StringIndex(words, 1, wts)
+    dev = torch.device("cuda:0")
+    limit = 20
+
+    def run(qs):
+        raw = torch.tensor(list(b"".join(qs)), dtype=torch.uint8, device=dev)
+        offs = [0]
+        for q in qs:
+            offs.append(offs[-1] + len(q))
+        off = torch.tensor(offs, dtype=torch.int64, device=dev)
+        counts = torch.zeros(len(qs), dtype=torch.int32, device=dev)
+        keys = torch.zeros(len(qs) * limit, dtype=torch.int32, device=dev)
+        scores = torch.zeros(len(qs) * limit, dtype=torch.float32, device=dev)
+        gi.search_device(raw.data_ptr(), off.data_ptr(), len(qs), 0.3, limit, limit, counts.data_ptr(),
+                         keys.data_ptr(), scores.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        c, k, s = counts.cpu().tolist(), keys.cpu().tolist(), scores.cpu().tolist()
+        return [[(gi.key(k[i * limit + j]), s[i * limit + j]) for j in range(c[i])] for i in range(len(qs))]
+
+    small = ssl.synth.gen_queries(words, 1, 50, rng)
+    big = ssl.synth.gen_queries(words, 1, 200, rng) * 40 + [b"x" * 70000]  # > the first 64 KB buffer
+    for qs in (small, big, small):
+        got = run(qs)
+        host = gi.score_batch(qs, 0.3, limit)
+        for i, h in enumerate(host):
+            assert_exact(got[i], h, f"device q#{i} of {len(qs)}")
+    gi.dispose()
+
+
 def test_dispose_and_handle_reuse():
     words = [b"ALPHA BRAVO", b"CHARLIE DELTA", b"ECHO FOXTROT"]
     a = ssl.StringIndex(words)
