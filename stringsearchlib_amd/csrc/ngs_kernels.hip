@@ -236,11 +236,91 @@ __device__ __forceinline__ uint32_t string_match_t(const uint32_t (&qc)[8], uint
     }
     return m - best;
 }
-// term t of the index against the query (m <= 8 characters in qc)
-__device__ __forceinline__ uint32_t string_match(const uint32_t (&qc)[8], uint32_t m, const DevIndex& X, uint32_t t) {
+
+// The same value by Myers' bit-vector algorithm (J. ACM 46(3), 1999) in its approximate-matching
+// form: bit i of the vertical deltas is row i + 1 of the DP column; a free start in the source is
+// a zero carried into the horizontal deltas, the score tracks the last row (the query's end), and
+// its minimum over the columns is the free end. peq[c] holds the query positions holding
+// character c (c < 256; others are compared with qc); ~16 operations per source character
+// against ~50 for the column DP. Tested against the DP above and the reference's through the
+// oracle (tests/test_gpu_parity.py short corpora, test_oracle_golden.py).
+template <typename TT>
+__device__ __forceinline__ uint32_t myers_match_t(const uint8_t* peq, const uint32_t (&qc)[8], uint32_t m,
+                                                  const TT* s, uint32_t L) {
+    const uint32_t top = 1u << (m - 1u);
+    uint32_t pv = ~0u, mv = 0u, score = m, best = m;
+    // byte strings are read a dword at a time, the next one in flight while the current one is
+    // consumed (term_bytes is padded to whole dwords): a byte load per character was the cost
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(reinterpret_cast<uintptr_t>(s) & ~(uintptr_t)3);
+    const uint32_t skip = (uint32_t)(reinterpret_cast<uintptr_t>(s) & 3u);
+    uint32_t cur = 0, nxt = 0;
+    if (sizeof(TT) == 1 && L) {
+        cur = w[0] >> (8u * skip);
+        nxt = skip + L > 4u ? w[1] : 0u;
+    }
+    uint32_t avail = 4u - skip, k = 1;
+    for (uint32_t j = 0; j < L; ++j) {
+        uint32_t c;
+        if constexpr (sizeof(TT) == 1) {
+            if (!avail) {
+                cur = nxt;
+                avail = 4u;
+                ++k;
+                if (j + 4u < L) nxt = w[k];
+            }
+            c = cur & 255u;
+            cur >>= 8;
+            --avail;
+        } else {
+            c = s[j];
+        }
+        uint32_t eq;
+        if (sizeof(TT) == 1 || c < 256u) {
+            eq = peq[c];
+        } else {
+            eq = 0u;
+#pragma unroll
+            for (uint32_t i = 0; i < 8; ++i) eq |= (i < m && qc[i] == c) ? 1u << i : 0u;
+        }
+        const uint32_t xv = eq | mv;
+        const uint32_t xh = (((eq & pv) + pv) ^ pv) | eq;
+        uint32_t ph = mv | ~(xh | pv);
+        uint32_t mh = pv & xh;
+        score += (ph & top) ? 1u : 0u;
+        score -= (mh & top) ? 1u : 0u;
+        ph <<= 1;  // row 0's horizontal delta is 0: the match may start anywhere in the source
+        mh <<= 1;
+        pv = mh | ~(xv | ph);
+        mv = ph & xv;
+        best = min(best, score);
+    }
+    return m - best;
+}
+
+// the match-mask table of Myers' algorithm for characters < 256: peq[c] bit i = (q[i] == c);
+// threads [tid0, tid0 + nthreads) of the caller fill it (the caller orders it before use)
+template <class QF>
+__device__ __forceinline__ void build_peq(uint8_t* peq, QF q, uint32_t m, uint32_t tid0, uint32_t nthreads) {
+    for (uint32_t c = tid0; c < 256u; c += nthreads) {
+        uint32_t e = 0;
+        for (uint32_t i = 0; i < m && i < 8; ++i) e |= (q(i) == c) ? 1u << i : 0u;
+        peq[c] = (uint8_t)e;
+    }
+}
+
+#ifndef NGS_MYERS
+#define NGS_MYERS 1  // 0: the column DP (A/B)
+#endif
+// term t of the index against the query (m <= 8 characters in qc; peq its match masks)
+__device__ __forceinline__ uint32_t string_match(const uint8_t* peq, const uint32_t (&qc)[8], uint32_t m,
+                                                 const DevIndex& X, uint32_t t) {
     const uint64_t a = X.term_off[t], b = X.term_off[t + 1];
-    if (X.csize == 4) return string_match_t(qc, m, reinterpret_cast<const uint32_t*>(X.term_bytes) + a, (uint32_t)(b - a));
-    return string_match_t(qc, m, X.term_bytes + a, (uint32_t)(b - a));
+    if (X.csize == 4) {
+        const uint32_t* s = reinterpret_cast<const uint32_t*>(X.term_bytes) + a;
+        return NGS_MYERS ? myers_match_t(peq, qc, m, s, (uint32_t)(b - a)) : string_match_t(qc, m, s, (uint32_t)(b - a));
+    }
+    const uint8_t* s = X.term_bytes + a;
+    return NGS_MYERS ? myers_match_t(peq, qc, m, s, (uint32_t)(b - a)) : string_match_t(qc, m, s, (uint32_t)(b - a));
 }
 
 // Gram of the query characters at position i (accessor qf), as a row of the gram space:
@@ -281,6 +361,7 @@ struct FastSmem {
     uint2 part[kMaxBuckets];       // parts: bucket range [x, y & 0x7fffffff), y >> 31 = oversized
     uint32_t pre[260];             // segment prefix sums
     uint8_t q[264];
+    uint8_t peq[256];              // Myers match masks of the query (short search)
     uint64_t tau;                  // records >= tau cannot enter the top-L
     uint64_t p_left;
     unsigned long long seg_total;
@@ -557,11 +638,13 @@ __device__ void fast_one(const uint32_t q, FastSmem& S, const DevIndex& X, const
         uint32_t qc[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) qc[i] = (uint32_t)i < m ? S.q[i] : 0;
+        build_peq(S.peq, [&](uint32_t i) { return (uint32_t)S.q[i]; }, m, tid, kFastThreads);
+        __syncthreads();
         uint32_t t = tid;
         const float fm = (float)m;
         produce(S, X, P, m, L, &stats->errors, [&](EmitState& st) -> int {
             if (t >= X.n_short) return 0;
-            const uint32_t match = string_match(qc, m, X, t);
+            const uint32_t match = string_match(S.peq, qc, m, X, t);
             const float s = (float)match / fm;  // nGramSearch.hpp:244
             const uint32_t id = t;
             t += kFastThreads;
@@ -787,6 +870,7 @@ struct alignas(16) WaveSmem {
     uint32_t cbuf[64];               // sketch candidates (terms)
     uint8_t surv_c[kWaveSurv];       // hit count, | 0x80 for a Levenshtein (short search) match count
     uint32_t q[kWaveMaxGrams + 8];   // normalised query, one code point per entry
+    uint8_t peq[LEAN ? 4 : 256];     // tier 1b: Myers match masks of the query (short search)
     uint32_t surv_total;             // stats
     uint32_t ncand;                  // sketch candidates of the part, all waves
     uint32_t x_surv_n, x_cand_n;     // wave 0's emit state, handed round in exact-path turns
@@ -1434,11 +1518,16 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
         for (int i = 0; i < 8; ++i) qc[i] = (uint32_t)i < m ? S.q[i] : 0;
         const unsigned long long okm = __ballot(lane <= m && !(sc_short < P.thr));  // hpp:315
         const uint32_t cmin_s = okm ? (uint32_t)(__ffsll((long long)okm) - 1) : 64u;
+        if constexpr (!LEAN) {
+            build_peq(S.peq, [&](uint32_t i) { return S.q[i]; }, m, lane, 64u);
+            wave_sync();
+        }
         for (uint32_t t0 = 0; t0 < X.n_short; t0 += 64) {
             if (surv_n + 64 > (uint32_t)kWaveSurv) wave_emit(S, X, P, m, L, sc_long, sc_short, surv_n, cand_n, tau);
             const uint32_t t = t0 + lane;
             uint32_t match = 0;
-            if (t < X.n_short) match = string_match(qc, m, X, t);
+            if constexpr (!LEAN)
+                if (t < X.n_short) match = string_match(S.peq, qc, m, X, t);
             surv_append(S, t < X.n_short && match >= cmin_s, t, match | 0x80u, surv_n);
         }
     }
@@ -2304,10 +2393,13 @@ __global__ __launch_bounds__(256) void k_gen_short(DevIndex X, SearchParams P, c
     uint32_t qc[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) qc[i] = (uint32_t)i < m ? char_at(qs, i, X.csize) : 0;
+    __shared__ uint8_t peq[256];
+    build_peq(peq, [&](uint32_t i) { return char_at(qs, i, X.csize); }, m, threadIdx.x, blockDim.x);
+    __syncthreads();
     uint32_t* K = kenc + (size_t)gi * X.n_keys;
     const float fm = (float)m;
     for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < end; t += gridDim.x * blockDim.x) {
-        const float s = (float)string_match(qc, m, X, t) / fm;
+        const float s = (float)string_match(peq, qc, m, X, t) / fm;
         if (!(s < P.thr)) emit_global(X, t, s, qs, m, P.valid, K);
     }
 }
