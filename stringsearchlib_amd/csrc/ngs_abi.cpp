@@ -35,6 +35,10 @@ constexpr size_t kGeneralBudget = size_t(2) << 30;   // bytes of dense general-p
 constexpr uint32_t kSmallBatch = 16;                 // host batches up to this many queries take the latency path
 constexpr size_t kSmallBlock = size_t(1) << 20;      // ... if their output block is at most this many bytes
 constexpr size_t kPartBudget = size_t(1) << 30;      // bytes of sliced tier-1b partial results per call
+constexpr size_t kSmallQ = size_t(64) << 10;         // ... and if their offsets + bytes fit this many bytes
+// the latency path's one block, device and pinned host: statistics | results | queries
+constexpr size_t kSioStats = sizeof(DevStats) * (kStatSlots + 1);
+constexpr size_t kSioBytes = kSioStats + kSmallBlock + kSmallQ;
 constexpr int kRetryQcap = -6;                       // finish_search: rerun with the batch's byte count
 
 bool hip_ok(hipError_t e, const char* what) {
@@ -128,15 +132,18 @@ struct Context {
     size_t ptemp_bytes = 0;
     GeneralBuffers gen;
     Pinned h_off, h_raw, h_res;  // queries in; results out
+    uint8_t* d_sio = nullptr;     // the latency path's block (kSioBytes): one copy in, one copy out
+    uint8_t* h_sio = nullptr;     // ... its pinned host image
 
     ~Context() {
         hipSetDevice(device);
         for (void* p : {(void*)d_raw, (void*)d_off, (void*)d_norm, (void*)d_qm, (void*)d_glist, (void*)d_list2, (void*)d_fb, (void*)d_fb2, (void*)d_heavy, (void*)d_full, (void*)d_lslots,
                         (void*)d_esn, (void*)d_est, (void*)d_esc, (void*)d_prec, (void*)d_pcnt,
-                        (void*)d_group, (void*)d_stats, (void*)d_out, (void*)d_pos, (void*)d_pk, (void*)d_ps, d_ptemp, (void*)gen.cnt,
+                        (void*)d_group, (void*)d_stats, (void*)d_sio, (void*)d_out, (void*)d_pos, (void*)d_pk, (void*)d_ps, d_ptemp, (void*)gen.cnt,
                         (void*)gen.kenc, (void*)gen.list, (void*)gen.sorted, (void*)gen.lcount, gen.temp})
             if (p) hipFree(p);
         if (h_stats) hipHostFree(h_stats);
+        if (h_sio) hipHostFree(h_sio);
         for (hipEvent_t e : ev)
             if (e) hipEventDestroy(e);
         for (hipEvent_t e : {fork, join, join2})
@@ -197,6 +204,8 @@ struct Replica {
         for (hipEvent_t& e : c->ev)
             if (!HIP_CHECK(hipEventCreate(&e))) return nullptr;
         if (!dev_alloc(&c->d_group, 64) || !dev_alloc(&c->d_stats, kStatSlots + 1 + 2 * kListSlots) ||
+            !dev_alloc(&c->d_sio, kSioBytes) ||
+            !HIP_CHECK(hipHostMalloc((void**)&c->h_sio, kSioBytes, hipHostMallocDefault)) ||
             !HIP_CHECK(hipHostMalloc((void**)&c->h_stats, sizeof(DevStats) * (kStatSlots + 1), hipHostMallocDefault)))
             return nullptr;
         c->d_gcount = reinterpret_cast<uint32_t*>(c->d_stats + kStatSlots);
@@ -483,6 +492,10 @@ bool ensure_general(const Replica& R, Context& c, hipStream_t s) {
 int queue_search(Library& L, Replica& R, Context& c, const uint8_t* d_raw, const uint64_t* d_off, uint32_t B,
                  uint64_t qbytes, float thr, uint32_t limit, uint32_t stride, uint32_t* d_n, uint32_t* d_k,
                  float* d_s, hipStream_t s, SearchParams& P, bool small) {
+    // small: the statistics go to the latency block (zeroed by k_prep, read back by the caller
+    // together with the results)
+    DevStats* sd = small ? reinterpret_cast<DevStats*>(c.d_sio) : c.d_stats;
+    uint32_t* gc = reinterpret_cast<uint32_t*>(sd + kStatSlots);
     P = SearchParams{};
     P.thr = thr;
     P.limit = limit;
@@ -520,39 +533,42 @@ int queue_search(Library& L, Replica& R, Context& c, const uint8_t* d_raw, const
     P.esc = c.d_esc;
     P.nslices = small ? 1u : ensure_parts(c, B, P.limit);
     P.qcap = c.qcap;
-    P.oflow = c.d_gcount + 6;
+    P.oflow = gc + 6;
+    if (small) {
+        P.zero_stats = reinterpret_cast<uint32_t*>(sd);
+        P.zero_words = (uint32_t)(kSioStats / sizeof(uint32_t));
+    }
     P.prec = c.d_prec;
     P.pcnt = c.d_pcnt;
     const bool timing = L.timing.load();
     // statistics, path counts and list counters
-    if (!HIP_CHECK(hipMemsetAsync(c.d_stats, 0, sizeof(DevStats) * (kStatSlots + 1 + 2 * kListSlots), s))) return -4;
+    if (!small && !HIP_CHECK(hipMemsetAsync(c.d_stats, 0, sizeof(DevStats) * (kStatSlots + 1 + 2 * kListSlots), s)))
+        return -4;
     if (timing) HIP_CHECK(hipEventRecord(c.ev[0], s));
-    if (!HIP_CHECK(launch_prep(d_raw, d_off, B, P, c.d_norm, c.d_qm, R.dev.csize, R.dev, c.d_heavy, c.d_gcount + 3,
-                               c.d_full, c.d_gcount + 5, c.d_lslots, c.d_lctr, s)))
+    if (!HIP_CHECK(launch_prep(d_raw, d_off, B, P, c.d_norm, c.d_qm, R.dev.csize, R.dev, c.d_heavy, gc + 3, c.d_full,
+                               gc + 5, c.d_lslots, c.d_lctr, s)))
         return -4;
     if (timing) HIP_CHECK(hipEventRecord(c.ev[1], s));
     if (timing) HIP_CHECK(hipEventRecord(c.ev[2], s));
-    if (!HIP_CHECK(launch_fast(R.dev, P, c.d_norm, d_off, c.d_qm, d_n, d_k, d_s, c.d_list2, c.d_gcount + 1,
-                               c.d_fb, c.d_gcount + 2, c.d_fb2, c.d_gcount + 4, c.d_heavy, c.d_gcount + 3, c.d_full,
-                               c.d_gcount + 5, c.d_glist, c.d_gcount, c.d_stats, s, c.side, c.side2, c.fork, c.join,
-                               c.join2)))
+    if (!HIP_CHECK(launch_fast(R.dev, P, c.d_norm, d_off, c.d_qm, d_n, d_k, d_s, c.d_list2, gc + 1, c.d_fb, gc + 2,
+                               c.d_fb2, gc + 4, c.d_heavy, gc + 3, c.d_full, gc + 5, c.d_glist, gc, sd, s, c.side,
+                               c.side2, c.fork, c.join, c.join2)))
         return -4;
     if (timing) HIP_CHECK(hipEventRecord(c.ev[3], s));
     // the statistics and the path counts in one read-back (the general path adds no statistics)
-    if (!HIP_CHECK(hipMemcpyAsync(c.h_stats, c.d_stats, sizeof(DevStats) * (kStatSlots + 1), hipMemcpyDeviceToHost,
-                                  s)))
-        return -4;
+    if (!small && !HIP_CHECK(hipMemcpyAsync(c.h_stats, c.d_stats, kSioStats, hipMemcpyDeviceToHost, s))) return -4;
     return 0;
 }
 
 int finish_search(Library& L, Replica& R, Context& c, uint32_t B, const SearchParams& P, const uint64_t* d_off,
-                  uint32_t* d_n, uint32_t* d_k, float* d_s, hipStream_t s) {
+                  uint32_t* d_n, uint32_t* d_k, float* d_s, hipStream_t s, bool small = false) {
     if (!HIP_CHECK(hipStreamSynchronize(s))) return -4;
+    const DevStats* hst = small ? reinterpret_cast<const DevStats*>(c.h_sio) : c.h_stats;
     const bool timing = L.timing.load();
     ngs_stats st{};
     st.queries = B;
     // general, tier 2, tier 1a hand-overs, heavy, heavy hand-overs, full
-    const uint32_t* counts3 = reinterpret_cast<const uint32_t*>(c.h_stats + kStatSlots);
+    const uint32_t* counts3 = reinterpret_cast<const uint32_t*>(hst + kStatSlots);
     if (counts3[6]) return kRetryQcap;  // a query past the normalised-query buffer: nothing is valid
     const uint32_t ngen = counts3[0];
     if (ngen) {
@@ -578,7 +594,7 @@ int finish_search(Library& L, Replica& R, Context& c, uint32_t B, const SearchPa
     }
     DevStats ds{};
     for (uint32_t i = 0; i < kStatSlots; ++i) {
-        const DevStats& x = c.h_stats[i];
+        const DevStats& x = hst[i];
         ds.postings += x.postings;
         ds.lists += x.lists;
         ds.results += x.results;
@@ -653,43 +669,70 @@ bool host_search_one(Library& L, Replica& R, const CharT* const* queries, uint32
     bool ok = true;
     for (uint32_t q0 = 0; q0 < nq && ok; q0 += (uint32_t)max_chunk) {
         const uint32_t B = (uint32_t)std::min<size_t>(max_chunk, nq - q0);
-        // queries into pinned staging: offsets, then the bytes
+        // query offsets into pinned staging
         ok = c->h_off.grow(sizeof(uint64_t) * (B + 1));
         if (!ok) break;
         uint64_t* ho = c->h_off.as<uint64_t>();
         ho[0] = 0;
         for (uint32_t i = 0; i < B; ++i) ho[i + 1] = ho[i] + (queries[q0 + i] ? str_len(queries[q0 + i]) * cs : 0);
-        ok = c->h_raw.grow(std::max<uint64_t>(ho[B], 1));
-        if (!ok) break;
-        for (uint32_t i = 0; i < B; ++i)
-            if (queries[q0 + i]) std::memcpy(c->h_raw.as<uint8_t>() + ho[i], queries[q0 + i], ho[i + 1] - ho[i]);
-        ok = ensure_queries(*c, B, ho[B]) && ensure_outputs(*c, B, stride) &&
-             HIP_CHECK(hipMemcpyAsync(c->d_raw, c->h_raw.p, ho[B], hipMemcpyHostToDevice, c->stream)) &&
-             HIP_CHECK(hipMemcpyAsync(c->d_off, ho, sizeof(uint64_t) * (B + 1), hipMemcpyHostToDevice, c->stream));
-        if (!ok) break;
-        // small batches: one kernel per tier on one stream, and the whole output block read back
-        // with the statistics before the one wait (score()'s latency path)
+        const uint64_t qbytes = ho[B];
+        // small batches (score()'s latency path): one kernel per tier on one stream, the queries
+        // in with one copy and the statistics with the whole output block out with one copy,
+        // all through the context's latency block [statistics | results | offsets, bytes]
         const size_t block = sizeof(uint32_t) * (B + 1 + 2 * (size_t)B * stride);
-        const bool small = B <= kSmallBatch && block <= kSmallBlock;
+        const size_t qspace = sizeof(uint64_t) * (B + 1) + qbytes;
+        const bool small = B <= kSmallBatch && block <= kSmallBlock && qspace <= kSmallQ;
+        const uint8_t* d_raw = c->d_raw;
+        const uint64_t* d_off = c->d_off;
+        uint32_t *d_n = c->d_n, *d_k = c->d_k;
+        float* d_s = c->d_s;
+        if (small) {
+            uint8_t* hq = c->h_sio + kSioStats + kSmallBlock;
+            std::memcpy(hq, ho, sizeof(uint64_t) * (B + 1));
+            for (uint32_t i = 0; i < B; ++i)
+                if (queries[q0 + i])
+                    std::memcpy(hq + sizeof(uint64_t) * (B + 1) + ho[i], queries[q0 + i], ho[i + 1] - ho[i]);
+            uint8_t* dq = c->d_sio + kSioStats + kSmallBlock;
+            d_off = reinterpret_cast<const uint64_t*>(dq);
+            d_raw = dq + sizeof(uint64_t) * (B + 1);
+            d_n = reinterpret_cast<uint32_t*>(c->d_sio + kSioStats);
+            d_k = d_n + B + 1;
+            d_s = reinterpret_cast<float*>(d_k + (size_t)B * stride);
+            ok = HIP_CHECK(hipMemcpyAsync(dq, hq, qspace, hipMemcpyHostToDevice, c->stream));
+        } else {
+            ok = c->h_raw.grow(std::max<uint64_t>(qbytes, 1));
+            if (!ok) break;
+            for (uint32_t i = 0; i < B; ++i)
+                if (queries[q0 + i]) std::memcpy(c->h_raw.as<uint8_t>() + ho[i], queries[q0 + i], ho[i + 1] - ho[i]);
+            ok = ensure_queries(*c, B, qbytes) && ensure_outputs(*c, B, stride) &&
+                 HIP_CHECK(hipMemcpyAsync(c->d_raw, c->h_raw.p, qbytes, hipMemcpyHostToDevice, c->stream)) &&
+                 HIP_CHECK(hipMemcpyAsync(c->d_off, ho, sizeof(uint64_t) * (B + 1), hipMemcpyHostToDevice, c->stream));
+            d_raw = c->d_raw;
+            d_off = c->d_off;
+            d_n = c->d_n;
+            d_k = c->d_k;
+            d_s = c->d_s;
+        }
+        if (!ok) break;
         SearchParams P;
-        ok = queue_search(L, R, *c, c->d_raw, c->d_off, B, ho[B], thr, Lm, (uint32_t)stride, c->d_n, c->d_k, c->d_s,
-                          c->stream, P, small) == 0;
+        ok = queue_search(L, R, *c, d_raw, d_off, B, qbytes, thr, Lm, (uint32_t)stride, d_n, d_k, d_s, c->stream, P,
+                          small) == 0;
         if (!ok) break;
         if (small) {
-            ok = c->h_res.grow(block) &&
-                 HIP_CHECK(hipMemcpyAsync(c->h_res.p, c->d_out, block, hipMemcpyDeviceToHost, c->stream));
+            ok = HIP_CHECK(hipMemcpyAsync(c->h_sio, c->d_sio, kSioStats + block, hipMemcpyDeviceToHost, c->stream));
             if (!ok) break;
         }
-        ok = finish_search(L, R, *c, B, P, c->d_off, c->d_n, c->d_k, c->d_s, c->stream) == 0;
+        ok = finish_search(L, R, *c, B, P, d_off, d_n, d_k, d_s, c->stream, small) == 0;
         if (!ok) break;
-        const uint32_t* counts3 = reinterpret_cast<const uint32_t*>(c->h_stats + kStatSlots);
-        if (small && counts3[0]) {  // the general path ran after the read-back: read again
-            ok = HIP_CHECK(hipMemcpyAsync(c->h_res.p, c->d_out, block, hipMemcpyDeviceToHost, c->stream)) &&
-                 HIP_CHECK(hipStreamSynchronize(c->stream));
-            if (!ok) break;
-        }
         if (small) {
-            const uint32_t* hn = c->h_res.as<uint32_t>();
+            const uint32_t* counts3 = reinterpret_cast<const uint32_t*>(c->h_sio) + kStatSlots * 16;
+            if (counts3[0]) {  // the general path ran after the read-back: read the results again
+                ok = HIP_CHECK(hipMemcpyAsync(c->h_sio + kSioStats, c->d_sio + kSioStats, block,
+                                              hipMemcpyDeviceToHost, c->stream)) &&
+                     HIP_CHECK(hipStreamSynchronize(c->stream));
+                if (!ok) break;
+            }
+            const uint32_t* hn = reinterpret_cast<const uint32_t*>(c->h_sio + kSioStats);
             const uint32_t* hk = hn + B + 1;
             const float* hs = reinterpret_cast<const float*>(hk + (size_t)B * stride);
             for (uint32_t i = 0; i < B; ++i) {

@@ -225,6 +225,10 @@ struct SearchParams {
     // (ngsSearchDevice does not read the batch's byte count back before launching)
     uint64_t qcap;
     uint32_t* oflow;
+    // the latency path: k_prep zeroes these words (the statistics and path counts, which the
+    // tier kernels after it accumulate) in place of a memset launch; null otherwise
+    uint32_t* zero_stats;
+    uint32_t zero_words;
 };
 
 // Tier 1b slices per query (SearchParams.nslices): a full-list or handed-over query is a few
