@@ -35,6 +35,8 @@ constexpr size_t kGeneralBudget = size_t(2) << 30;   // bytes of dense general-p
 constexpr uint32_t kSmallBatch = 16;                 // host batches up to this many queries take the latency path
 constexpr size_t kSmallBlock = size_t(1) << 20;      // ... if their output block is at most this many bytes
 constexpr size_t kPartBudget = size_t(1) << 30;      // bytes of sliced tier-1b partial results per call
+constexpr uint32_t kSmallWaves = 1;                  // ... with this many waves per query (k_wave<W>)
+constexpr uint32_t kSmallSlices = 32;                // ... or term-id slices per query (sliced k_wave<1>)
 constexpr size_t kSmallQ = size_t(64) << 10;         // ... and if their offsets + bytes fit this many bytes
 // the latency path's one block, device and pinned host: statistics | results | queries
 constexpr size_t kSioStats = sizeof(DevStats) * (kStatSlots + 1);
@@ -411,12 +413,7 @@ bool ensure_queries(Context& c, size_t B, size_t bytes) {
 
 // Sliced tier 1b's partial results: B * slices * limit records. Within kPartBudget bytes, else the
 // call runs tier 1b unsliced (returns the slice count to use).
-uint32_t ensure_parts(Context& c, size_t B, uint32_t limit) {
-    static const uint32_t slices = [] {
-        const char* e = std::getenv("NGS_SLICES");
-        const uint32_t v = e ? (uint32_t)std::strtoul(e, nullptr, 0) : kSlices;
-        return std::max<uint32_t>(1, std::min<uint32_t>(v, 16));
-    }();
+uint32_t ensure_parts(Context& c, size_t B, uint32_t limit, uint32_t slices) {
     if (slices <= 1 || limit > kWaveMaxLimit) return 1;
     const size_t need = B * slices * limit;
     if (need * sizeof(uint64_t) > kPartBudget) return 1;
@@ -511,7 +508,12 @@ int queue_search(Library& L, Replica& R, Context& c, const uint8_t* d_raw, const
         const uint32_t w = e ? (uint32_t)std::strtoul(e, nullptr, 0) : kDefaultWaves;
         return w == 0 || w == 1 || w == 2 || w == 4 ? w : kDefaultWaves;
     }();
-    P.waves = small ? 1u : waves;
+    static const uint32_t small_waves = [] {  // waves per query of the latency path
+        const char* e = std::getenv("NGS_SMALL_WAVES");
+        const uint32_t w = e ? (uint32_t)std::strtoul(e, nullptr, 0) : kSmallWaves;
+        return w == 1 || w == 2 || w == 4 ? w : kSmallWaves;
+    }();
+    P.waves = small ? small_waves : waves;
     static const uint32_t heavy_waves = [] {
         const char* e = std::getenv("NGS_HEAVY_WAVES");
         const uint32_t w = e ? (uint32_t)std::strtoul(e, nullptr, 0) : kHeavyWaves;
@@ -531,7 +533,25 @@ int queue_search(Library& L, Replica& R, Context& c, const uint8_t* d_raw, const
     P.esn = c.d_esn;
     P.est = c.d_est;
     P.esc = c.d_esc;
-    P.nslices = small ? 1u : ensure_parts(c, B, P.limit);
+    static const uint32_t list_slices = [] {  // term-id slices of the hand-over / full lists' tier 1b
+        const char* e = std::getenv("NGS_SLICES");
+        const uint32_t v = e ? (uint32_t)std::strtoul(e, nullptr, 0) : kSlices;
+        return std::max<uint32_t>(1, std::min<uint32_t>(v, 16));
+    }();
+    static const uint32_t small_slices = [] {  // ... and of every query of the latency path
+        const char* e = std::getenv("NGS_SMALL_SLICES");
+        const uint32_t v = e ? (uint32_t)std::strtoul(e, nullptr, 0) : kSmallSlices;
+        return std::max<uint32_t>(1, std::min<uint32_t>(v, 64));
+    }();
+    if (small) {
+        // one query's postings over several CUs: a wave per (query, slice of at least 8 skip
+        // buckets), then k_merge; a small library stays on one wave per query
+        const uint32_t sl = std::min<uint32_t>(small_slices, R.dev.n_buckets / 8);
+        P.nslices = sl > 1 ? ensure_parts(c, B, P.limit, sl) : 1u;
+        if (P.nslices > 1) P.waves = 1;
+    } else {
+        P.nslices = ensure_parts(c, B, P.limit, list_slices);
+    }
     P.qcap = c.qcap;
     P.oflow = gc + 6;
     if (small) {

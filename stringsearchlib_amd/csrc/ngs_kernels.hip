@@ -2158,13 +2158,14 @@ __global__ __launch_bounds__(64 * W, kWaveWavesPerSimd) void k_wave(DevIndex X, 
                                                                    const uint32_t* __restrict__ qlist,
                                                                    const uint32_t* __restrict__ qcount) {
     __shared__ WaveSmem<W> S;
-    if (!qlist) {
-        wave_query<W, false>(S, blockIdx.x, X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats,
-                             nullptr, nullptr);
+    const uint32_t nsl = W == 1 && P.nslices > 1 ? P.nslices : 1u;  // sliced: k_merge follows
+    if (!qlist) {  // every query of the batch: a workgroup per (query, slice)
+        const uint32_t q = blockIdx.x / nsl;
+        wave_query<W, false>(S, q, X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats, nullptr,
+                             nullptr, blockIdx.x - q * nsl, nsl);
         return;
     }
     const uint32_t cnt = *qcount;
-    const uint32_t nsl = W == 1 && P.nslices > 1 ? P.nslices : 1u;  // sliced: k_merge follows
     for (uint32_t t = blockIdx.x; t < cnt * nsl; t += gridDim.x) {
         const uint32_t i = t / nsl;
         wave_query<W, false>(S, qlist[i], X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats,
@@ -2309,9 +2310,9 @@ __global__ __launch_bounds__(64) void k_merge(DevIndex X, SearchParams P, const 
                                               DevStats* __restrict__ stats) {
     __shared__ EmitSmem S;
     const uint32_t lane = lane_id(), nsl = P.nslices, L = P.limit;
-    const uint32_t cnt = *qcount;
+    const uint32_t cnt = qlist ? *qcount : P.n_queries;  // no list: every query of the batch
     for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
-        const uint32_t q = qlist[i];
+        const uint32_t q = qlist ? qlist[i] : i;
         const uint32_t* pc = P.pcnt + (size_t)q * nsl;
         if (pc[0] == kNoPart) continue;  // answered by slice 0 directly
         uint32_t cand_n = 0;
@@ -2603,8 +2604,12 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
             break;
         }
         case 1:
-            hipLaunchKernelGGL(k_wave<1>, dim3(P.n_queries), dim3(64), 0, s, X, P, qnorm, off, qm, out_n, out_k,
-                               out_s, list2, count2, stats, (const uint32_t*)nullptr, (const uint32_t*)nullptr);
+            hipLaunchKernelGGL(k_wave<1>, dim3(P.n_queries * std::max<uint32_t>(P.nslices, 1u)), dim3(64), 0, s, X, P,
+                               qnorm, off, qm, out_n, out_k, out_s, list2, count2, stats, (const uint32_t*)nullptr,
+                               (const uint32_t*)nullptr);
+            if (P.nslices > 1)
+                hipLaunchKernelGGL(k_merge, dim3(P.n_queries), dim3(64), 0, s, X, P, (const uint32_t*)nullptr,
+                                   (const uint32_t*)nullptr, out_n, out_k, out_s, stats);
             break;
         case 2:
             hipLaunchKernelGGL(k_wave<2>, dim3(P.n_queries), dim3(128), 0, s, X, P, qnorm, off, qm, out_n, out_k,

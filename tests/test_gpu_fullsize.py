@@ -87,6 +87,17 @@ def assert_same(a, b, where):
         assert k1 == k2 and bits(s1) == bits(s2), f"{where}: {k1!r}|{s1} vs {k2!r}|{s2}"
 
 
+def check_small_batches(h, qs, got, thr, limit, idx, where):
+    """The latency path (batches of <= 16 queries: a wave per (query, term-id slice) and k_merge on
+    a large library) gives the batch path's answers."""
+    for i0 in range(0, len(idx), 16):
+        part = idx[i0:i0 + 16]
+        for i, g in zip(part, gpu_batch(h, [qs[i] for i in part], thr, limit)):
+            assert_same(g, got[i], f"{where} small batch q#{i}")
+    for i in idx[:24]:
+        assert_same(gpu_batch(h, [qs[i]], thr, limit)[0], got[i], f"{where} single q#{i}")
+
+
 def check_properties(res, limit, where):
     assert len(res) <= limit, where
     keys = [k for k, _ in res]
@@ -105,6 +116,7 @@ def test_c2_full_exact():
     ref = oracle_batch(oh, qs, 0.0, 100)
     for i, (g, r) in enumerate(zip(got, ref)):
         assert_same(g, r, f"C2 q#{i} {qs[i]!r}")
+    check_small_batches(h, qs, got, 0.0, 100, list(range(96)), "C2")
     olib().ngo_free(oh)
     _native.lib().dispose(h)
 
@@ -125,6 +137,7 @@ def test_c3_full_sampled_exact_and_properties():
     again = gpu_batch(h, qs[:4096], 0.3, 100)
     for i in range(4096):
         assert_same(again[i], got[i], f"C3 rerun q#{i}")
+    check_small_batches(h, qs, got, 0.3, 100, list(range(B, B + 8)) + list(range(88)), "C3")
     oh = olib().ngo_build(wp, rows, 1, wt)
     sample = sorted(rng.sample(range(len(qs)), 768))
     ref = oracle_batch(oh, [qs[i] for i in sample], 0.3, 100)
