@@ -207,6 +207,8 @@ struct Replica {
             if (!HIP_CHECK(hipEventCreate(&e))) return nullptr;
         if (!dev_alloc(&c->d_group, 64) || !dev_alloc(&c->d_stats, kStatSlots + 1 + 2 * kListSlots) ||
             !dev_alloc(&c->d_sio, kSioBytes) ||
+            !HIP_CHECK(hipMemsetAsync(c->d_sio, 0, kSioStats, c->stream)) ||
+            !HIP_CHECK(hipStreamSynchronize(c->stream)) ||
             !HIP_CHECK(hipHostMalloc((void**)&c->h_sio, kSioBytes, hipHostMallocDefault)) ||
             !HIP_CHECK(hipHostMalloc((void**)&c->h_stats, sizeof(DevStats) * (kStatSlots + 1), hipHostMallocDefault)))
             return nullptr;
@@ -556,7 +558,9 @@ int queue_search(Library& L, Replica& R, Context& c, const uint8_t* d_raw, const
     P.oflow = gc + 6;
     if (small) {
         P.zero_stats = reinterpret_cast<uint32_t*>(sd);
-        P.zero_words = (uint32_t)(kSioStats / sizeof(uint32_t));
+        // the slots this batch's queries add to (q & (kStatSlots - 1), errors in slot 0); the
+        // others stay zero from the block's allocation
+        P.zero_words = (uint32_t)(std::min<size_t>(B, kStatSlots) * sizeof(DevStats) / sizeof(uint32_t));
     }
     P.prec = c.d_prec;
     P.pcnt = c.d_pcnt;

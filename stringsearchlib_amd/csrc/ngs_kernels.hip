@@ -99,8 +99,10 @@ __global__ __launch_bounds__(64) void k_prep(const uint8_t* __restrict__ raw, co
     const uint32_t lane = threadIdx.x, gl = lane & 15u, sh = lane & 48u;
     const uint32_t q = blockIdx.x * 4 + (lane >> 4);
     const bool live = q < B;
-    if (P.zero_stats)  // (the host sized qcap for the batch, so no block sets *oflow meanwhile)
+    if (P.zero_stats) {  // (the host sized qcap for the batch, so no block sets *oflow meanwhile)
         for (uint32_t i = blockIdx.x * 64 + lane; i < P.zero_words; i += gridDim.x * 64) P.zero_stats[i] = 0;
+        if (blockIdx.x == 0 && lane < 16) P.zero_stats[kStatSlots * 16 + lane] = 0;  // the path counts
+    }
     const uint8_t* rq = raw;  // query q: characters of cs bytes from byte offset off[q]
     uint8_t* nq = qnorm;
     uint64_t n = 0;
