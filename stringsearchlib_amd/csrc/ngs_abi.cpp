@@ -233,7 +233,8 @@ struct Library {
     std::atomic<bool> timing{false};
     std::mutex stats_mu;
     ngs_stats last{};
-    bool tk_identity = false;  // DevIndex.tk_identity / w_max, computed once for every replica
+    bool tk_identity = false;  // DevIndex.tk_identity / tk_monotone / w_max, computed once for every replica
+    bool tk_monotone = false;
     float w_max = 0.0f;
 
     ~Library() { reps.clear(); }
@@ -265,6 +266,7 @@ bool upload_replica(Library& L, Replica& R, bool keys_unique) {
     X.n_keys = H.n_keys;
     X.keys_unique = keys_unique ? 1u : 0u;
     X.tk_identity = L.tk_identity ? 1u : 0u;
+    X.tk_monotone = L.tk_monotone ? 1u : 0u;
     X.w_max = L.w_max;
     const std::vector<char>& kb = H.key_bytes;
     uint64_t *gram_off, *term_off, *key_off;
@@ -374,6 +376,23 @@ bool upload(Library& L, const std::vector<int>& devs) {
     // term -> pairs shape and the largest weight (term_pairs in ngs_kernels.hip)
     L.tk_identity = H.tk_off.size() == (size_t)H.n_terms + 1;
     for (size_t t = 0; L.tk_identity && t < H.tk_off.size(); ++t) L.tk_identity = H.tk_off[t] == t;
+    // term ids in key-rank order: every key rank of term t is below every key rank of t + 1
+    // (DevIndex.tk_monotone; the build orders terms by their best key rank, so this fails only
+    // where a key has several terms or a short term's key ranks above a long one's)
+    L.tk_monotone = true;
+    {
+        int64_t prev = -1;
+        for (size_t t = 0; L.tk_monotone && t + 1 < H.tk_off.size(); ++t) {
+            uint32_t lo = UINT32_MAX, hi = 0;
+            for (uint32_t p = H.tk_off[t]; p < H.tk_off[t + 1]; ++p) {
+                lo = std::min(lo, H.tk[p].x);
+                hi = std::max(hi, H.tk[p].x);
+            }
+            if (lo == UINT32_MAX) continue;  // no pair
+            L.tk_monotone = (int64_t)lo > prev;
+            prev = hi;
+        }
+    }
     L.w_max = 0.0f;
     for (const uint2& kw : H.tk) {
         float w;
@@ -1201,8 +1220,10 @@ NGS_API int ngsIndexDigest(uint32_t handle, uint64_t* out, int n) {
     const void* tptrs[8] = {X.term_off, X.term_bytes, X.tk_off, X.tk, X.key_off, X.key_bytes, X.wild_key, X.wild_score};
     for (int i = 0; i < 8; ++i)
         if (!digest(tptrs[i], tsizes[i], vals[8 + i])) return -4;
-    const int m = std::min(n, 16);
-    for (int i = 0; i < m; ++i) out[i] = vals[i];
+    // the shape flags the kernels branch on
+    const uint64_t flags = (X.keys_unique ? 1u : 0u) | (X.tk_identity ? 2u : 0u) | (X.tk_monotone ? 4u : 0u);
+    const int m = std::min(n, 17);
+    for (int i = 0; i < m; ++i) out[i] = i < 16 ? vals[i] : flags;
     return m;
 }
 

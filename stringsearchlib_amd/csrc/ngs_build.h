@@ -3,6 +3,9 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+#include <cstring>
+
 #include "ngs_common.h"
 
 namespace ngs {
@@ -22,6 +25,19 @@ hipError_t build_grams_device(const uint64_t* term_off, const uint8_t* term_byte
                               uint32_t n_terms, DeviceGrams& out);
 
 struct HostIndex;
+
+// Term ids within each class (short, long) follow first appearance, or with NGS_TERM_ORDER=rank
+// the terms' best key rank first (both builds read it). The rank order makes DevIndex.tk_monotone
+// hold, so tier 1b stops counting one-hit terms exactly once its top-L is full of them: C2
+// (thr 0) 8.8 -> 14.7 Mq/s; but it groups the terms by key length, which skews the skip buckets'
+// posting mass and the sketch candidates of the lean kernel: C3 29.1 -> 20.2 Mq/s.
+inline bool term_order_by_rank() {
+    static const bool r = [] {
+        const char* e = std::getenv("NGS_TERM_ORDER");
+        return e && std::strcmp(e, "rank") == 0;
+    }();
+    return r;
+}
 
 // String interning, term ids, key ranks, the term -> key CSR and the wildcard weights of an index
 // on the current device (ngs_intern.hip), into the host index (ix.csize, short_term_len set by the

@@ -187,6 +187,8 @@ struct DevIndex {  // passed by value to kernels; all pointers are device pointe
                                 // share a key and the top-L needs no key dedup pass
     uint32_t tk_identity;       // 1: term t's pairs are exactly tk[t] (tk_off[t] == t): one load less
     float w_max;                // largest pair weight (<= 0: none positive); bounds a term's best score
+    uint32_t tk_monotone;       // 1: term ids ascend with key rank (all of t's below all of t + 1's):
+                                // a term loses every score tie against the records of lower terms
     // gram size and character width (indexG / indexW extensions; 3 and 1 for indexN)
     uint32_t gsz, csize, gram_mode;         // gram_mode 1: grams via the dictionary below
     uint32_t short_query_len, full_scan_len; // 3g and g (nGramSearch.hpp:381, :247)

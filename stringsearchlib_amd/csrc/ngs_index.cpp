@@ -450,16 +450,29 @@ static void build_impl(HostIndex& ix, const CharT* const* words, uint64_t size, 
         ix.key_off[ix.n_keys] = o;
     }
 
-    // term ids: shortLib first (hpp:82-85), each class in first-appearance order
+    // term ids: shortLib first (hpp:82-85), each class in first-appearance order, or by the terms'
+    // best key rank first (term_order_by_rank(), ngs_build.h; the reference's ids are internal)
     ix.n_terms = terms.size();
     std::vector<uint32_t> tmap(ix.n_terms);
     {
+        std::vector<uint32_t> minrank(ix.n_terms, UINT32_MAX);
+        if (term_order_by_rank())
+            for (const Pair& p : pairs) minrank[p.term] = std::min(minrank[p.term], krank[p.key]);
+        std::vector<uint32_t> ord(ix.n_terms);
+        for (uint32_t t = 0; t < ix.n_terms; ++t) ord[t] = t;
+        auto is_long = [&](uint32_t t) { return terms.len(t) / cs >= ix.short_term_len; };
+        std::sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) {
+            const bool la = is_long(a), lb = is_long(b);
+            if (la != lb) return lb;
+            if (minrank[a] != minrank[b]) return minrank[a] < minrank[b];
+            return a < b;
+        });
         uint32_t s = 0;
-        for (uint32_t t = 0; t < ix.n_terms; ++t)
-            if (terms.len(t) / cs < ix.short_term_len) tmap[t] = s++;
+        for (uint32_t r = 0; r < ix.n_terms; ++r) {
+            tmap[ord[r]] = r;
+            if (!is_long(ord[r])) s = r + 1;
+        }
         ix.n_short = s;
-        for (uint32_t t = 0; t < ix.n_terms; ++t)
-            if (terms.len(t) / cs >= ix.short_term_len) tmap[t] = s++;
         std::vector<uint32_t> inv(ix.n_terms);
         for (uint32_t t = 0; t < ix.n_terms; ++t) inv[tmap[t]] = t;
         ix.term_off.resize((size_t)ix.n_terms + 1);

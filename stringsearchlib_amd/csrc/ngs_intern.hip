@@ -12,7 +12,8 @@
 //                (term, key) pair, term hash
 //   3. terms     valid words sorted by (hash, word): equal-hash runs are one term (every member is
 //                compared with the run head: a 64-bit collision falls back to the host build);
-//                term ids = runs sorted by (long?, first word)
+//                term ids = runs sorted by (long?, first word), or (long?, best key rank of the
+//                term's words, first word) with term_order_by_rank() (after step 4)
 //   4. keys      rows with a valid pair sorted by (key hash, row): runs are keys; ranks = runs
 //                sorted by (length, first row) — the ScoreComparer tie-break (h:262-269) plus
 //                first appearance
@@ -44,7 +45,9 @@ namespace {
 
 constexpr uint32_t kInternCollision = 1u;  // two different strings with one 64-bit hash
 constexpr uint32_t kInternNaN = 2u;        // a NaN weight (host semantics: first-seen NaN sticks)
-constexpr uint64_t kLongBit = 1ull << 40;  // term order key: long terms after short ones
+constexpr uint64_t kKeyLenBit = 1ull << 40;      // key order key: (length << 40) | row
+constexpr uint64_t kTermLongBit = 1ull << 63;    // term order key: long? | best key rank << 31 | first word
+constexpr uint64_t kTermItemMask = (1ull << 31) - 1;
 
 __device__ __forceinline__ bool d_space(uint32_t c) { return c == 32u || (c >= 9u && c <= 13u); }
 
@@ -189,14 +192,24 @@ __global__ __launch_bounds__(256) void k_check(const uint32_t* __restrict__ idx,
         }
 }
 
-// order keys of the runs: terms (long?, first word), keys (length, first row)
+// the best (smallest) key rank among each term run's words
+__global__ __launch_bounds__(256) void k_term_minrank(const uint32_t* __restrict__ idx, const uint32_t* __restrict__ seg,
+                                                      uint32_t n, uint32_t rowSize,
+                                                      const uint32_t* __restrict__ key_of_row,
+                                                      uint32_t* __restrict__ minr) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < n) atomicMin(&minr[seg[p]], key_of_row[idx[p] / rowSize]);
+}
+
+// order keys of the runs: terms (long?, best key rank, first word), keys (length, first row)
 __global__ __launch_bounds__(256) void k_term_order(const uint32_t* __restrict__ idx, const uint32_t* __restrict__ hpos,
                                                     uint32_t nruns, const uint32_t* __restrict__ tlen, uint32_t long_len,
-                                                    uint64_t* __restrict__ okey, uint32_t* __restrict__ oval) {
+                                                    const uint32_t* __restrict__ minr, uint64_t* __restrict__ okey,
+                                                    uint32_t* __restrict__ oval) {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= nruns) return;
-    const uint32_t j = idx[hpos[s]];
-    okey[s] = (tlen[j] >= long_len ? kLongBit : 0ull) | j;
+    const uint32_t j = idx[hpos[s]];  // < 2^31 (larger builds stay on the host)
+    okey[s] = (tlen[j] >= long_len ? kTermLongBit : 0ull) | ((uint64_t)minr[s] << 31) | j;
     oval[s] = s;
 }
 
@@ -211,15 +224,15 @@ __global__ __launch_bounds__(256) void k_key_order(const uint32_t* __restrict__ 
 }
 
 // rank of every run (its position in the order), the head item of every rank, and the number of
-// short terms (okey below kLongBit)
+// short terms (order keys below long_bit)
 __global__ __launch_bounds__(256) void k_ranks(const uint64_t* __restrict__ okey_sorted, const uint32_t* __restrict__ oval_sorted,
-                                               uint32_t n, uint32_t* __restrict__ rank_of_run,
+                                               uint32_t n, uint64_t long_bit, uint32_t* __restrict__ rank_of_run,
                                                uint32_t* __restrict__ n_short) {
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= n) return;
     rank_of_run[oval_sorted[r]] = r;
-    const bool lng = okey_sorted[r] >= kLongBit;
-    if (lng && (r == 0 || okey_sorted[r - 1] < kLongBit)) *n_short = r;
+    const bool lng = okey_sorted[r] >= long_bit;
+    if (lng && (r == 0 || okey_sorted[r - 1] < long_bit)) *n_short = r;
 }
 
 // item -> rank of its run (items: the sorted index list)
@@ -232,7 +245,7 @@ __global__ __launch_bounds__(256) void k_item_rank(const uint32_t* __restrict__ 
 
 // per rank: the head item and its length (+ extra: the key's NUL)
 __global__ __launch_bounds__(256) void k_rank_items(const uint64_t* __restrict__ okey_sorted, uint32_t n,
-                                                    const uint32_t* __restrict__ len, uint32_t extra,
+                                                    uint64_t item_mask, const uint32_t* __restrict__ len, uint32_t extra,
                                                     uint32_t* __restrict__ item, uint64_t* __restrict__ rlen) {
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r > n) return;
@@ -240,7 +253,7 @@ __global__ __launch_bounds__(256) void k_rank_items(const uint64_t* __restrict__
         rlen[r] = 0;
         return;
     }
-    const uint32_t it = (uint32_t)(okey_sorted[r] & (kLongBit - 1));
+    const uint32_t it = (uint32_t)(okey_sorted[r] & item_mask);
     item[r] = it;
     rlen[r] = (uint64_t)len[it] + extra;
 }
@@ -501,38 +514,6 @@ hipError_t intern_impl(HostIndex& ix, const CharT* const* words, uint64_t size, 
     TRY(runs_of(d_hs, V_n, d_head, d_seg, d_hpos, tmp, nullptr, n_terms));
     hipLaunchKernelGGL(k_check<CharT>, blocks(V_n), dim3(256), 0, nullptr, d_sj, d_seg, d_hpos, V_n, d_nblob, d_woff,
                        (const uint32_t*)nullptr, d_tlen, d_err);
-    uint64_t *d_ok, *d_oks;
-    uint32_t *d_ov, *d_ovs, *d_rank, *d_nshort, *d_term_of_word;
-    TRY(A.get(&d_ok, n_terms));
-    TRY(A.get(&d_oks, n_terms));
-    TRY(A.get(&d_ov, n_terms));
-    TRY(A.get(&d_ovs, n_terms));
-    TRY(A.get(&d_rank, n_terms));
-    TRY(A.get(&d_nshort, 1));
-    TRY(A.get(&d_term_of_word, size));
-    hipLaunchKernelGGL(k_term_order, blocks(n_terms), dim3(256), 0, nullptr, d_sj, d_hpos, n_terms, d_tlen,
-                       ix.short_term_len, d_ok, d_ov);
-    TRY(sort_pairs(d_ok, d_oks, d_ov, d_ovs, n_terms, 41, tmp));
-    TRY(hipMemcpy(d_nshort, &n_terms, sizeof(uint32_t), hipMemcpyHostToDevice));  // all short unless a long one is found
-    hipLaunchKernelGGL(k_ranks, blocks(n_terms), dim3(256), 0, nullptr, d_oks, d_ovs, n_terms, d_rank, d_nshort);
-    hipLaunchKernelGGL(k_item_rank, blocks(V_n), dim3(256), 0, nullptr, d_sj, d_seg, d_rank, V_n, d_term_of_word);
-    // term layout: lengths by id -> offsets -> characters
-    uint32_t* d_titem;
-    uint64_t *d_tl64, *d_toff;
-    char* d_tbytes;
-    TRY(A.get(&d_titem, n_terms));
-    TRY(A.get(&d_tl64, n_terms + 1));
-    TRY(A.get(&d_toff, n_terms + 1));
-    hipLaunchKernelGGL(k_rank_items, blocks(n_terms + 1), dim3(256), 0, nullptr, d_oks, n_terms, d_tlen, 0u, d_titem,
-                       d_tl64);
-    TRY(excl_scan(d_tl64, d_toff, n_terms + 1, tmp));
-    uint64_t tchars = 0;
-    TRY(hipMemcpy(&tchars, d_toff + n_terms, sizeof(uint64_t), hipMemcpyDeviceToHost));
-    TRY(A.get(&d_tbytes, std::max<uint64_t>(tchars, 1) * cs));
-    hipLaunchKernelGGL(k_layout<CharT>, blocks(n_terms), dim3(256), 0, nullptr, d_titem, n_terms, d_nblob, d_woff,
-                       (const uint32_t*)nullptr, d_tlen, d_toff, reinterpret_cast<CharT*>(d_tbytes), false);
-    TRY(hipGetLastError());
-
     // ---- 4. keys: rows with a valid pair ----
     uint32_t *d_rflag, *d_rpos, *d_vr;
     TRY(A.get(&d_rflag, nrows + 1));
@@ -577,7 +558,8 @@ hipError_t intern_impl(HostIndex& ix, const CharT* const* words, uint64_t size, 
     TRY(A.get(&d_dummy, 1));
     hipLaunchKernelGGL(k_key_order, blocks(n_keys), dim3(256), 0, nullptr, d_sr, d_khpos, n_keys, d_kl, d_kok, d_kov);
     TRY(sort_pairs(d_kok, d_koks, d_kov, d_kovs, n_keys, 64, tmp));
-    hipLaunchKernelGGL(k_ranks, blocks(n_keys), dim3(256), 0, nullptr, d_koks, d_kovs, n_keys, d_krank, d_dummy);
+    hipLaunchKernelGGL(k_ranks, blocks(n_keys), dim3(256), 0, nullptr, d_koks, d_kovs, n_keys, kKeyLenBit, d_krank,
+                       d_dummy);
     hipLaunchKernelGGL(k_item_rank, blocks(R_n), dim3(256), 0, nullptr, d_sr, d_kseg, d_krank, R_n, d_key_of_row);
     uint32_t* d_kitem;
     uint64_t *d_kl64, *d_koff;
@@ -586,13 +568,55 @@ hipError_t intern_impl(HostIndex& ix, const CharT* const* words, uint64_t size, 
     TRY(A.get(&d_kl64, n_keys + 1));
     TRY(A.get(&d_koff, n_keys + 1));
     // key order key = (length << 40) | row: the item is the row
-    hipLaunchKernelGGL(k_rank_items, blocks(n_keys + 1), dim3(256), 0, nullptr, d_koks, n_keys, d_kl, 1u, d_kitem, d_kl64);
+    hipLaunchKernelGGL(k_rank_items, blocks(n_keys + 1), dim3(256), 0, nullptr, d_koks, n_keys, kKeyLenBit - 1, d_kl, 1u,
+                       d_kitem, d_kl64);
     TRY(excl_scan(d_kl64, d_koff, n_keys + 1, tmp));
     uint64_t kchars = 0;
     TRY(hipMemcpy(&kchars, d_koff + n_keys, sizeof(uint64_t), hipMemcpyDeviceToHost));
     TRY(A.get(&d_kbytes, std::max<uint64_t>(kchars, 1) * cs));
     hipLaunchKernelGGL(k_layout<CharT>, blocks(n_keys), dim3(256), 0, nullptr, d_kitem, n_keys, d_blob, d_rowoff, d_ka,
                        d_kl, d_koff, reinterpret_cast<CharT*>(d_kbytes), true);
+    TRY(hipGetLastError());
+
+    // ---- 3b. term ids: by (long?, first word) or (long?, best key rank, first word) ----
+    uint64_t *d_ok, *d_oks;
+    uint32_t *d_ov, *d_ovs, *d_rank, *d_nshort, *d_term_of_word;
+    TRY(A.get(&d_ok, n_terms));
+    TRY(A.get(&d_oks, n_terms));
+    TRY(A.get(&d_ov, n_terms));
+    TRY(A.get(&d_ovs, n_terms));
+    TRY(A.get(&d_rank, n_terms));
+    TRY(A.get(&d_nshort, 1));
+    TRY(A.get(&d_term_of_word, size));
+    uint32_t* d_minr;
+    TRY(A.get(&d_minr, n_terms));
+    const bool by_rank = term_order_by_rank();
+    TRY(hipMemset(d_minr, by_rank ? 0xFF : 0, n_terms * sizeof(uint32_t)));
+    if (by_rank)
+        hipLaunchKernelGGL(k_term_minrank, blocks(V_n), dim3(256), 0, nullptr, d_sj, d_seg, V_n, (uint32_t)rowSize,
+                           d_key_of_row, d_minr);
+    hipLaunchKernelGGL(k_term_order, blocks(n_terms), dim3(256), 0, nullptr, d_sj, d_hpos, n_terms, d_tlen,
+                       ix.short_term_len, d_minr, d_ok, d_ov);
+    TRY(sort_pairs(d_ok, d_oks, d_ov, d_ovs, n_terms, 64, tmp));
+    TRY(hipMemcpy(d_nshort, &n_terms, sizeof(uint32_t), hipMemcpyHostToDevice));  // all short unless a long one is found
+    hipLaunchKernelGGL(k_ranks, blocks(n_terms), dim3(256), 0, nullptr, d_oks, d_ovs, n_terms, kTermLongBit, d_rank,
+                       d_nshort);
+    hipLaunchKernelGGL(k_item_rank, blocks(V_n), dim3(256), 0, nullptr, d_sj, d_seg, d_rank, V_n, d_term_of_word);
+    // term layout: lengths by id -> offsets -> characters
+    uint32_t* d_titem;
+    uint64_t *d_tl64, *d_toff;
+    char* d_tbytes;
+    TRY(A.get(&d_titem, n_terms));
+    TRY(A.get(&d_tl64, n_terms + 1));
+    TRY(A.get(&d_toff, n_terms + 1));
+    hipLaunchKernelGGL(k_rank_items, blocks(n_terms + 1), dim3(256), 0, nullptr, d_oks, n_terms, kTermItemMask, d_tlen,
+                       0u, d_titem, d_tl64);
+    TRY(excl_scan(d_tl64, d_toff, n_terms + 1, tmp));
+    uint64_t tchars = 0;
+    TRY(hipMemcpy(&tchars, d_toff + n_terms, sizeof(uint64_t), hipMemcpyDeviceToHost));
+    TRY(A.get(&d_tbytes, std::max<uint64_t>(tchars, 1) * cs));
+    hipLaunchKernelGGL(k_layout<CharT>, blocks(n_terms), dim3(256), 0, nullptr, d_titem, n_terms, d_nblob, d_woff,
+                       (const uint32_t*)nullptr, d_tlen, d_toff, reinterpret_cast<CharT*>(d_tbytes), false);
     TRY(hipGetLastError());
 
     // ---- 5. pairs ----

@@ -1011,6 +1011,36 @@ __device__ void wave_flush(SM& S, uint32_t& cand_n, uint64_t& tau, uint32_t L, b
     wave_sync();
 }
 
+// (defined below)
+template <class SM>
+__device__ void wave_emit(SM& S, const DevIndex& X, const SearchParams& P, uint32_t m, uint32_t L,
+                          float sc_long, float sc_short, uint32_t& surv_n, uint32_t& cand_n, uint64_t& tau);
+
+// The smallest hit count a term of the next part needs to enter the running top-L (>= cmin). A
+// count-c term scores at most max(w_max * c / n, 0) in fp32 (term_pairs' bound), so once the top-L
+// is full every count whose bound encodes below tau's score is out; with DevIndex.tk_monotone also
+// the count whose bound ties it: a later part's terms have larger ids, hence larger key ranks than
+// every record so far, and lose the tie (ScoreComparer, nGramSearch.h:262-269). A count that can
+// be an exact match (s > 0.999, promoted to 100) is never excluded. At thr 0 (cmin 1) on a large
+// library this turns the exact counting of every posting into the sketch at cmin 2 after the
+// first parts have filled the top-L with one-hit records of the shortest keys.
+template <class SM>
+__device__ uint32_t raised_cmin(SM& S, const DevIndex& X, const SearchParams& P, uint32_t m, uint32_t n, uint32_t L,
+                                uint32_t cmin, float sc_long, float sc_short, uint32_t& surv_n, uint32_t& cand_n,
+                                uint64_t& tau) {
+    if (tau == kNoCand && cand_n + surv_n >= L) {  // full enough: settle tau now
+        if (surv_n) wave_emit(S, X, P, m, L, sc_long, sc_short, surv_n, cand_n, tau);
+        if (tau == kNoCand && cand_n >= L) wave_flush(S, cand_n, tau, L, X.keys_unique != 0);
+    }
+    if (tau == kNoCand) return cmin;
+    const uint32_t lane = lane_id(), te = ~(uint32_t)(tau >> 32);
+    const float ub = X.w_max * sc_long;  // lane c: the bound of c hits
+    const uint32_t ue = ub > 0.0f ? __float_as_uint(ub) + 1u : 1u;
+    const bool out = lane >= 1 && lane <= n && !((double)sc_long > 0.999) && (ue < te || (X.tk_monotone && ue == te));
+    const unsigned long long om = __ballot(out);  // a prefix of the counts: the bound grows with c
+    return max(cmin, om ? 64u - (uint32_t)__clzll((long long)om) : 0u);
+}
+
 // calcScore (nGramSearch.hpp:310-341) over the survivor list: term -> (key, weight) pairs,
 // max(w*s, 0), exact-match promotion, into the running top-L.
 template <class SM>
@@ -1728,7 +1758,15 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
                     } else if constexpr (LEAN && kLeanCandInTable) { bail(); return; }
                     else wave_emit(S, X, P, m, L, sc_long, sc_short, surv_n, cand_n, tau);
                 }
-                const uint32_t nc = sketch ? part_sketch(S, cv, c_vm, c_mt, cmin, X.n_short, X.n_terms, surv_n, P.dbg) : 65u;
+                // the count this part must reach: cmin, raised once the running top-L is full and
+                // a term of fewer hits could not enter it (tier 1b, one wave)
+                uint32_t ceff = cmin;
+                if constexpr (!LEAN && W == 1) {
+                    if (!(P.dbg & 128u)) ceff = raised_cmin(S, X, P, m, n, L, cmin, sc_long, sc_short, surv_n, cand_n, tau);
+                }
+                // (survivors must pass the threshold exactly: no sketch past its u4 range)
+                const bool sk = ceff >= kSketchMinCmin && ceff <= kSketchMax;
+                const uint32_t nc = sk ? part_sketch(S, cv, c_vm, c_mt, ceff, X.n_short, X.n_terms, surv_n, P.dbg) : 65u;
                 const bool done = nc <= 64;
                 WCOUNT(11, 1);
                 WCOUNT(12, done ? 0 : 1);
@@ -1765,7 +1803,7 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
                             if (cnt <= (uint32_t)TableGeom<LEAN>::kCap || tb - ta <= 1) break;
                             tb = ta + (tb - ta) / 2;
                         }
-                        part_exact(S, cv, c_vm, c_mt, ta, tb, pass++, X, P, m, L, cmin, sc_long, sc_short, surv_n,
+                        part_exact(S, cv, c_vm, c_mt, ta, tb, pass++, X, P, m, L, ceff, sc_long, sc_short, surv_n,
                                    cand_n, tau, err);
                         ta = tb;
                     }

@@ -22,8 +22,8 @@ pytestmark = pytest.mark.gpu
 
 
 def _digest(idx):
-    out = (C.c_uint64 * 16)()
-    assert _native.lib().ngsIndexDigest(idx.handle, out, 16) == 16
+    out = (C.c_uint64 * 17)()
+    assert _native.lib().ngsIndexDigest(idx.handle, out, 17) == 17
     return list(out)
 
 
