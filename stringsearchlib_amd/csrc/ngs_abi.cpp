@@ -92,6 +92,7 @@ struct Context {
     hipStream_t side = nullptr;      // the heavy list (cmin 2) beside tier 1a
     hipStream_t side2 = nullptr;     // tier 1b on the full list (cmin 1, short search) beside both
     hipEvent_t fork = nullptr, join = nullptr, join2 = nullptr;
+    hipEvent_t prep_ev = nullptr, lists_ev = nullptr;  // k_prep done (s), heavy / full lists merged (side)
     hipEvent_t ev[6] = {};
     size_t qcap = 0, bcap = 0, ncap = 0, ocap = 0;
     uint8_t* d_raw = nullptr;
@@ -148,7 +149,7 @@ struct Context {
         if (h_sio) hipHostFree(h_sio);
         for (hipEvent_t e : ev)
             if (e) hipEventDestroy(e);
-        for (hipEvent_t e : {fork, join, join2})
+        for (hipEvent_t e : {fork, join, join2, prep_ev, lists_ev})
             if (e) hipEventDestroy(e);
         if (stream) hipStreamDestroy(stream);
         if (side) hipStreamDestroy(side);
@@ -201,7 +202,9 @@ struct Replica {
             !HIP_CHECK(make_side_stream(&c->side)) || !HIP_CHECK(make_side_stream(&c->side2)) ||
             !HIP_CHECK(hipEventCreateWithFlags(&c->fork, hipEventDisableTiming)) ||
             !HIP_CHECK(hipEventCreateWithFlags(&c->join, hipEventDisableTiming)) ||
-            !HIP_CHECK(hipEventCreateWithFlags(&c->join2, hipEventDisableTiming)))
+            !HIP_CHECK(hipEventCreateWithFlags(&c->join2, hipEventDisableTiming)) ||
+            !HIP_CHECK(hipEventCreateWithFlags(&c->prep_ev, hipEventDisableTiming)) ||
+            !HIP_CHECK(hipEventCreateWithFlags(&c->lists_ev, hipEventDisableTiming)))
             return nullptr;
         for (hipEvent_t& e : c->ev)
             if (!HIP_CHECK(hipEventCreate(&e))) return nullptr;
@@ -589,13 +592,13 @@ int queue_search(Library& L, Replica& R, Context& c, const uint8_t* d_raw, const
         return -4;
     if (timing) HIP_CHECK(hipEventRecord(c.ev[0], s));
     if (!HIP_CHECK(launch_prep(d_raw, d_off, B, P, c.d_norm, c.d_qm, R.dev.csize, R.dev, c.d_heavy, gc + 3, c.d_full,
-                               gc + 5, c.d_lslots, c.d_lctr, s)))
+                               gc + 5, c.d_lslots, c.d_lctr, s, c.side, c.prep_ev, c.lists_ev)))
         return -4;
     if (timing) HIP_CHECK(hipEventRecord(c.ev[1], s));
     if (timing) HIP_CHECK(hipEventRecord(c.ev[2], s));
     if (!HIP_CHECK(launch_fast(R.dev, P, c.d_norm, d_off, c.d_qm, d_n, d_k, d_s, c.d_list2, gc + 1, c.d_fb, gc + 2,
                                c.d_fb2, gc + 4, c.d_heavy, gc + 3, c.d_full, gc + 5, c.d_glist, gc, sd, s, c.side,
-                               c.side2, c.fork, c.join, c.join2)))
+                               c.side2, c.fork, c.join, c.join2, c.lists_ev)))
         return -4;
     if (timing) HIP_CHECK(hipEventRecord(c.ev[3], s));
     // the statistics and the path counts in one read-back (the general path adds no statistics)

@@ -11,11 +11,12 @@ namespace ngs {
 // qnorm (same offsets as the raw bytes) and its length into qm (kQueryWildcard for ""/"*").
 // The heavy and full lists (tier-1 routing) go through 2 x kListSlots slot lists: `slots` holds
 // 2 * kListSlots * ceil(B / kListSlots) entries, `ctr` 2 * kListSlots counters 16 words apart
-// (zeroed by the caller).
+// (zeroed by the caller). The lists are merged on `side` after an event on s (prep_ev), so the
+// main tier-1a launch queued next on s does not wait for them; lists_ev marks them done.
 hipError_t launch_prep(const uint8_t* raw, const uint64_t* off, uint32_t B, const SearchParams& P,
                        uint8_t* qnorm, uint32_t* qm, uint32_t cs, const DevIndex& X, uint32_t* heavy,
                        uint32_t* hcount, uint32_t* full, uint32_t* fcount, uint32_t* slots, uint32_t* ctr,
-                       hipStream_t s);
+                       hipStream_t s, hipStream_t side, hipEvent_t prep_ev, hipEvent_t lists_ev);
 
 // Fused per-query kernel: short Levenshtein scan of shortLib (4 <= m < 9), 3-gram posting
 // count in an LDS hash table per term-id part, threshold, term->key weighting, per-key max
@@ -27,7 +28,8 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
                        uint32_t* count2, uint32_t* fb, uint32_t* fbc, uint32_t* fb2, uint32_t* fbc2,
                        const uint32_t* heavy, const uint32_t* hcount, const uint32_t* full,
                        const uint32_t* fcount, uint32_t* glist, uint32_t* gcount, DevStats* stats, hipStream_t s,
-                       hipStream_t side, hipStream_t side2, hipEvent_t fork, hipEvent_t join, hipEvent_t join2);
+                       hipStream_t side, hipStream_t side2, hipEvent_t fork, hipEvent_t join, hipEvent_t join2,
+                       hipEvent_t lists_ev);
 
 // Result compaction for the host entry points: pos[0..B] = exclusive prefix sum of n[0..B) (n
 // holds B + 1 entries, n[B] = 0), then query q's n[q] records (k, s at q * stride) are copied to

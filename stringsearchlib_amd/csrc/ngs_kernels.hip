@@ -2561,13 +2561,20 @@ __global__ __launch_bounds__(256) void k_lists(const uint32_t* __restrict__ slot
 
 hipError_t launch_prep(const uint8_t* raw, const uint64_t* off, uint32_t B, const SearchParams& P, uint8_t* qnorm,
                        uint32_t* qm, uint32_t cs, const DevIndex& X, uint32_t* heavy, uint32_t* hcount,
-                       uint32_t* full, uint32_t* fcount, uint32_t* slots, uint32_t* ctr, hipStream_t s) {
+                       uint32_t* full, uint32_t* fcount, uint32_t* slots, uint32_t* ctr, hipStream_t s,
+                       hipStream_t side, hipEvent_t prep_ev, hipEvent_t lists_ev) {
     if (!B) return hipSuccess;
     const uint32_t cap = (B + kListSlots - 1) / kListSlots;
     const bool lists = P.waves == 0;
     hipLaunchKernelGGL(k_prep, dim3((B + 3) / 4), dim3(64), 0, s, raw, off, B, P, qnorm, qm, cs, X,
                        lists ? slots : nullptr, ctr, cap);
-    if (lists) hipLaunchKernelGGL(k_lists, dim3(1), dim3(256), 0, s, slots, ctr, cap, heavy, hcount, full, fcount);
+    if (lists) {  // on the side stream: the main tier-1a launch needs only k_prep's output
+        hipError_t e;
+        if ((e = hipEventRecord(prep_ev, s)) != hipSuccess || (e = hipStreamWaitEvent(side, prep_ev, 0)) != hipSuccess)
+            return e;
+        hipLaunchKernelGGL(k_lists, dim3(1), dim3(256), 0, side, slots, ctr, cap, heavy, hcount, full, fcount);
+        if ((e = hipEventRecord(lists_ev, side)) != hipSuccess) return e;
+    }
     return hipGetLastError();
 }
 
@@ -2576,7 +2583,8 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
                        uint32_t* count2, uint32_t* fb, uint32_t* fbc, uint32_t* fb2, uint32_t* fbc2,
                        const uint32_t* heavy, const uint32_t* hcount, const uint32_t* full,
                        const uint32_t* fcount, uint32_t* glist, uint32_t* gcount, DevStats* stats, hipStream_t s,
-                       hipStream_t side, hipStream_t side2, hipEvent_t fork, hipEvent_t join, hipEvent_t join2) {
+                       hipStream_t side, hipStream_t side2, hipEvent_t fork, hipEvent_t join, hipEvent_t join2,
+                       hipEvent_t lists_ev) {
     if (!P.n_queries) return hipSuccess;
     hipError_t e = hipSuccess;
     switch (P.waves) {  // waves per query (SearchParams.waves, NGS_WAVES; 0 = tier 1a + 1b)
@@ -2597,7 +2605,8 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
             // the main launch is queued first: the GPU idled ~35 us while the host queued the side
             // streams' launches ahead of it
             if (kMainFirst) main_lean();
-            if ((e = hipStreamWaitEvent(side, fork, 0)) != hipSuccess || (e = hipStreamWaitEvent(side2, fork, 0)) != hipSuccess)
+            // side: k_lists is already queued there (launch_prep); side2 waits for the lists
+            if ((e = hipStreamWaitEvent(side, fork, 0)) != hipSuccess || (e = hipStreamWaitEvent(side2, lists_ev, 0)) != hipSuccess)
                 return e;
             if (P.heavy_waves == 4)
                 hipLaunchKernelGGL(k_wave<4>, dim3(gh), dim3(256), 0, side2, X, P, qnorm, off, qm, out_n, out_k,
