@@ -129,6 +129,11 @@ constexpr bool kMainFirst = NGS_MAIN_FIRST != 0;  // queue the main tier-1a laun
 #define NGS_SKIP_COLD 1
 #endif
 constexpr bool kSkipCold = NGS_SKIP_COLD != 0;  // skip the sketch candidate pass when no cell reached cmin
+#ifndef NGS_SKETCH_LOOSE
+#define NGS_SKETCH_LOOSE 1
+#endif
+// one-wave sketch add pass without per-entry mask bits (segment-edge entries counted too)
+constexpr bool kSketchLoose = NGS_SKETCH_LOOSE != 0;
 constexpr uint32_t kListSlots = 64;             // slot lists per routing list in k_prep
 constexpr uint32_t kNoEmit = 0xFFFFFFFFu;       // esn[q]: query not finished by tier 1a
 constexpr uint32_t kEmitHeavy = 0x80000000u;    // esn[q] flag: finished by the heavy-list launch

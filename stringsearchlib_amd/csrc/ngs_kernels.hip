@@ -1323,19 +1323,41 @@ __device__ __forceinline__ uint32_t part_sketch(WaveSmem<W, LEAN>& S, const uint
     // at >= cmin had exactly one such add in this part: the table starts clear and adds are 0/1)
     bool ovf = false, hot = false;
     const uint32_t cm1 = __builtin_amdgcn_readfirstlane(cmin - 1u);
+    if constexpr (kSketchLoose && W == 1) {
+        // the add pass also counts the <= 3 entries of neighbouring lists at each segment edge
+        // (never an undercount; the candidate pass below masks them out), so an add needs no
+        // per-entry mask bit, and one running max of the counters it saw stands for both tests:
+        // >= cmin - 1 (an add reached cmin: candidates) and == 15 (a counter wrapped)
+        uint32_t seen = 0;
 #pragma unroll
-    for (uint32_t r = 0; r < (uint32_t)NR; ++r) {
-        if (64 * r < mt) {
-            const uint32_t t[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
-            // (issuing the four returning adds together, one wait, was measured no faster: the
-            // other waves of the SIMD already cover the LDS latency)
+        for (uint32_t r = 0; r < (uint32_t)NR; ++r) {
+            if (64 * r < mt && 64 * r + lane < mt) {
+                const uint32_t t[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
 #pragma unroll
-            for (uint32_t e = 0; e < 4; ++e) {
-                const uint32_t sh4 = sketch_sh4<W, LEAN>(t[e]);
-                const uint32_t old = atomicAdd(sketch_word<W, LEAN>(S.table, t[e]), ((vmask >> (4 * r + e)) & 1u) << (sh4 & 31u));
-                const uint32_t on = __builtin_amdgcn_ubfe(old, sh4, 4u);
-                ovf |= on == kSketchMax;
-                if constexpr (kSkipCold && W == 1) hot |= on == cm1;
+                for (uint32_t e = 0; e < 4; ++e) {
+                    const uint32_t sh4 = sketch_sh4<W, LEAN>(t[e]);
+                    const uint32_t old = atomicAdd(sketch_word<W, LEAN>(S.table, t[e]), 1u << (sh4 & 31u));
+                    seen = max(seen, __builtin_amdgcn_ubfe(old, sh4, 4u));
+                }
+            }
+        }
+        ovf = seen == kSketchMax;
+        hot = seen >= cm1;
+    } else {
+#pragma unroll
+        for (uint32_t r = 0; r < (uint32_t)NR; ++r) {
+            if (64 * r < mt) {
+                const uint32_t t[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
+                // (issuing the four returning adds together, one wait, was measured no faster: the
+                // other waves of the SIMD already cover the LDS latency)
+#pragma unroll
+                for (uint32_t e = 0; e < 4; ++e) {
+                    const uint32_t sh4 = sketch_sh4<W, LEAN>(t[e]);
+                    const uint32_t old = atomicAdd(sketch_word<W, LEAN>(S.table, t[e]), ((vmask >> (4 * r + e)) & 1u) << (sh4 & 31u));
+                    const uint32_t on = __builtin_amdgcn_ubfe(old, sh4, 4u);
+                    ovf |= on == kSketchMax;
+                    if constexpr (kSkipCold && W == 1) hot |= on == cm1;
+                }
             }
         }
     }
