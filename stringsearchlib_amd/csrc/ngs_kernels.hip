@@ -1386,10 +1386,12 @@ __device__ __forceinline__ uint32_t part_sketch(WaveSmem<W, LEAN>& S, const uint
                 for (uint32_t e = 0; e < 4; ++e) w[e] = *sketch_word<W, LEAN>(S.table, t[e]);
 #pragma unroll
                 for (uint32_t e = 0; e < 4; ++e) {
-                    const bool f = ((vmask >> (4 * r + e)) & 1u) &&
-                                   __builtin_amdgcn_ubfe(w[e], sketch_sh4<W, LEAN>(t[e]), 4u) >= cmin;
-                    const unsigned long long b = __ballot(f);
-                    if (b) {
+                    // the entry's mask bit is tested only in the (rare) branch taken when some
+                    // cell of the slot reached cmin
+                    bool f = __builtin_amdgcn_ubfe(w[e], sketch_sh4<W, LEAN>(t[e]), 4u) >= cmin;
+                    if (__ballot(f)) {
+                        f = f && ((vmask >> (4 * r + e)) & 1u);
+                        const unsigned long long b = __ballot(f);
                         const uint32_t pos = nw + rank_below(b);
                         if (f && pos < 64u) S.cbuf[pos] = t[e];
                         nw += (uint32_t)__popcll(b);
