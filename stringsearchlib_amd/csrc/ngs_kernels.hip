@@ -2289,21 +2289,22 @@ __device__ __forceinline__ void emit_query(EmitSmem& S, const uint32_t q, const 
     const uint32_t lane = lane_id();
     const uint32_t* et = P.est + (size_t)q * kEmitCap;
     const uint8_t* ec = P.esc + (size_t)q * kEmitCap;
-    // the first 64 survivors load beside the count (the slots always exist): one round trip less
+    // the first 64 survivors and the query's length load beside the count (the slots always
+    // exist): one round trip for all of them
     uint32_t t = et[lane], code = ec[lane];
     uint32_t sn = P.esn[q];
+    const uint32_t m = qm[q];
     if (sn == kNoEmit) return;  // tier 1a did not finish this query
     // the main launch leaves the heavy launch's queries to the heavy list's k_emit
     if (!heavy_launch && (sn & kEmitHeavy)) return;
     sn &= ~kEmitHeavy;
-    const uint32_t m = qm[q], n = m - X.gsz + 1, L = P.limit;
-    const uint8_t* qg = qnorm + qoff[q];
-    for (uint32_t i = lane; i < m; i += 64) S.q[i] = char_at(qg, i, X.csize);
+    const uint32_t n = m - X.gsz + 1, L = P.limit;
     const float sc_long = lane <= n ? (float)lane / (float)n : 0.0f;  // as wave_query
     const float sc_short = lane <= m ? (float)lane / (float)m : 0.0f;
     uint32_t cand_n = 0;
     uint64_t tau = kNoCand;
-    wave_sync();
+    // the query's characters only for an exact-match test (a survivor scoring > 0.999), rare
+    bool have_q = false;
     // wave_emit over the survivors in HBM
     for (uint32_t base = 0; base < sn; base += 64) {
         const uint32_t i = base + lane;
@@ -2315,6 +2316,12 @@ __device__ __forceinline__ void emit_query(EmitSmem& S, const uint32_t q, const 
         const float s_l = __shfl(sc_long, (int)(code & 63u)), s_s = __shfl(sc_short, (int)(code & 63u));
         const float s = (code & 0x80u) ? s_s : s_l;
         const bool promo = (double)s > 0.999;  // nGramSearch.hpp:328
+        if (!have_q && __ballot(i < sn && promo)) {
+            const uint8_t* qg = qnorm + qoff[q];
+            for (uint32_t k = lane; k < m; k += 64) S.q[k] = char_at(qg, k, X.csize);
+            wave_sync();
+            have_q = true;
+        }
         if (i < sn) term_pairs(X, t, s, promo, tau, p, pe);
         while (__ballot(p < pe)) {
             uint64_t rec = kNoCand;
