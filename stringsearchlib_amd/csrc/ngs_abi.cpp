@@ -95,6 +95,7 @@ struct Context {
     hipEvent_t prep_ev = nullptr, lists_ev = nullptr;  // k_prep done (s), heavy / full lists merged (side)
     hipEvent_t ev[6] = {};
     size_t qcap = 0, bcap = 0, ncap = 0, ocap = 0;
+    uint32_t ecap = kEmitCap;  // survivor slots per query in d_est / d_esc (ensure_queries)
     uint8_t* d_raw = nullptr;
     uint64_t* d_off = nullptr;
     uint8_t* d_norm = nullptr;
@@ -418,10 +419,11 @@ bool ensure_queries(Context& c, size_t B, size_t bytes) {
                          (void**)&c.d_fb2, (void**)&c.d_heavy, (void**)&c.d_full, (void**)&c.d_lslots, (void**)&c.d_esn, (void**)&c.d_est, (void**)&c.d_esc})
             if (*p) { hipFree(*p); *p = nullptr; }
         size_t nb = std::max<size_t>(B, 1024);
+        c.ecap = nb <= kEmitWideBatch ? std::max(kEmitCap, kEmitCapWide) : kEmitCap;
         if (!dev_alloc(&c.d_off, nb + 1) || !dev_alloc(&c.d_qm, nb) || !dev_alloc(&c.d_glist, nb) ||
             !dev_alloc(&c.d_list2, nb) || !dev_alloc(&c.d_fb, nb) || !dev_alloc(&c.d_fb2, nb) || !dev_alloc(&c.d_heavy, nb) || !dev_alloc(&c.d_full, nb) ||
             !dev_alloc(&c.d_lslots, 2 * (nb + kListSlots)) ||
-            !dev_alloc(&c.d_esn, nb) || !dev_alloc(&c.d_est, nb * kEmitCap) || !dev_alloc(&c.d_esc, nb * kEmitCap))
+            !dev_alloc(&c.d_esn, nb) || !dev_alloc(&c.d_est, nb * c.ecap) || !dev_alloc(&c.d_esc, nb * c.ecap))
             return false;
         c.bcap = nb;
     }
@@ -557,6 +559,7 @@ int queue_search(Library& L, Replica& R, Context& c, const uint8_t* d_raw, const
     P.esn = c.d_esn;
     P.est = c.d_est;
     P.esc = c.d_esc;
+    P.ecap = c.ecap;
     static const uint32_t list_slices = [] {  // term-id slices of the hand-over / full lists' tier 1b
         const char* e = std::getenv("NGS_SLICES");
         const uint32_t v = e ? (uint32_t)std::strtoul(e, nullptr, 0) : kSlices;

@@ -151,6 +151,12 @@ constexpr bool kHeavyLean = NGS_HEAVY_LEAN != 0;
 #define NGS_LEAN_SHRINK2 1
 #endif
 constexpr uint32_t kLeanShrink2 = NGS_LEAN_SHRINK2;  // tier 1a cmin-2 sketch parts: cap and target >> this
+#ifndef NGS_LEAN_ONES
+#define NGS_LEAN_ONES 1
+#endif
+// tier 1a also takes cmin-1 queries (threshold 0) on the heavy list: part_ones
+constexpr bool kLeanOnes = NGS_LEAN_ONES != 0;
+constexpr uint32_t kOnesShrink = 2;             // ... in parts of a quarter of the sketch cap
 constexpr uint32_t kHeavyWaves = 1;             // ... on this many waves per query
 constexpr uint32_t kHeavyGrid = 4096;           // ... by this many workgroups (grid-stride)
 constexpr bool kSidePriority = false;           // ... on a highest-priority stream
@@ -166,7 +172,14 @@ constexpr int kWaveTarget = kWaveCap * 5 / 8;   // postings per exact part the b
 constexpr int kSketchTarget = kSketchCap * NGS_TGT8 / 8;  // ... per sketch part (bucket groups aim at NGS_TGT8/8 of the cap)
 constexpr uint32_t kStray = 0xFFFFFFFFu;        // staged entry outside its list segment
 constexpr int kWaveSurv = 128;                  // survivor list (term, count) before calcScore
-constexpr uint32_t kEmitCap = 1024;             // tier 1a survivors per query spilled to HBM for k_emit
+#ifndef NGS_EMIT_CAP
+#define NGS_EMIT_CAP 1024
+#endif
+constexpr uint32_t kEmitCap = NGS_EMIT_CAP;
+// batches up to kEmitWideBatch queries get kEmitCapWide slots per query (5 bytes each): a
+// threshold-0 query has thousands of one-hit survivors at C2 (part_ones)
+constexpr uint32_t kEmitCapWide = 4096;
+constexpr size_t kEmitWideBatch = 262144;             // tier 1a survivors per query spilled to HBM for k_emit
 constexpr uint32_t kWaveMaxGrams = 63;          // counts <= 63: one lane per count value
 #ifndef NGS_SK2
 #define NGS_SK2 2     // smallest cmin counted by the sketch (below: exact hash counting)
@@ -220,6 +233,7 @@ struct SearchParams {
     uint32_t* esn;
     uint32_t* est;
     uint8_t* esc;
+    uint32_t ecap;       // survivor slots per query (kEmitCap, or kEmitCapWide for batches <= kEmitWideBatch)
     // sliced tier 1b (kSlices): the full list and the hand-over lists run as nslices term-id
     // slices of each query (one wave each, bucket ranges of the skip table); slice j of query q
     // leaves its top-L records at prec[(q * nslices + j) * limit] and their count at

@@ -71,8 +71,9 @@ __device__ __forceinline__ uint32_t char_at(const uint8_t* base, uint64_t i, uin
 // 1 (heavy list) match-count threshold cmin == 2, where every term sharing a (g+1)-gram with the
 //   query survives: hundreds of survivors, which the heavy list's lean launch spills to k_emit
 //   (kHeavyLean);
-// 2 (full list, tier 1b) cmin 1, which needs exact counting, or a short search over shortLib
-//   (m < 3g, hpp:381); without kHeavyLean also cmin 2.
+//   The same list takes cmin 1 (kLeanOnes: part_ones, every term sharing a gram survives);
+// 2 (full list, tier 1b) a short search over shortLib (m < 3g, hpp:381); without kHeavyLean
+//   also cmin 1 and 2.
 // Both run beside tier 1a. cmin is computed exactly as the wave kernel does: the first c with
 // !((float)c / n < thr).
 __device__ __forceinline__ uint32_t heavy_class(const DevIndex& X, const SearchParams& P, uint32_t m) {
@@ -85,7 +86,7 @@ __device__ __forceinline__ uint32_t heavy_class(const DevIndex& X, const SearchP
     for (uint32_t c = n; c >= 1; --c)
         if (!((float)c / fn < P.thr)) cmin = c;
     if (cmin > kHeavyCmin) return 0;
-    return kHeavyLean && cmin >= kSketchMinCmin ? 1 : 2;
+    return kHeavyLean && (cmin >= kSketchMinCmin || kLeanOnes) ? 1 : 2;
 }
 
 // ---------------------------------------------------------------- normalisation ------
@@ -1470,6 +1471,93 @@ __device__ __forceinline__ uint32_t part_sketch(WaveSmem<W, LEAN>& S, const uint
     return nc;
 }
 
+// Tier 1a at cmin 1 (threshold 0: every term sharing a gram with the query survives): the sketch
+// adds of part_sketch, then every entry alone in its cell is a one-hit term, written straight to
+// the query's survivor slots in HBM (et / ec at `spilled`, for k_emit), and the entries of cells
+// that reached 2 (terms with more hits, and the few colliding pairs of one-hit terms) are
+// resolved exactly by comparing them with each other. Returns the number of those candidates;
+// above 64, a wrapped counter, or survivor slots running out (kEmitCap) it returns 65: the
+// caller hands the query to tier 1b. Parts are cut to a quarter of a sketch part so that pairs
+// colliding in the 8,192 cells stay few.
+template <int NR = kDmaRounds>
+__device__ __forceinline__ uint32_t part_ones(WaveSmem<1, true>& S, const uint4 (&v)[NR], uint32_t vmask, uint32_t mt,
+                                              uint32_t n_short, uint32_t n_terms, uint32_t& surv_n,
+                                              uint32_t* __restrict__ et, uint8_t* __restrict__ ec, uint32_t& spilled,
+                                              uint32_t ecap) {
+    const uint32_t lane = lane_id();
+    mt = __builtin_amdgcn_readfirstlane(mt);
+    uint32_t seen = 0;
+#pragma unroll
+    for (uint32_t r = 0; r < (uint32_t)NR; ++r) {
+        if (64 * r < mt && 64 * r + lane < mt) {
+            const uint32_t t[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
+#pragma unroll
+            for (uint32_t e = 0; e < 4; ++e) {
+                const uint32_t sh4 = sketch_sh4<1, true>(t[e]);
+                const uint32_t old = atomicAdd(sketch_word<1, true>(S.table, t[e]), 1u << (sh4 & 31u));
+                seen = max(seen, __builtin_amdgcn_ubfe(old, sh4, 4u));
+            }
+        }
+    }
+    const bool ovf = __ballot(seen == kSketchMax) != 0;
+    wave_sync();
+    uint32_t nw = 0;
+    if (!ovf) {
+#pragma unroll
+        for (uint32_t r = 0; r < (uint32_t)NR; ++r) {
+            if (64 * r < mt) {
+                const uint32_t t[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
+                uint32_t w[4];
+#pragma unroll
+                for (uint32_t e = 0; e < 4; ++e) w[e] = *sketch_word<1, true>(S.table, t[e]);
+#pragma unroll
+                for (uint32_t e = 0; e < 4; ++e) {
+                    const uint32_t c = ((vmask >> (4 * r + e)) & 1u) ? __builtin_amdgcn_ubfe(w[e], sketch_sh4<1, true>(t[e]), 4u) : 0u;
+                    const bool one = c == 1, two = c >= 2;
+                    const unsigned long long b1 = __ballot(one);
+                    if (b1) {
+                        const uint32_t pos = spilled + rank_below(b1);
+                        if (one && pos < ecap) {
+                            et[pos] = min(n_short + t[e], n_terms - 1u);
+                            ec[pos] = 1;
+                        }
+                        spilled += (uint32_t)__popcll(b1);
+                    }
+                    const unsigned long long b2 = __ballot(two);
+                    if (b2) {
+                        const uint32_t pos = nw + rank_below(b2);
+                        if (two && pos < 64u) S.cbuf[pos] = t[e];
+                        nw += (uint32_t)__popcll(b2);
+                    }
+                }
+            }
+        }
+    }
+    wave_sync();
+    {
+        uint4* T4 = reinterpret_cast<uint4*>(S.table);
+        for (uint32_t i = lane; i < (uint32_t)TableGeom<true>::kSlots / 4; i += 64) T4[i] = make_uint4(0, 0, 0, 0);
+    }
+    if (ovf || nw > 64 || spilled + surv_n > ecap) {
+        wave_sync();
+        return 65;
+    }
+    if (nw) {  // exact counts of the candidates (as part_sketch), every one of them a survivor
+        const uint32_t t = lane < nw ? S.cbuf[lane] : kStray;
+        uint32_t cnt = 0;
+        bool first = true;
+        for (uint32_t j = 0; j < nw; ++j) {
+            const uint32_t tj = __builtin_amdgcn_readlane(t, j);
+            const bool eq = t == tj;
+            cnt += eq;
+            first &= !(eq && j < lane);
+        }
+        surv_append(S, lane < nw && first, min(n_short + t, n_terms - 1u), cnt, surv_n);
+    }
+    wave_sync();
+    return nw;
+}
+
 // One query on W waves. LEAN (tier 1a, W = 1): the common case only, sketch counting with no
 // exact-count pass, no mid-loop calcScore and no short search, which keeps the kernel within 96
 // VGPRs (5 waves per SIMD); a query that needs any of those is appended to fb[] untouched and
@@ -1546,9 +1634,9 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
     // (spilled of them written so far); false if they are full (the query is handed over)
     uint32_t spilled = 0;
     auto spill = [&]() -> bool {
-        if (spilled + surv_n > kEmitCap) return false;
-        uint32_t* et = P.est + (size_t)q * kEmitCap + spilled;
-        uint8_t* ec = P.esc + (size_t)q * kEmitCap + spilled;
+        if (spilled + surv_n > P.ecap) return false;
+        uint32_t* et = P.est + (size_t)q * P.ecap + spilled;
+        uint8_t* ec = P.esc + (size_t)q * P.ecap + spilled;
         for (uint32_t i = lane; i < surv_n; i += 64) {
             et[i] = S.surv_t[i];
             ec[i] = S.surv_c[i];
@@ -1950,6 +2038,7 @@ __device__ __forceinline__ void lean_stage(WaveSmem<1, true>& S, gptr<uint4> pos
 // k_emit. The full kernel's part loop (bucket groups, term-id sub-parts, loads one part ahead)
 // with its own staging (lean_stage) and the sketch counter part_sketch; a query that needs exact
 // counting, a short search or more than kEmitCap survivor slots is handed to tier 1b untouched.
+template <bool ONES>
 __device__ __forceinline__ void lean_query(WaveSmem<1, true>& S, const uint32_t q, const DevIndex& X,
                                            const SearchParams& P, const uint8_t* __restrict__ qnorm,
                                            const uint64_t* __restrict__ qoff, const uint32_t* __restrict__ qm,
@@ -2034,13 +2123,14 @@ __device__ __forceinline__ void lean_query(WaveSmem<1, true>& S, const uint32_t 
     const uint64_t p_total = wave_sum((uint64_t)glen);
     WSTAMP(0);
     const bool sketch = cmin >= kSketchMinCmin && cmin <= kSketchMax;
-    if (p_total && cmin <= n && !sketch) { bail(); return; }  // exact counting: tier 1b
+    const bool ones = ONES && cmin == 1;  // part_ones (the heavy list's launch only)
+    if (p_total && cmin <= n && !sketch && !ones) { bail(); return; }  // exact counting: tier 1b
     uint32_t surv_n = 0, spilled = 0;
     // the LDS survivor list to this query's kEmitCap slots in HBM; false if they are full
     auto spill = [&]() -> bool {
-        if (spilled + surv_n > kEmitCap) return false;
-        uint32_t* et = P.est + (size_t)q * kEmitCap + spilled;
-        uint8_t* ec = P.esc + (size_t)q * kEmitCap + spilled;
+        if (spilled + surv_n > P.ecap) return false;
+        uint32_t* et = P.est + (size_t)q * P.ecap + spilled;
+        uint8_t* ec = P.esc + (size_t)q * P.ecap + spilled;
         for (uint32_t i = lane; i < surv_n; i += 64) {
             et[i] = S.surv_t[i];
             ec[i] = S.surv_c[i];
@@ -2051,7 +2141,7 @@ __device__ __forceinline__ void lean_query(WaveSmem<1, true>& S, const uint32_t 
     };
     if (p_total && cmin <= n) {
         // cmin 2: every colliding pair is a false candidate, so those parts are cut at half the size
-        const uint32_t shrink = cmin == 2 ? kLeanShrink2 : 0u;
+        const uint32_t shrink = ones ? kOnesShrink : cmin == 2 ? kLeanShrink2 : 0u;
         const uint32_t kChunks = (uint32_t)kWaveChunks >> shrink;  // part cap in 16-byte chunks
         const uint32_t K = X.n_buckets, span = X.bucket_span;
         const uint32_t wmax = (uint32_t)max64(1, min64(K, kMaxPartSpan / max(span, 1u)));
@@ -2179,7 +2269,13 @@ __device__ __forceinline__ void lean_query(WaveSmem<1, true>& S, const uint32_t 
                     if (!spill()) { bail(); return; }
                     wave_sync();  // the list is read before it is refilled
                 }
-                const uint32_t nc = part_sketch(S, cv, c_vm, c_mt, cmin, X.n_short, X.n_terms, surv_n, P.dbg);
+                uint32_t nc;
+                if constexpr (ONES)
+                    nc = ones ? part_ones(S, cv, c_vm, c_mt, X.n_short, X.n_terms, surv_n, P.est + (size_t)q * P.ecap,
+                                          P.esc + (size_t)q * P.ecap, spilled, P.ecap)
+                              : part_sketch(S, cv, c_vm, c_mt, cmin, X.n_short, X.n_terms, surv_n, P.dbg);
+                else
+                    nc = part_sketch(S, cv, c_vm, c_mt, cmin, X.n_short, X.n_terms, surv_n, P.dbg);
                 WCOUNT(11, 1);
                 WCOUNT(13, (c_mt + 63) / 64);
                 WCOUNT(14, nc);
@@ -2242,7 +2338,9 @@ __global__ __launch_bounds__(64 * W, kWaveWavesPerSimd) void k_wave(DevIndex X, 
 
 // Tier 1a: the lean wave kernel over every query (qlist == nullptr), or over the heavy list.
 // DEFER: survivors spill to HBM for k_emit (the heavy launch always; the main one if kDeferEmit).
-template <bool DEFER>
+// ONES: the heavy list's launch, which also takes cmin-1 queries (part_ones); the main launch
+// is compiled without that path
+template <bool DEFER, bool ONES = false>
 __global__ __launch_bounds__(64, kLeanWavesPerSimd) void k_wave_lean(DevIndex X, SearchParams P,
                                                                     const uint8_t* __restrict__ qnorm,
                                                                     const uint64_t* __restrict__ qoff,
@@ -2258,12 +2356,12 @@ __global__ __launch_bounds__(64, kLeanWavesPerSimd) void k_wave_lean(DevIndex X,
                                                                     const uint32_t* __restrict__ qcount) {
     __shared__ WaveSmem<1, true> S;
     if (!qlist) {
-        lean_query(S, blockIdx.x, X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats, fb, fbc);
+        lean_query<ONES>(S, blockIdx.x, X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats, fb, fbc);
         return;
     }
     const uint32_t cnt = *qcount;  // the heavy list, grid-stride
     for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
-        lean_query(S, qlist[i], X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats, fb, fbc);
+        lean_query<ONES>(S, qlist[i], X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats, fb, fbc);
         wave_sync();
     }
 }
@@ -2287,8 +2385,8 @@ __device__ __forceinline__ void emit_query(EmitSmem& S, const uint32_t q, const 
                                            uint32_t* __restrict__ out_n, uint32_t* __restrict__ out_k,
                                            float* __restrict__ out_s, DevStats* __restrict__ stats) {
     const uint32_t lane = lane_id();
-    const uint32_t* et = P.est + (size_t)q * kEmitCap;
-    const uint8_t* ec = P.esc + (size_t)q * kEmitCap;
+    const uint32_t* et = P.est + (size_t)q * P.ecap;
+    const uint8_t* ec = P.esc + (size_t)q * P.ecap;
     // the first 64 survivors and the query's length load beside the count (the slots always
     // exist): one round trip for all of them
     uint32_t t = et[lane], code = ec[lane];
@@ -2657,7 +2755,7 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
             if (kHeavyLean) {
                 SearchParams PH = P;
                 PH.lean_all = 1;
-                hipLaunchKernelGGL(k_wave_lean<true>, dim3(gh), dim3(64), 0, side, X, PH, qnorm, off, qm, out_n,
+                hipLaunchKernelGGL((k_wave_lean<true, kLeanOnes>), dim3(gh), dim3(64), 0, side, X, PH, qnorm, off, qm, out_n,
                                    out_k, out_s, list2, count2, stats, fb2, fbc2, heavy, hcount);
                 hipLaunchKernelGGL(k_emit, dim3((gh + kEmitWaves - 1) / kEmitWaves), dim3(64 * kEmitWaves), 0, side,
                                    X, PH, qnorm, off, qm, out_n, out_k, out_s, stats, heavy, hcount);

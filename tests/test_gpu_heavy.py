@@ -60,3 +60,37 @@ def test_cmin2_spill_parity(alphabet, rows, lo, hi, expect_handover):
     for i, g in enumerate(big):
         assert g == small[i % len(qs)], f"batch of {len(big)}: q#{i} differs"
     gi.dispose()
+
+
+@pytest.mark.parametrize("alphabet,rows,lo,hi,qlen", [
+    (b"ABCDEFGHIJKLMNOPQRSTUVWXYZ", 60000, 8, 24, 12),  # hundreds of one-hit terms: part_ones
+    (b"ABCDEFGHIJKL", 30000, 3, 20, 10),                # thousands, with a shortLib beside
+])
+def test_cmin1_ones_and_short_routing(alphabet, rows, lo, hi, qlen):
+    """Threshold 0 (cmin 1): the heavy list's lean launch counts the parts with part_ones (one-hit
+    terms straight to the survivor slots, the rest resolved exactly); queries with more than
+    kEmitCap survivors hand over to tier 1b. Short queries (|q| < 9 with a shortLib) take the full
+    list into tier 1b. Exact vs the oracle."""
+    rng = random.Random(rows + qlen)
+    words = _words(rng, alphabet, rows, lo, hi)
+    wts = [rng.choice([1.0, 0.5, 0.25 + rng.random()]) for _ in words]
+    gi = ssl.StringIndex(words, 1, wts)
+    gi.set_timing(True)
+    oi = OracleIndex(words, 1, wts)
+    cases = [(_queries(rng, words, 40, qlen), 0.0, "ones")]
+    if lo < 6:
+        cases.append((_queries(rng, words, 24, 6), 0.3, "short"))
+    for qs, thr, kind in cases:
+        for limit in (100, 10):
+            got = gi.score_batch(qs, thr, limit)
+            st = gi.last_stats()
+            for q, g in zip(qs, got):
+                ref = oi.score(q, thr, limit)
+                assert len(g) == len(ref), f"{kind} q={q!r} limit={limit}: {len(g)} vs {len(ref)}"
+                for i, ((k1, s1), (k2, s2)) in enumerate(zip(g, ref)):
+                    assert k1 == k2 and bits(s1) == bits(s2), f"{kind} q={q!r} #{i}: {k1!r}|{s1} vs {k2!r}|{s2}"
+            if kind == "ones":
+                assert st["heavy_queries"] == len(qs) and st["full_queries"] == 0, st
+            else:
+                assert st["full_queries"] == len(qs), st
+    gi.dispose()
