@@ -2406,9 +2406,11 @@ __device__ __forceinline__ void emit_query(EmitSmem& S, const uint32_t q, const 
     // wave_emit over the survivors in HBM
     for (uint32_t base = 0; base < sn; base += 64) {
         const uint32_t i = base + lane;
-        if (base) {
-            t = i < sn ? et[i] : 0u;
-            code = i < sn ? ec[i] : 0u;
+        // the next 64 survivors load while this batch's pairs do (one round trip per batch)
+        uint32_t t_next = 0, code_next = 0;
+        if (base + 64 < sn && i + 64 < sn) {
+            t_next = et[i + 64];
+            code_next = ec[i + 64];
         }
         uint32_t p = 0, pe = 0;
         const float s_l = __shfl(sc_long, (int)(code & 63u)), s_s = __shfl(sc_short, (int)(code & 63u));
@@ -2434,6 +2436,8 @@ __device__ __forceinline__ void emit_query(EmitSmem& S, const uint32_t q, const 
             if (want) S.cand()[cand_n + rank_below(bw)] = rec;
             cand_n += __popcll(bw);
         }
+        t = t_next;
+        code = code_next;
     }
     wave_flush(S, cand_n, tau, L, X.keys_unique != 0);
     const size_t ob = (size_t)q * P.out_stride;
@@ -2730,13 +2734,29 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
                                    out_n, out_k, out_s, list2, count2, stats, fb, fbc, (const uint32_t*)nullptr,
                                    (const uint32_t*)nullptr);
             };
-            if ((e = hipEventRecord(fork, s)) != hipSuccess) return e;
             // the main launch is queued first: the GPU idled ~35 us while the host queued the side
             // streams' launches ahead of it
             if (kMainFirst) main_lean();
-            // side: k_lists is already queued there (launch_prep); side2 waits for the lists
-            if ((e = hipStreamWaitEvent(side, fork, 0)) != hipSuccess || (e = hipStreamWaitEvent(side2, lists_ev, 0)) != hipSuccess)
-                return e;
+            // then the heavy list's chain on side, which is already ordered after k_prep with k_lists
+            // queued on it (launch_prep): queued second, so that it starts soon after k_lists (the
+            // host queues ~15 operations per call; at C2 this launch carries every query)
+            if (kHeavyLean) {
+                SearchParams PH = P;
+                PH.lean_all = 1;
+                hipLaunchKernelGGL((k_wave_lean<true, kLeanOnes>), dim3(gh), dim3(64), 0, side, X, PH, qnorm, off, qm, out_n,
+                                   out_k, out_s, list2, count2, stats, fb2, fbc2, heavy, hcount);
+                hipLaunchKernelGGL(k_emit, dim3((gh + kEmitWaves - 1) / kEmitWaves), dim3(64 * kEmitWaves), 0, side,
+                                   X, PH, qnorm, off, qm, out_n, out_k, out_s, stats, heavy, hcount);
+                hipLaunchKernelGGL(k_wave<1>, dim3(g1s), dim3(64), 0, side, X, P, qnorm, off, qm, out_n, out_k,
+                                   out_s, list2, count2, stats, (const uint32_t*)fb2, (const uint32_t*)fbc2);
+                if (P.nslices > 1)
+                    hipLaunchKernelGGL(k_merge, dim3(g1b), dim3(64), 0, side, X, P, (const uint32_t*)fb2,
+                                       (const uint32_t*)fbc2, out_n, out_k, out_s, stats);
+            }
+            if ((e = hipEventRecord(join, side)) != hipSuccess) return e;
+            // side2 waits for the lists
+            (void)fork;
+            if ((e = hipStreamWaitEvent(side2, lists_ev, 0)) != hipSuccess) return e;
             if (P.heavy_waves == 4)
                 hipLaunchKernelGGL(k_wave<4>, dim3(gh), dim3(256), 0, side2, X, P, qnorm, off, qm, out_n, out_k,
                                    out_s, list2, count2, stats, full, fcount);
@@ -2752,20 +2772,6 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
                                    list2, count2, stats, full, fcount);
             }
             if ((e = hipEventRecord(join2, side2)) != hipSuccess) return e;
-            if (kHeavyLean) {
-                SearchParams PH = P;
-                PH.lean_all = 1;
-                hipLaunchKernelGGL((k_wave_lean<true, kLeanOnes>), dim3(gh), dim3(64), 0, side, X, PH, qnorm, off, qm, out_n,
-                                   out_k, out_s, list2, count2, stats, fb2, fbc2, heavy, hcount);
-                hipLaunchKernelGGL(k_emit, dim3((gh + kEmitWaves - 1) / kEmitWaves), dim3(64 * kEmitWaves), 0, side,
-                                   X, PH, qnorm, off, qm, out_n, out_k, out_s, stats, heavy, hcount);
-                hipLaunchKernelGGL(k_wave<1>, dim3(g1s), dim3(64), 0, side, X, P, qnorm, off, qm, out_n, out_k,
-                                   out_s, list2, count2, stats, (const uint32_t*)fb2, (const uint32_t*)fbc2);
-                if (P.nslices > 1)
-                    hipLaunchKernelGGL(k_merge, dim3(g1b), dim3(64), 0, side, X, P, (const uint32_t*)fb2,
-                                       (const uint32_t*)fbc2, out_n, out_k, out_s, stats);
-            }
-            if ((e = hipEventRecord(join, side)) != hipSuccess) return e;
             if (!kMainFirst) main_lean();
             if (kDeferEmit)
                 hipLaunchKernelGGL(k_emit, dim3((P.n_queries + kEmitWaves - 1) / kEmitWaves), dim3(64 * kEmitWaves), 0,
