@@ -12,5 +12,6 @@ mkdir -p gpurun_out/keep_$TAG
 cp gpurun_out/prof_$TAG/stats/run_kernel_stats.csv gpurun_out/prof_$TAG/timeline.txt gpurun_out/prof_$TAG/bench.json \
    gpurun_out/pmc_$TAG/summary.txt gpurun_out/keep_$TAG/
 cp gpurun_out/prof_$TAG/fetch/run_counter_collection.csv gpurun_out/keep_$TAG/fetch_counter_collection.csv
+cp profiles/pmc_c3.json gpurun_out/keep_$TAG/pmc_c3.json
 rm -rf gpurun_out/prof_$TAG gpurun_out/pmc_$TAG
 ls -la gpurun_out/keep_$TAG
