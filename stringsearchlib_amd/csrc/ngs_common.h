@@ -156,7 +156,10 @@ constexpr uint32_t kLeanShrink2 = NGS_LEAN_SHRINK2;  // tier 1a cmin-2 sketch pa
 #endif
 // tier 1a also takes cmin-1 queries (threshold 0) on the heavy list: part_ones
 constexpr bool kLeanOnes = NGS_LEAN_ONES != 0;
-constexpr uint32_t kOnesShrink = 2;             // ... in parts of a quarter of the sketch cap
+#ifndef NGS_ONES_SHRINK
+#define NGS_ONES_SHRINK 2
+#endif
+constexpr uint32_t kOnesShrink = NGS_ONES_SHRINK;  // ... in parts of a quarter of the sketch cap
 constexpr uint32_t kHeavyWaves = 1;             // ... on this many waves per query
 constexpr uint32_t kHeavyGrid = 4096;           // ... by this many workgroups (grid-stride)
 constexpr bool kSidePriority = false;           // ... on a highest-priority stream
