@@ -881,10 +881,24 @@ uint32_t marshal(const Library& L, const std::vector<uint32_t>& keys, const std:
     const size_t n = keys.size();
     if (scores) *scores = new float[n];
     *results = new CharT*[n];
-    for (size_t i = 0; i < n; ++i) {
-        (*results)[i] = reinterpret_cast<CharT*>(const_cast<char*>(L.host.key_bytes.data()) +
-                                                 L.host.key_off[keys[i]] * sizeof(CharT));
-        if (scores) (*scores)[i] = sc[i];
+    CharT** res = *results;
+    float* out_s = scores ? *scores : nullptr;
+    char* base = const_cast<char*>(L.host.key_bytes.data());
+    const uint64_t* koff = L.host.key_off.data();
+    auto fill = [&](size_t a, size_t b) {  // key_off is gathered at random: memory-latency bound
+        for (size_t i = a; i < b; ++i) {
+            res[i] = reinterpret_cast<CharT*>(base + koff[keys[i]] * sizeof(CharT));
+            if (out_s) out_s[i] = sc[i];
+        }
+    };
+    // a whole batch's records (1.3M at C3) on several host threads
+    const size_t nt = n < (size_t(1) << 18) ? 1 : std::min<size_t>(8, std::max(1u, std::thread::hardware_concurrency()));
+    if (nt <= 1) {
+        fill(0, n);
+    } else {
+        std::vector<std::thread> th;
+        for (size_t t = 0; t < nt; ++t) th.emplace_back(fill, n * t / nt, n * (t + 1) / nt);
+        for (auto& x : th) x.join();
     }
     return (uint32_t)n;
 }
