@@ -803,17 +803,17 @@ bool host_search_one(Library& L, Replica& R, const CharT* const* queries, uint32
         if (!ok) break;
         const uint32_t total = c->h_res.as<uint32_t>()[B];
         for (uint32_t i = 0; i < B; ++i) counts[q0 + i] = c->h_res.as<uint32_t>()[i + 1] - c->h_res.as<uint32_t>()[i];
-        const size_t k0 = keys.size();
-        keys.resize(k0 + total);
-        scores.resize(k0 + total);
         ok = c->h_res.grow(sizeof(uint32_t) * 2 * (size_t)total) &&
              HIP_CHECK(hipMemcpyAsync(c->h_res.p, c->d_pk, sizeof(uint32_t) * total, hipMemcpyDeviceToHost, c->stream)) &&
              HIP_CHECK(hipMemcpyAsync(c->h_res.as<uint32_t>() + total, c->d_ps, sizeof(float) * total,
                                       hipMemcpyDeviceToHost, c->stream)) &&
              HIP_CHECK(hipStreamSynchronize(c->stream));
         if (!ok) break;
-        std::memcpy(keys.data() + k0, c->h_res.p, sizeof(uint32_t) * total);
-        std::memcpy(scores.data() + k0, c->h_res.as<uint32_t>() + total, sizeof(float) * total);
+        // appended straight from the pinned buffer (no zero-filling resize first)
+        const uint32_t* pk = c->h_res.as<uint32_t>();
+        const float* ps = reinterpret_cast<const float*>(pk + total);
+        keys.insert(keys.end(), pk, pk + total);
+        scores.insert(scores.end(), ps, ps + total);
     }
     R.give_back(std::move(c));
     return ok;
