@@ -184,6 +184,16 @@ NGS_API int ngsLastStats(uint32_t handle, ngs_stats* out);
  * -1 (bad handle), -4 (HIP error). */
 NGS_API int ngsIndexDigest(uint32_t handle, uint64_t* out, int n);
 
+/* Index files (an extension; the reference rebuilds on every indexN): ngsSaveIndex writes the
+ * interned library of `handle` (terms, term -> (key, weight) pairs, keys, wildcard weights,
+ * the validChar set) to `path`: 0, or -1 (bad handle), -2 (unbuilt index), -3 (I/O), -4 (HIP
+ * error). ngsLoadIndex builds an index from such a file like indexN builds one from words (the
+ * gram CSR is rebuilt; the devices of ngsSetDevices apply): its handle, or 0 if the file cannot
+ * be read, is not an index file or is inconsistent. A loaded index answers exactly like the
+ * saved one. */
+NGS_API int ngsSaveIndex(uint32_t handle, const char* path);
+NGS_API uint32_t ngsLoadIndex(const char* path);
+
 /* Library build identification: "ngram_search <version> gfx950 src=<hash>", where <hash> is the
  * first 16 hex digits of the SHA-256 of the sources the library was compiled from. */
 NGS_API const char* ngsVersion(void);

@@ -137,6 +137,10 @@ def lib():
     L.ngsIndexDigest.argtypes = [u32, C.POINTER(u64), C.c_int]
     L.ngsVersion.restype = cp
     L.ngsVersion.argtypes = []
+    L.ngsSaveIndex.restype = C.c_int
+    L.ngsSaveIndex.argtypes = [u32, cp]
+    L.ngsLoadIndex.restype = u32
+    L.ngsLoadIndex.argtypes = [cp]
     L.ngsPhaseStats.restype = C.c_int
     L.ngsPhaseStats.argtypes = [C.POINTER(C.c_uint64), C.c_int, C.c_int]
     version = L.ngsVersion().decode()

@@ -178,6 +178,7 @@ hipError_t make_side_stream(hipStream_t* s) {
 struct Replica {
     int device = 0;
     DevIndex dev{};
+    const float* wild_w = nullptr;  // the keys' wildcard weights (ngsSaveIndex reads them back)
     std::vector<void*> owned;
     std::mutex pool_mu;
     std::vector<std::unique_ptr<Context>> pool;
@@ -327,6 +328,7 @@ bool upload_replica(Library& L, Replica& R, bool keys_unique) {
     X.ghash_bits = H.ghash_bits;
     X.ghash_key = ghash_key;
     X.ghash_val = ghash_val;
+    R.wild_w = wild_w;
     if (!dev_alloc(&wild_key, H.n_keys)) return false;
     R.owned.push_back(wild_key);
     if (!dev_alloc(&wild_score, H.n_keys)) return false;
@@ -1245,6 +1247,125 @@ NGS_API int ngsIndexDigest(uint32_t handle, uint64_t* out, int n) {
     const int m = std::min(n, 17);
     for (int i = 0; i < m; ++i) out[i] = i < 16 ? vals[i] : flags;
     return m;
+}
+
+// ---- index files: the interned library, the part the build spends its
+// time on; the gram CSR and skip table are rebuilt from it on load (GPU, or host for gram
+// dictionaries), the keys' wildcard answer too. Little-endian, native widths:
+//   "NGSIDX01" | u32 csize, gsz, gram_mode, short_term_len, short_query_len, full_scan_len,
+//   n_terms, n_short, n_keys, valid[8] | arrays (u64 element count, then the elements):
+//   term_off u64, term_bytes u8, tk_off u32, tk {u32 key, u32 weight bits}, key_off u64,
+//   key_bytes u8, wild_w f32
+extern "C++" {
+namespace ngs {
+namespace {
+constexpr char kIndexMagic[8] = {'N', 'G', 'S', 'I', 'D', 'X', '0', '1'};
+
+template <class T>
+bool put_array(std::FILE* f, const T* p, uint64_t n) {
+    return std::fwrite(&n, sizeof n, 1, f) == 1 && (n == 0 || std::fwrite(p, sizeof(T), n, f) == n);
+}
+template <class T>
+bool get_array(std::FILE* f, std::vector<T>& v, uint64_t max_n) {
+    uint64_t n = 0;
+    if (std::fread(&n, sizeof n, 1, f) != 1 || n > max_n) return false;
+    v.resize(n);
+    return n == 0 || std::fread(v.data(), sizeof(T), n, f) == n;
+}
+template <class T>
+bool download_vec(std::vector<T>& v, const T* d, uint64_t n) {
+    v.resize(n);
+    return n == 0 || HIP_CHECK(hipMemcpy(v.data(), d, n * sizeof(T), hipMemcpyDeviceToHost));
+}
+}  // namespace
+}  // namespace ngs
+}  // extern "C++"
+
+NGS_API int ngsSaveIndex(uint32_t handle, const char* path) {
+    std::shared_lock<std::shared_mutex> lk(g_lock);
+    Library* L = find_lib(handle);
+    if (!L) return -1;
+    if (!L->host.indexed || L->reps.empty()) return -2;
+    if (!path) return -3;
+    const HostIndex& H = L->host;
+    const Replica& R = *L->reps.front();
+    if (!HIP_CHECK(hipSetDevice(R.device))) return -4;
+    const DevIndex& X = R.dev;
+    std::vector<uint64_t> term_off;
+    std::vector<uint8_t> term_bytes;
+    std::vector<uint32_t> tk_off;
+    std::vector<uint2> tk;
+    std::vector<float> wild_w;
+    if (!download_vec(term_off, X.term_off, (uint64_t)H.n_terms + 1) ||
+        !download_vec(term_bytes, X.term_bytes, term_off.back() * H.csize) ||
+        !download_vec(tk_off, X.tk_off, (uint64_t)H.n_terms + 1) || !download_vec(tk, X.tk, tk_off.back()) ||
+        !download_vec(wild_w, R.wild_w, H.n_keys))
+        return -4;
+    uint32_t valid[8];
+    {
+        std::lock_guard<std::mutex> g(L->valid_mu);
+        std::memcpy(valid, L->valid, sizeof valid);
+    }
+    std::FILE* f = std::fopen(path, "wb");
+    if (!f) return -3;
+    const uint32_t sc[9] = {H.csize,          H.gsz,         H.gram_mode, H.short_term_len, H.short_query_len,
+                            H.full_scan_len,  H.n_terms,     H.n_short,   H.n_keys};
+    bool ok = std::fwrite(kIndexMagic, 1, 8, f) == 8 && std::fwrite(sc, sizeof sc, 1, f) == 1 &&
+              std::fwrite(valid, sizeof valid, 1, f) == 1 && put_array(f, term_off.data(), term_off.size()) &&
+              put_array(f, term_bytes.data(), term_bytes.size()) && put_array(f, tk_off.data(), tk_off.size()) &&
+              put_array(f, tk.data(), tk.size()) && put_array(f, H.key_off.data(), H.key_off.size()) &&
+              put_array(f, H.key_bytes.data(), H.key_bytes.size()) && put_array(f, wild_w.data(), wild_w.size());
+    ok = (std::fclose(f) == 0) && ok;
+    return ok ? 0 : -3;
+}
+
+NGS_API uint32_t ngsLoadIndex(const char* path) {
+    if (!path) return 0;
+    std::FILE* f = std::fopen(path, "rb");
+    if (!f) return 0;
+    HostIndex H;
+    char magic[8];
+    uint32_t sc[9], valid[8];
+    constexpr uint64_t kMax = uint64_t(1) << 40;
+    bool ok = std::fread(magic, 1, 8, f) == 8 && std::memcmp(magic, kIndexMagic, 8) == 0 &&
+              std::fread(sc, sizeof sc, 1, f) == 1 && std::fread(valid, sizeof valid, 1, f) == 1 &&
+              get_array(f, H.term_off, kMax) && get_array(f, H.term_bytes, kMax) && get_array(f, H.tk_off, kMax) &&
+              get_array(f, H.tk, kMax) && get_array(f, H.key_off, kMax) && get_array(f, H.key_bytes, kMax) &&
+              get_array(f, H.wild_w, kMax);
+    std::fclose(f);
+    if (!ok) return 0;
+    H.csize = sc[0];
+    H.gsz = sc[1];
+    H.gram_mode = sc[2];
+    H.short_term_len = sc[3];
+    H.short_query_len = sc[4];
+    H.full_scan_len = sc[5];
+    H.n_terms = sc[6];
+    H.n_short = sc[7];
+    H.n_keys = sc[8];
+    // the arrays must describe the counts (a truncated or foreign file is refused)
+    if ((H.csize != 1 && H.csize != 4) || H.gsz < 1 || H.gsz > kMaxGramSize || H.gram_mode > 1 ||
+        H.n_short > H.n_terms || H.term_off.size() != (size_t)H.n_terms + 1 ||
+        H.tk_off.size() != (size_t)H.n_terms + 1 || H.key_off.size() != (size_t)H.n_keys + 1 ||
+        H.wild_w.size() != H.n_keys || H.term_bytes.size() != H.term_off.back() * H.csize ||
+        H.tk.size() != H.tk_off.back() || H.key_bytes.size() != H.key_off.back() * H.csize)
+        return 0;
+    for (const uint2& kw : H.tk)
+        if (kw.x >= H.n_keys) return 0;
+    H.indexed = true;
+    H.grams_built = false;
+    const uint32_t handle = new_library([&](HostIndex& dst) {
+        dst = std::move(H);
+        if (dst.gram_mode == 1) build_grams_host(dst);  // dictionary indexes: the gram CSR on the host
+    });
+    if (handle) {
+        std::shared_lock<std::shared_mutex> lk(g_lock);
+        if (Library* L = find_lib(handle)) {
+            std::lock_guard<std::mutex> g(L->valid_mu);
+            std::memcpy(L->valid, valid, sizeof valid);
+        }
+    }
+    return handle;
 }
 
 NGS_API int ngsPhaseStats(uint64_t* out, int n, int reset) {

@@ -9,6 +9,7 @@ batched extension that puts a whole query batch through one GPU pass.
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 from . import _native
 
@@ -49,8 +50,41 @@ class StringIndex:
         if not self.handle:
             raise RuntimeError(f"{self._INDEX} failed (no usable GPU, or gram_size not in 1..3?) — see stderr")
 
+    def save(self, path) -> None:
+        """Writes the index to `path` (ngsSaveIndex): the interned library; `load` rebuilds the
+        rest on the GPU."""
+        rc = _native.lib().ngsSaveIndex(self.handle, os.fsencode(path))
+        if rc:
+            raise OSError(f"ngsSaveIndex({path!r}) failed: {rc}")
+
+    @classmethod
+    def load(cls, path, devices=None):
+        """An index from a file `save` wrote (ngsLoadIndex), of the same width as the saved one."""
+        L = _native.lib()
+        if devices is not None:
+            ds = (C.c_int * max(1, len(devices)))(*devices)
+            rc = L.ngsSetDevices(ds, len(devices))
+            if rc:
+                raise RuntimeError(f"ngsSetDevices({list(devices)}) failed: {rc}")
+        try:
+            handle = L.ngsLoadIndex(os.fsencode(path))
+        finally:
+            if devices is not None:
+                L.ngsSetDevices(None, 0)
+        if not handle:
+            raise OSError(f"ngsLoadIndex({path!r}) failed: not an index file, or no usable GPU")
+        cs = L.ngsCharSize(handle)
+        if cs != cls._CS:
+            L.dispose(handle)
+            raise TypeError(f"{path!r} holds an index of {cs}-byte characters, not {cls.__name__}'s")
+        self = cls.__new__(cls)
+        self.handle = handle
+        self._keep = None
+        return self
+
     # -- per-width plumbing (overridden by WideStringIndex) ------------------------------
     _INDEX = "indexN"
+    _CS = 1  # bytes per character
 
     @staticmethod
     def _words(words):
@@ -199,6 +233,7 @@ class WideStringIndex(StringIndex):
     of ints for raw code units such as values above 0x10FFFF), gram_size 1..3."""
 
     _INDEX = "indexW"
+    _CS = 4
     _RES = C.POINTER(_U32P)
     _fn = {"search": "searchW", "score": "scoreW", "release": "releaseW", "scoreBatch": "scoreBatchW",
            "key": "ngsKeyW"}
