@@ -2403,8 +2403,53 @@ __device__ __forceinline__ void emit_query(EmitSmem& S, const uint32_t q, const 
     uint64_t tau = kNoCand;
     // the query's characters only for an exact-match test (a survivor scoring > 0.999), rare
     bool have_q = false;
+    // one pair per term (DevIndex.tk_identity): a software pipeline over the batches of 64: while
+    // batch b is scored, batch b + 1's pairs and batch b + 2's survivors load (a threshold-0
+    // query has thousands of survivors, and a batch is otherwise two dependent round trips)
+    uint32_t base0 = 0;
+    if (X.tk_identity && sn > 64) {
+        uint32_t t0 = t, c0 = code, t1 = 0, c1 = 0;
+        if (64 + lane < sn) {
+            t1 = et[64 + lane];
+            c1 = ec[64 + lane];
+        }
+        uint2 k0 = X.tk[lane < sn ? t0 : 0u];
+        for (uint32_t base = 0; base < sn; base += 64) {
+            const uint32_t i = base + lane;
+            uint32_t t2 = 0, c2 = 0;
+            if (i + 128 < sn) {
+                t2 = et[i + 128];
+                c2 = ec[i + 128];
+            }
+            const uint2 k1 = X.tk[i + 64 < sn ? t1 : 0u];
+            const float s_l = __shfl(sc_long, (int)(c0 & 63u)), s_s = __shfl(sc_short, (int)(c0 & 63u));
+            const float s = (c0 & 0x80u) ? s_s : s_l;
+            const bool promo = (double)s > 0.999;  // nGramSearch.hpp:328
+            if (!have_q && __ballot(i < sn && promo)) {
+                const uint8_t* qg = qnorm + qoff[q];
+                for (uint32_t k = lane; k < m; k += 64) S.q[k] = char_at(qg, k, X.csize);
+                wave_sync();
+                have_q = true;
+            }
+            uint32_t p = 0, pe = 0;
+            if (i < sn) term_pairs(X, t0, s, promo, tau, p, pe);  // p == t0 unless pruned
+            uint64_t rec = kNoCand;
+            if (p < pe) rec = ((uint64_t)(~pair_enc(k0, s, promo, X, S.q, 4u, m, P.valid)) << 32) | k0.x;
+            if (cand_n + 64 > (uint32_t)kWaveCand) wave_flush(S, cand_n, tau, L, X.keys_unique != 0);
+            const bool want = rec < tau;
+            const unsigned long long bw = __ballot(want);
+            if (want) S.cand()[cand_n + rank_below(bw)] = rec;
+            cand_n += __popcll(bw);
+            t0 = t1;
+            c0 = c1;
+            k0 = k1;
+            t1 = t2;
+            c1 = c2;
+        }
+        base0 = sn;
+    }
     // wave_emit over the survivors in HBM
-    for (uint32_t base = 0; base < sn; base += 64) {
+    for (uint32_t base = base0; base < sn; base += 64) {
         const uint32_t i = base + lane;
         // the next 64 survivors load while this batch's pairs do (one round trip per batch)
         uint32_t t_next = 0, code_next = 0;
