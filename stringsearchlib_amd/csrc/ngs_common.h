@@ -134,6 +134,9 @@ constexpr bool kSkipCold = NGS_SKIP_COLD != 0;  // skip the sketch candidate pas
 #endif
 // one-wave sketch add pass without per-entry mask bits (segment-edge entries counted too)
 constexpr bool kSketchLoose = NGS_SKETCH_LOOSE != 0;
+#ifndef NGS_ADD_BATCH
+#define NGS_ADD_BATCH 1  // a round's four sketch adds issued before their results are read
+#endif
 constexpr uint32_t kListSlots = 64;             // slot lists per routing list in k_prep
 constexpr uint32_t kNoEmit = 0xFFFFFFFFu;       // esn[q]: query not finished by tier 1a
 constexpr uint32_t kEmitHeavy = 0x80000000u;    // esn[q] flag: finished by the heavy-list launch

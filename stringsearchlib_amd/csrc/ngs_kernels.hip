@@ -1334,12 +1334,23 @@ __device__ __forceinline__ uint32_t part_sketch(WaveSmem<W, LEAN>& S, const uint
         for (uint32_t r = 0; r < (uint32_t)NR; ++r) {
             if (64 * r < mt && 64 * r + lane < mt) {
                 const uint32_t t[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
+#if NGS_ADD_BATCH
+                // the round's four returning adds issued together, then their values read (one LDS
+                // wait per round: +3 % once the VALU diet left latency to hide, 31.5 -> 32.4 Mq/s)
+                uint32_t old[4];
+#pragma unroll
+                for (uint32_t e = 0; e < 4; ++e)
+                    old[e] = atomicAdd(sketch_word<W, LEAN>(S.table, t[e]), 1u << (sketch_sh4<W, LEAN>(t[e]) & 31u));
+#pragma unroll
+                for (uint32_t e = 0; e < 4; ++e) seen = max(seen, __builtin_amdgcn_ubfe(old[e], sketch_sh4<W, LEAN>(t[e]), 4u));
+#else
 #pragma unroll
                 for (uint32_t e = 0; e < 4; ++e) {
                     const uint32_t sh4 = sketch_sh4<W, LEAN>(t[e]);
                     const uint32_t old = atomicAdd(sketch_word<W, LEAN>(S.table, t[e]), 1u << (sh4 & 31u));
                     seen = max(seen, __builtin_amdgcn_ubfe(old, sh4, 4u));
                 }
+#endif
             }
         }
         ovf = seen == kSketchMax;
@@ -1491,12 +1502,12 @@ __device__ __forceinline__ uint32_t part_ones(WaveSmem<1, true>& S, const uint4 
     for (uint32_t r = 0; r < (uint32_t)NR; ++r) {
         if (64 * r < mt && 64 * r + lane < mt) {
             const uint32_t t[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
+            uint32_t old[4];  // (the four adds issued together, as in part_sketch)
 #pragma unroll
-            for (uint32_t e = 0; e < 4; ++e) {
-                const uint32_t sh4 = sketch_sh4<1, true>(t[e]);
-                const uint32_t old = atomicAdd(sketch_word<1, true>(S.table, t[e]), 1u << (sh4 & 31u));
-                seen = max(seen, __builtin_amdgcn_ubfe(old, sh4, 4u));
-            }
+            for (uint32_t e = 0; e < 4; ++e)
+                old[e] = atomicAdd(sketch_word<1, true>(S.table, t[e]), 1u << (sketch_sh4<1, true>(t[e]) & 31u));
+#pragma unroll
+            for (uint32_t e = 0; e < 4; ++e) seen = max(seen, __builtin_amdgcn_ubfe(old[e], sketch_sh4<1, true>(t[e]), 4u));
         }
     }
     const bool ovf = __ballot(seen == kSketchMax) != 0;
