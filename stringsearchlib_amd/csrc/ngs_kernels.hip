@@ -381,7 +381,7 @@ __device__ void bitonic_sort(uint64_t* a, uint32_t n) {
     for (uint32_t k = 2; k <= n; k <<= 1) {
         for (uint32_t j = k >> 1; j > 0; j >>= 1) {
             for (uint32_t p = tid; p < n / 2; p += kFastThreads) {
-                const uint32_t i = (p / j) * 2 * j + (p % j), l = i + j;
+                const uint32_t i = ((p & ~(j - 1u)) << 1) | (p & (j - 1u)), l = i + j;  // j is a power of two
                 const uint64_t x = a[i], y = a[l];
                 if ((x > y) == ((i & k) == 0)) { a[i] = y; a[l] = x; }
             }
@@ -978,7 +978,7 @@ __device__ void wave_flush(SM& S, uint32_t& cand_n, uint64_t& tau, uint32_t L, b
         for (uint32_t k = 2; k <= P2; k <<= 1) {
             for (uint32_t j = k >> 1; j > 0; j >>= 1) {
                 for (uint32_t p = lane; p < P2 / 2; p += 64) {
-                    const uint32_t i = (p / j) * 2 * j + (p % j), l = i + j;
+                    const uint32_t i = ((p & ~(j - 1u)) << 1) | (p & (j - 1u)), l = i + j;  // j is a power of two
                     const uint64_t x = S.cand()[i], y = S.cand()[l];
                     if ((x > y) == ((i & k) == 0)) { S.cand()[i] = y; S.cand()[l] = x; }
                 }
