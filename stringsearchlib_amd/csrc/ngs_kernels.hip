@@ -170,6 +170,13 @@ __global__ __launch_bounds__(64) void k_prep(const uint8_t* __restrict__ raw, co
     }
 }
 
+#ifndef NGS_G1S_CAP
+// workgroups of the sliced hand-over launches (grid-stride); C4, whose 26,594 hand-overs of a
+// batch run as 4 slices each: 65,536 -> 443-446 ms, 16,384 -> 457-463, 4,096 -> 541 per batch
+// (static striding balances worse than the hardware dispatcher); C3/C5 within noise
+#define NGS_G1S_CAP 65536
+#endif
+
 // ---------------------------------------------------------------- shared helpers -----
 // libStr = escapeBlank(key); trim; libStr == query (nGramSearch.hpp:330-334: the key is NOT
 // upper-cased, so only keys already in query form promote).
@@ -2782,7 +2789,7 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
             // hand-overs (side), and the full list through tier 1b (side2)
             const uint32_t g1b = std::min<uint32_t>(P.n_queries, 4096);  // grid-stride over the list
             // sliced tier-1b launches: a wave per (query, slice)
-            const uint32_t g1s = std::min<uint32_t>(P.n_queries * std::max<uint32_t>(P.nslices, 1u), 16384);
+            const uint32_t g1s = std::min<uint32_t>(P.n_queries * std::max<uint32_t>(P.nslices, 1u), NGS_G1S_CAP);
             const uint32_t gh = std::min<uint32_t>(P.n_queries, P.heavy_grid ? P.heavy_grid : 4096);
             // (esn[] was reset by k_prep)
             auto main_lean = [&]() {
