@@ -99,9 +99,9 @@ constexpr int kDmaRounds = kWaveChunks / 64;    // dwordx4 loads per lane for on
 #define NGS_LEAN_CELL_XOR 0  // tier-1a sketch cell: 1 = (t ^ t >> 13) & mask, 0 = t & mask
 #endif
 #ifndef NGS_WPS
-#define NGS_WPS 4
+#define NGS_WPS 3
 #endif
-constexpr int kWaveWavesPerSimd = NGS_WPS;      // occupancy target of tier 1b: 4 -> <= 128 VGPRs
+constexpr int kWaveWavesPerSimd = NGS_WPS;      // occupancy target of tier 1b: 3 -> <= 168 VGPRs (C4 -7 % time against 4)
 #ifndef NGS_LEAN_WPS
 #define NGS_LEAN_WPS 6
 #endif
