@@ -6,10 +6,12 @@
  * binds the reference through its C ABI binds this library unchanged.
  *
  * The search path runs on the GPU: queries are normalised, hashed into 3-grams, matched
- * against gram -> term posting lists kept as CSR in HBM, counted in LDS hash tables,
- * weighted, merged per key and cut to `limit` by HIP kernels for gfx950. indexN builds
- * the CSR on the host and uploads it once. There is no CPU search fallback: if no GPU
- * is usable, indexN prints the HIP error and returns 0.
+ * against gram -> term posting lists kept as CSR in HBM, counted in a u4 count-sketch in LDS
+ * (candidates resolved exactly; exact LDS hash counting where the sketch cannot decide),
+ * weighted, merged per key and cut to `limit` by HIP kernels for gfx950. indexN interns the
+ * strings and builds the CSR on the GPU (ngs_intern.hip, ngs_build.hip; gram dictionaries of
+ * other gram sizes on the host) and keeps it resident. There is no CPU search fallback: if no
+ * GPU is usable, indexN prints the HIP error and returns 0.
  *
  * Threading: one global reader/writer lock, as the reference (dllmain.cpp:22). indexN and
  * dispose are exclusive; everything else may run concurrently (each call takes its own
@@ -125,7 +127,8 @@ NGS_API int ngsSetDevice(int device);
  * allowed; n = 0 restores the default). score/search/scoreBatch/searchBatch on such a handle
  * split a batch of at least 4,096 queries per replica into contiguous slices, one per replica,
  * scored concurrently (one host thread and stream each) and joined in query order: the results
- * are those of one device. ngsSearchDevice uses the replica on the caller's current device.
+ * are those of one device. ngsSearchDevice uses the replica on the caller's current device
+ * (-3 if the index has none there).
  * Returns 0, or a negative HIP error code (nothing changed). */
 NGS_API int ngsSetDevices(const int* devices, int n);
 /* Replicas of the index (devices it was placed on); -1 for an unknown handle. */
@@ -173,6 +176,10 @@ typedef struct {
     uint64_t full_queries;     /* listed by the prep kernel for tier 1b from the start (cmin 1, short search) */
 } ngs_stats;
 NGS_API int ngsSetTiming(uint32_t handle, int enable);
+/* The last HIP error code a call on this thread failed with (0: none); clear != 0 resets it.
+ * The reference entry points answer 0 on failure, indistinguishable from "no results": a caller
+ * that must tell them apart asks here afterwards. */
+NGS_API int ngsLastError(int clear);
 NGS_API int ngsLastStats(uint32_t handle, ngs_stats* out);
 
 /* Test support: digests of the index as the kernels read it, for comparing the GPU index build

@@ -131,6 +131,9 @@ def lib():
                                   C.c_void_p, C.c_void_p]
     L.ngsSetTiming.restype = C.c_int
     L.ngsSetTiming.argtypes = [u32, C.c_int]
+    if hasattr(L, "ngsLastError"):  # (experiment builds of older sources lack it)
+        L.ngsLastError.restype = C.c_int
+        L.ngsLastError.argtypes = [C.c_int]
     L.ngsLastStats.restype = C.c_int
     L.ngsLastStats.argtypes = [u32, C.POINTER(NgsStats)]
     L.ngsIndexDigest.restype = C.c_int

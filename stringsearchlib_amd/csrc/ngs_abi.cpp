@@ -43,9 +43,14 @@ constexpr size_t kSioStats = sizeof(DevStats) * (kStatSlots + 1);
 constexpr size_t kSioBytes = kSioStats + kSmallBlock + kSmallQ;
 constexpr int kRetryQcap = -6;                       // finish_search: rerun with the batch's byte count
 
+// the last HIP failure on this thread (ngsLastError): the reference's entry points answer 0 on
+// failure, indistinguishable from "no results", so callers that care ask afterwards
+thread_local int t_last_error = 0;
+
 bool hip_ok(hipError_t e, const char* what) {
     if (e == hipSuccess) return true;
     std::fprintf(stderr, "ngram_search: %s failed: %s\n", what, hipGetErrorString(e));
+    t_last_error = (int)e;
     return false;
 }
 #define HIP_CHECK(expr) hip_ok((expr), #expr)
@@ -95,7 +100,8 @@ struct Context {
     hipEvent_t prep_ev = nullptr, lists_ev = nullptr;  // k_prep done (s), heavy / full lists merged (side)
     hipEvent_t ev[6] = {};
     size_t qcap = 0, bcap = 0, ncap = 0, ocap = 0;
-    uint32_t ecap = kEmitCap;  // survivor slots per query in d_est / d_esc (ensure_queries)
+    uint32_t ecap = kEmitCap;  // survivor slots per query in d_est / d_esc (ensure_queries, emit_cap)
+    size_t ebcap = 0;          // ... for this many queries
     uint8_t* d_raw = nullptr;
     uint64_t* d_off = nullptr;
     uint8_t* d_norm = nullptr;
@@ -243,11 +249,11 @@ struct Library {
     float w_max = 0.0f;
 
     ~Library() { reps.clear(); }
-    // the replica on `dev`, else the first
-    Replica& replica_on(int dev) {
+    // the replica on `dev`, or null
+    Replica* replica_at(int dev) {
         for (auto& r : reps)
-            if (r->device == dev) return *r;
-        return *reps.front();
+            if (r->device == dev) return r.get();
+        return nullptr;
     }
 };
 
@@ -415,19 +421,37 @@ bool upload(Library& L, const std::vector<int>& devs) {
     return true;
 }
 
-bool ensure_queries(Context& c, size_t B, size_t bytes) {
+// Survivor slots per query of tier 1a (d_est / d_esc, 5 bytes each): the wide cap only where a
+// typical query can be counted at cmin 1 (part_ones: thousands of one-hit survivors at C2's
+// threshold 0), i.e. thr <= 1/8 (queries of >= 8 grams), and for batches up to kEmitWideBatch:
+// 1.25 GiB per context at 65,536 queries. Above thr 1/8 only queries of < 8 grams can reach
+// cmin 1, and those of them with more survivors than kEmitCap go to tier 1b.
+uint32_t emit_cap(size_t B, float thr) {
+    return (thr <= 0.125f && B <= kEmitWideBatch) ? std::max(kEmitCap, kEmitCapWide) : kEmitCap;
+}
+
+bool ensure_queries(Context& c, size_t B, size_t bytes, float thr) {
     if (B > c.bcap) {
         for (void** p : {(void**)&c.d_off, (void**)&c.d_qm, (void**)&c.d_glist, (void**)&c.d_list2, (void**)&c.d_fb,
-                         (void**)&c.d_fb2, (void**)&c.d_heavy, (void**)&c.d_full, (void**)&c.d_lslots, (void**)&c.d_esn, (void**)&c.d_est, (void**)&c.d_esc})
+                         (void**)&c.d_fb2, (void**)&c.d_heavy, (void**)&c.d_full, (void**)&c.d_lslots, (void**)&c.d_esn})
             if (*p) { hipFree(*p); *p = nullptr; }
         size_t nb = std::max<size_t>(B, 1024);
-        c.ecap = nb <= kEmitWideBatch ? std::max(kEmitCap, kEmitCapWide) : kEmitCap;
         if (!dev_alloc(&c.d_off, nb + 1) || !dev_alloc(&c.d_qm, nb) || !dev_alloc(&c.d_glist, nb) ||
             !dev_alloc(&c.d_list2, nb) || !dev_alloc(&c.d_fb, nb) || !dev_alloc(&c.d_fb2, nb) || !dev_alloc(&c.d_heavy, nb) || !dev_alloc(&c.d_full, nb) ||
-            !dev_alloc(&c.d_lslots, 2 * (nb + kListSlots)) ||
-            !dev_alloc(&c.d_esn, nb) || !dev_alloc(&c.d_est, nb * c.ecap) || !dev_alloc(&c.d_esc, nb * c.ecap))
+            !dev_alloc(&c.d_lslots, 2 * (nb + kListSlots)) || !dev_alloc(&c.d_esn, nb))
             return false;
         c.bcap = nb;
+    }
+    // the survivor slots: (re)allocated when the batch or the cap this call needs outgrows them
+    const uint32_t want = emit_cap(B, thr);
+    if (!c.d_est || B > c.ebcap || want > c.ecap) {
+        for (void** p : {(void**)&c.d_est, (void**)&c.d_esc})
+            if (*p) { hipFree(*p); *p = nullptr; }
+        const size_t nb = std::max<size_t>({B, 1024, c.ebcap});
+        c.ebcap = 0;
+        if (!dev_alloc(&c.d_est, nb * want) || !dev_alloc(&c.d_esc, nb * want)) return false;
+        c.ecap = want;
+        c.ebcap = nb;
     }
     if (bytes > c.qcap) {
         for (void** p : {(void**)&c.d_raw, (void**)&c.d_norm})
@@ -557,7 +581,7 @@ int queue_search(Library& L, Replica& R, Context& c, const uint8_t* d_raw, const
         std::lock_guard<std::mutex> g(L.valid_mu);
         std::memcpy(P.valid, L.valid, sizeof(P.valid));
     }
-    if (!ensure_queries(c, B, qbytes)) return -4;
+    if (!ensure_queries(c, B, qbytes, thr)) return -4;
     P.esn = c.d_esn;
     P.est = c.d_est;
     P.esc = c.d_esc;
@@ -755,7 +779,7 @@ bool host_search_one(Library& L, Replica& R, const CharT* const* queries, uint32
             if (!ok) break;
             for (uint32_t i = 0; i < B; ++i)
                 if (queries[q0 + i]) std::memcpy(c->h_raw.as<uint8_t>() + ho[i], queries[q0 + i], ho[i + 1] - ho[i]);
-            ok = ensure_queries(*c, B, qbytes) && ensure_outputs(*c, B, stride) &&
+            ok = ensure_queries(*c, B, qbytes, thr) && ensure_outputs(*c, B, stride) &&
                  HIP_CHECK(hipMemcpyAsync(c->d_raw, c->h_raw.p, qbytes, hipMemcpyHostToDevice, c->stream)) &&
                  HIP_CHECK(hipMemcpyAsync(c->d_off, ho, sizeof(uint64_t) * (B + 1), hipMemcpyHostToDevice, c->stream));
             d_raw = c->d_raw;
@@ -1141,8 +1165,9 @@ NGS_API int ngsSearchDevice(uint32_t handle, const uint8_t* dQueryBytes, const u
     // the replica on the caller's current device (the buffers' device)
     int cur = L->device;
     if (!HIP_CHECK(hipGetDevice(&cur))) return -4;
-    Replica& R = L->replica_on(cur);
-    if (!HIP_CHECK(hipSetDevice(R.device))) return -4;
+    Replica* Rp = L->replica_at(cur);
+    if (!Rp) return -3;  // no replica on the caller's device: its buffers and stream belong there
+    Replica& R = *Rp;
     hipStream_t s = (hipStream_t)stream;
     if (Lm == 0) {
         return HIP_CHECK(hipMemsetAsync(dCounts, 0, sizeof(uint32_t) * nQueries, s)) &&
@@ -1172,6 +1197,12 @@ NGS_API int ngsSearchDevice(uint32_t handle, const uint8_t* dQueryBytes, const u
     }
     R.give_back(std::move(c));
     return rc;
+}
+
+NGS_API int ngsLastError(int clear) {
+    const int e = t_last_error;
+    if (clear) t_last_error = 0;
+    return e;
 }
 
 NGS_API int ngsSetTiming(uint32_t handle, int enable) {
@@ -1352,6 +1383,29 @@ NGS_API uint32_t ngsLoadIndex(const char* path) {
         return 0;
     for (const uint2& kw : H.tk)
         if (kw.x >= H.n_keys) return 0;
+    // every offset array ascends from 0 to its array's end (a crafted file must not send the
+    // kernels or marshal() out of bounds), every key ends in a NUL, the length parameters are the
+    // gram size's, and the short / long term split matches the term lengths
+    auto ascending = [](const auto& off) {
+        if (off.empty() || off.front() != 0) return false;
+        for (size_t i = 1; i < off.size(); ++i)
+            if (off[i] < off[i - 1]) return false;
+        return true;
+    };
+    if (!ascending(H.term_off) || !ascending(H.tk_off) || !ascending(H.key_off)) return 0;
+    if (H.short_term_len != 2 * H.gsz || H.short_query_len != 3 * H.gsz || H.full_scan_len != H.gsz ||
+        H.gram_mode != ((H.csize == 1 && H.gsz == 3) ? 0u : 1u))
+        return 0;
+    for (uint32_t k = 0; k < H.n_keys; ++k) {
+        if (H.key_off[k + 1] == H.key_off[k]) return 0;  // not even the NUL
+        const uint64_t last = (H.key_off[k + 1] - 1) * H.csize;
+        for (uint32_t b = 0; b < H.csize; ++b)
+            if (H.key_bytes[last + b] != 0) return 0;
+    }
+    for (uint32_t t = 0; t < H.n_terms; ++t) {
+        const bool is_short = H.term_off[t + 1] - H.term_off[t] < H.short_term_len;
+        if (is_short != (t < H.n_short)) return 0;
+    }
     H.indexed = true;
     H.grams_built = false;
     const uint32_t handle = new_library([&](HostIndex& dst) {

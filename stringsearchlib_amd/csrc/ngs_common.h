@@ -137,6 +137,12 @@ constexpr bool kSketchLoose = NGS_SKETCH_LOOSE != 0;
 #ifndef NGS_ADD_BATCH
 #define NGS_ADD_BATCH 1  // a round's four sketch adds issued before their results are read
 #endif
+#ifndef NGS_LEAN_G4
+#define NGS_LEAN_G4 0  // 1: tier-1a staging reads each list's chunk base from LDS (measured 1.5 % slower)
+#endif
+#ifndef NGS_LEAN_DEFER_SKIP
+#define NGS_LEAN_DEFER_SKIP 0  // 1: tier 1a issues the next skip-table read after the part's loads (1 % slower)
+#endif
 constexpr uint32_t kListSlots = 64;             // slot lists per routing list in k_prep
 constexpr uint32_t kNoEmit = 0xFFFFFFFFu;       // esn[q]: query not finished by tier 1a
 constexpr uint32_t kEmitHeavy = 0x80000000u;    // esn[q] flag: finished by the heavy-list launch

@@ -12,6 +12,9 @@
 // (-ffp-contract=off); threshold `s < thr` in fp32; promotion test `(double)s > 0.999`.
 #include <hipcub/hipcub.hpp>
 
+#include <cstdio>
+#include <cstdlib>
+
 #include "ngs_kernels.h"
 
 namespace ngs {
@@ -878,6 +881,7 @@ struct alignas(16) WaveSmem {
     uint2 segtab[W][64];             // staging, per wave: per list {first chunk - position, first | end entry << 16}
     uint8_t mark[W][kWaveChunks];    // staging, per wave: list index + 1 at the (wave-local) position of its first chunk
     unsigned long long lstart[kDmaRounds];  // tier 1a staging: bit (pre - 1) per list start, 64 chunk positions a word
+    uint32_t g4[LEAN ? 64 : 1];      // tier 1a: per list lane, the 16-byte chunk of its list's first posting
     uint32_t surv_t[kWaveSurv];      // survivor terms
     uint32_t cbuf[64];               // sketch candidates (terms)
     uint8_t surv_c[kWaveSurv];       // hit count, | 0x80 for a Levenshtein (short search) match count
@@ -2020,16 +2024,33 @@ __device__ __forceinline__ void lean_stage(WaveSmem<1, true>& S, gptr<uint4> pos
     const uint32_t pre = incl - nch;
     const uint32_t ord = rank_below(__ballot(nch != 0));
     mt = __builtin_amdgcn_readfirstlane(mt);
-    if (lane < (uint32_t)kDmaRounds) S.lstart[lane] = 0;
+    uint32_t g4 = 0;
+#if NGS_LEAN_G4
+    // the list's chunk base lives in LDS (S.g4, written once per query): values the part loop
+    // keeps in registers past 80 VGPRs were spilled to scratch, and a scratch reload's vmcnt(0)
+    // waited for every load in flight, the next part's included
+    if (nch) g4 = S.g4[lane];
+    (void)gbase;
+#else
+    g4 = (uint32_t)(gbase >> 2);
+#endif
+    {
+        // the zero and its address made here, for the same reason
+        uint32_t z, l = lane;
+        asm volatile("v_mov_b32 %0, 0" : "=v"(z), "+v"(l));
+        if (l < (uint32_t)kDmaRounds) S.lstart[l] = (unsigned long long)z;
+    }
     wave_sync();
     if (nch) {
         if (pre) atomicOr(&S.lstart[(pre - 1) >> 6], 1ull << ((pre - 1) & 63u));
-        const uint32_t first = (uint32_t)((gbase + cur) >> 2);
+        const uint32_t first = g4 + ((a0 + cur) >> 2);  // the list's chunk base (u32: chunk ids < 2^32)
         S.segtab[0][ord] = make_uint2(first - pre, (4 * pre + head) | ((4 * pre + head + len) << 16));
     }
     wave_sync();
     uint32_t below = 0;  // list starts in the earlier words
     vmask = 0;
+    uint32_t lo = lane;  // opaque: chunk positions are made per round, not hoisted (and spilled)
+    asm volatile("" : "+v"(lo));
 #pragma unroll
     for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) {
         if (64 * r < mt) {
@@ -2038,7 +2059,7 @@ __device__ __forceinline__ void lean_stage(WaveSmem<1, true>& S, gptr<uint4> pos
             const uint32_t whi = __builtin_amdgcn_readfirstlane((uint32_t)(wd >> 32));
             const uint32_t idx = __builtin_amdgcn_mbcnt_hi(whi, __builtin_amdgcn_mbcnt_lo(wlo, below));
             below += (uint32_t)__popc(wlo) + (uint32_t)__popc(whi);
-            const uint32_t c = 64 * r + lane;
+            const uint32_t c = 64 * r + lo;
             const bool ok = c < mt;
             const uint2 seg = S.segtab[0][idx & 63u];
             if (ok) v[r] = post4[seg.x + c];  // inactive lanes load nothing
@@ -2170,6 +2191,7 @@ __device__ __forceinline__ void lean_query(WaveSmem<1, true>& S, const uint32_t 
         gptr<uint4> post4 = (gptr<uint4>)reinterpret_cast<const uint4*>(X.post);
         asm volatile("" : "+s"(post4));
         const uint32_t a0 = (uint32_t)gbase & 3u;  // list start within its 16-byte chunk
+        if (NGS_LEAN_G4) S.g4[lane] = (uint32_t)(gbase >> 2);  // ... and its chunk (post holds < 2^34 entries)
         // entries [s, e) of this lane's list cover 16-byte chunks [(a0 + s) / 4, (a0 + e + 3) / 4)
         auto chunks = [a0](uint32_t s, uint32_t e) -> uint32_t { return e > s ? ((a0 + e + 3) >> 2) - ((a0 + s) >> 2) : 0u; };
         // end of the next bucket group: skip[row][min(K, bn + w)]; idle lanes load nothing
@@ -2205,9 +2227,9 @@ __device__ __forceinline__ void lean_query(WaveSmem<1, true>& S, const uint32_t 
                 if (tot && tot <= kChunks) {
                     len = e - cur;
                     bnext = min(K, bnext + w);
-                    if (lane < ng) e_pre = next_end(bnext);
+                    if (!NGS_LEAN_DEFER_SKIP && lane < ng) e_pre = next_end(bnext);
                     have_p = true;
-                    fast = true;
+                    fast = true;  // e_pre of the next group loads after this part's loads (below)
                 }
             }
             WSTAMP(2);
@@ -2280,6 +2302,9 @@ __device__ __forceinline__ void lean_query(WaveSmem<1, true>& S, const uint32_t 
                 p_mt = tot;
                 cur += len;
             }
+            // the fast path's skip-table read for the group after: issued behind the part's loads,
+            // so that nothing in staging waits for it (it is read at the next part's planning)
+            if (NGS_LEAN_DEFER_SKIP && fast && lane < ng) e_pre = next_end(bnext);
             WSTAMP(4);
             // ---- count part i while part i+1 is in flight ----
             if (have_c) {
@@ -2755,6 +2780,23 @@ __global__ __launch_bounds__(256) void k_lists(const uint32_t* __restrict__ slot
     }
 }
 
+// NGS_SYNC_DEBUG=1 (diagnostics): every launch of a search is followed by a wait on its stream,
+// and the first kernel whose wait fails is named on stderr (a fault is otherwise reported by a
+// later, unrelated call)
+static bool sync_debug() {
+    static const bool on = [] {
+        const char* e = std::getenv("NGS_SYNC_DEBUG");
+        return e && std::atoi(e) != 0;
+    }();
+    return on;
+}
+static void dbg_check(hipStream_t s, const char* what) {
+    if (!sync_debug()) return;
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) std::fprintf(stderr, "ngram_search: NGS_SYNC_DEBUG: %s failed: %s\n", what, hipGetErrorString(e));
+}
+
 hipError_t launch_prep(const uint8_t* raw, const uint64_t* off, uint32_t B, const SearchParams& P, uint8_t* qnorm,
                        uint32_t* qm, uint32_t cs, const DevIndex& X, uint32_t* heavy, uint32_t* hcount,
                        uint32_t* full, uint32_t* fcount, uint32_t* slots, uint32_t* ctr, hipStream_t s,
@@ -2764,11 +2806,13 @@ hipError_t launch_prep(const uint8_t* raw, const uint64_t* off, uint32_t B, cons
     const bool lists = P.waves == 0;
     hipLaunchKernelGGL(k_prep, dim3((B + 3) / 4), dim3(64), 0, s, raw, off, B, P, qnorm, qm, cs, X,
                        lists ? slots : nullptr, ctr, cap);
+    dbg_check(s, "k_prep");
     if (lists) {  // on the side stream: the main tier-1a launch needs only k_prep's output
         hipError_t e;
         if ((e = hipEventRecord(prep_ev, s)) != hipSuccess || (e = hipStreamWaitEvent(side, prep_ev, 0)) != hipSuccess)
             return e;
         hipLaunchKernelGGL(k_lists, dim3(1), dim3(256), 0, side, slots, ctr, cap, heavy, hcount, full, fcount);
+        dbg_check(side, "k_lists");
         if ((e = hipEventRecord(lists_ev, side)) != hipSuccess) return e;
     }
     return hipGetLastError();
@@ -2796,6 +2840,7 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
                 hipLaunchKernelGGL(k_wave_lean<kDeferEmit>, dim3(P.n_queries), dim3(64), 0, s, X, P, qnorm, off, qm,
                                    out_n, out_k, out_s, list2, count2, stats, fb, fbc, (const uint32_t*)nullptr,
                                    (const uint32_t*)nullptr);
+                dbg_check(s, "k_wave_lean");
             };
             // the main launch is queued first: the GPU idled ~35 us while the host queued the side
             // streams' launches ahead of it
@@ -2808,44 +2853,57 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
                 PH.lean_all = 1;
                 hipLaunchKernelGGL((k_wave_lean<true, kLeanOnes>), dim3(gh), dim3(64), 0, side, X, PH, qnorm, off, qm, out_n,
                                    out_k, out_s, list2, count2, stats, fb2, fbc2, heavy, hcount);
+                dbg_check(side, "k_wave_lean (heavy list)");
                 hipLaunchKernelGGL(k_emit, dim3((gh + kEmitWaves - 1) / kEmitWaves), dim3(64 * kEmitWaves), 0, side,
                                    X, PH, qnorm, off, qm, out_n, out_k, out_s, stats, heavy, hcount);
+                dbg_check(side, "k_emit (heavy list)");
                 hipLaunchKernelGGL(k_wave<1>, dim3(g1s), dim3(64), 0, side, X, P, qnorm, off, qm, out_n, out_k,
                                    out_s, list2, count2, stats, (const uint32_t*)fb2, (const uint32_t*)fbc2);
-                if (P.nslices > 1)
+                dbg_check(side, "k_wave<1> (heavy hand-overs)");
+                if (P.nslices > 1) {
                     hipLaunchKernelGGL(k_merge, dim3(g1b), dim3(64), 0, side, X, P, (const uint32_t*)fb2,
                                        (const uint32_t*)fbc2, out_n, out_k, out_s, stats);
+                    dbg_check(side, "k_merge (heavy hand-overs)");
+                }
             }
             if ((e = hipEventRecord(join, side)) != hipSuccess) return e;
             // side2 waits for the lists
             (void)fork;
             if ((e = hipStreamWaitEvent(side2, lists_ev, 0)) != hipSuccess) return e;
-            if (P.heavy_waves == 4)
+            if (P.heavy_waves == 4) {
                 hipLaunchKernelGGL(k_wave<4>, dim3(gh), dim3(256), 0, side2, X, P, qnorm, off, qm, out_n, out_k,
                                    out_s, list2, count2, stats, full, fcount);
-            else if (P.heavy_waves == 2)
+                dbg_check(side2, "k_wave<4> (full list)");
+            } else if (P.heavy_waves == 2) {
                 hipLaunchKernelGGL(k_wave<2>, dim3(gh), dim3(128), 0, side2, X, P, qnorm, off, qm, out_n, out_k,
                                    out_s, list2, count2, stats, full, fcount);
-            else {
+                dbg_check(side2, "k_wave<2> (full list)");
+            } else {
                 // unsliced: its cmin-1 parts are all counted exactly, and four slices of a C2 query
                 // measured 17 % slower than one wave (the hand-over lists below gain from slicing)
                 SearchParams PF = P;
                 PF.nslices = 1;
                 hipLaunchKernelGGL(k_wave<1>, dim3(gh), dim3(64), 0, side2, X, PF, qnorm, off, qm, out_n, out_k, out_s,
                                    list2, count2, stats, full, fcount);
+                dbg_check(side2, "k_wave<1> (full list)");
             }
             if ((e = hipEventRecord(join2, side2)) != hipSuccess) return e;
             if (!kMainFirst) main_lean();
-            if (kDeferEmit)
+            if (kDeferEmit) {
                 hipLaunchKernelGGL(k_emit, dim3((P.n_queries + kEmitWaves - 1) / kEmitWaves), dim3(64 * kEmitWaves), 0,
                                    s, X, P, qnorm, off, qm, out_n, out_k, out_s, stats, (const uint32_t*)nullptr,
                                    (const uint32_t*)nullptr);
+                dbg_check(s, "k_emit");
+            }
             // tier 1b over the queries tier 1a handed over
             hipLaunchKernelGGL(k_wave<1>, dim3(g1s), dim3(64), 0, s, X, P, qnorm, off, qm, out_n, out_k, out_s,
                                list2, count2, stats, (const uint32_t*)fb, (const uint32_t*)fbc);
-            if (P.nslices > 1)
+            dbg_check(s, "k_wave<1> (hand-overs)");
+            if (P.nslices > 1) {
                 hipLaunchKernelGGL(k_merge, dim3(g1b), dim3(64), 0, s, X, P, (const uint32_t*)fb, (const uint32_t*)fbc,
                                    out_n, out_k, out_s, stats);
+                dbg_check(s, "k_merge (hand-overs)");
+            }
             if ((e = hipStreamWaitEvent(s, join, 0)) != hipSuccess || (e = hipStreamWaitEvent(s, join2, 0)) != hipSuccess)
                 return e;
             break;
@@ -2854,22 +2912,28 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
             hipLaunchKernelGGL(k_wave<1>, dim3(P.n_queries * std::max<uint32_t>(P.nslices, 1u)), dim3(64), 0, s, X, P,
                                qnorm, off, qm, out_n, out_k, out_s, list2, count2, stats, (const uint32_t*)nullptr,
                                (const uint32_t*)nullptr);
-            if (P.nslices > 1)
+            dbg_check(s, "k_wave<1>");
+            if (P.nslices > 1) {
                 hipLaunchKernelGGL(k_merge, dim3(P.n_queries), dim3(64), 0, s, X, P, (const uint32_t*)nullptr,
                                    (const uint32_t*)nullptr, out_n, out_k, out_s, stats);
+                dbg_check(s, "k_merge");
+            }
             break;
         case 2:
             hipLaunchKernelGGL(k_wave<2>, dim3(P.n_queries), dim3(128), 0, s, X, P, qnorm, off, qm, out_n, out_k,
                                out_s, list2, count2, stats, (const uint32_t*)nullptr, (const uint32_t*)nullptr);
+            dbg_check(s, "k_wave");
             break;
         default:
             hipLaunchKernelGGL(k_wave<4>, dim3(P.n_queries), dim3(256), 0, s, X, P, qnorm, off, qm, out_n, out_k,
                                out_s, list2, count2, stats, (const uint32_t*)nullptr, (const uint32_t*)nullptr);
+            dbg_check(s, "k_wave");
             break;
     }
     const uint32_t grid2 = std::min<uint32_t>(P.n_queries, 1024);
     hipLaunchKernelGGL(k_fast, dim3(grid2), dim3(kFastThreads), 0, s, X, P, qnorm, off, qm, out_n, out_k, out_s,
                        (const uint32_t*)list2, (const uint32_t*)count2, glist, gcount, stats);
+    dbg_check(s, "k_fast");
     return hipGetLastError();
 }
 

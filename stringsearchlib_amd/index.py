@@ -20,6 +20,14 @@ def _b(s) -> bytes:
     return s if isinstance(s, bytes) else s.encode("latin-1")
 
 
+def _check(what: str) -> None:
+    """Raise if the last call on this thread hit a HIP error (ngsLastError): the reference's
+    entry points answer 0 on failure, which would otherwise read as "no results"."""
+    e = _native.lib().ngsLastError(1)
+    if e:
+        raise RuntimeError(f"{what} failed: HIP error {e} (see stderr)")
+
+
 class StringIndex:
     """One index of byte strings. gram_size 3 is the reference (indexN); 1 or 2 use the indexG
     extension (every reference threshold scaled by the gram size)."""
@@ -42,11 +50,14 @@ class StringIndex:
         w = None
         if weights is not None:
             w = (C.c_float * max(1, len(weights)))(*weights)
-        self._keep = self._words(words)  # alive during the build only
-        self.handle = self._index(L, self._keep if n else None, n, row_size, w, gram_size)
-        self._keep = None
-        if devices is not None:  # the device list applies to this build only
-            L.ngsSetDevices(None, 0)
+        self.handle = 0
+        try:
+            self._keep = self._words(words)  # alive during the build only
+            self.handle = self._index(L, self._keep if n else None, n, row_size, w, gram_size)
+        finally:
+            self._keep = None
+            if devices is not None:  # the device list applies to this build only
+                L.ngsSetDevices(None, 0)
         if not self.handle:
             raise RuntimeError(f"{self._INDEX} failed (no usable GPU, or gram_size not in 1..3?) — see stderr")
 
@@ -123,8 +134,10 @@ class StringIndex:
         L, f = _native.lib(), self._fn
         res = self._RES()
         sc = C.POINTER(C.c_float)()
+        L.ngsLastError(1)
         n = getattr(L, f["score"])(self.handle, self._q(query), C.byref(res), C.byref(sc), threshold, limit)
         if not n:
+            _check(f["score"])
             if res:
                 getattr(L, f["release"])(self.handle, res, sc)
             return []
@@ -136,7 +149,10 @@ class StringIndex:
         """dllmain.cpp:61: list of key bytes, best first."""
         L, f = _native.lib(), self._fn
         res = self._RES()
+        L.ngsLastError(1)
         n = getattr(L, f["search"])(self.handle, self._q(query), C.byref(res), threshold, limit)
+        if not n:
+            _check(f["search"])
         out = [self._string(res[i]) for i in range(n)]
         if res:
             getattr(L, f["release"])(self.handle, res, None)
@@ -150,8 +166,11 @@ class StringIndex:
         counts = (C.c_uint32 * max(1, nq))()
         res = self._RES()
         sc = C.POINTER(C.c_float)()
+        L.ngsLastError(1)
         total = getattr(L, f["scoreBatch"])(self.handle, qs, nq, threshold, limit, counts, C.byref(res),
                                             C.byref(sc))
+        if not total:
+            _check(f["scoreBatch"])
         out, o = [], 0
         for i in range(nq):
             c = counts[i]

@@ -64,6 +64,9 @@ class GatherBuffer:
     def decode(buf: torch.Tensor, stride: int, pad_b: int):
         """(counts, packed keys, packed scores) of a gathered buffer."""
         b = int(buf[0])
+        if not 0 <= b <= pad_b or buf.numel() != 1 + pad_b * (1 + 2 * stride):
+            raise ValueError(f"gathered buffer of batch {b} / {buf.numel()} words does not match pad_b {pad_b}, "
+                             f"stride {stride}")
         ko = 1 + pad_b
         so = ko + pad_b * stride
         return compact(buf[1:1 + b], buf[ko:ko + b * stride], buf[so:so + b * stride].view(torch.float32), stride)
@@ -103,6 +106,13 @@ def gather_to_root(counts, keys=None, scores=None, stride: int | None = None, gr
     else:
         if stride is None:
             raise ValueError("stride is required with tensor arguments")
+        if pad_b is None:
+            # uneven slices (n % world != 0) give ranks different batch sizes, and dist.gather of
+            # buffers of different lengths hangs or corrupts: agree on the largest one (one small
+            # all-reduce; callers that know it pass pad_b, e.g. shard.max_shard)
+            m = torch.tensor([counts.numel()], dtype=torch.int64, device=counts.device)
+            dist.all_reduce(m, op=dist.ReduceOp.MAX, group=group)
+            pad_b = int(m.item())
         gb = GatherBuffer(counts.numel(), stride, pad_b, counts.device).fill(counts, keys, scores)
     rank = dist.get_rank(group)
     world = dist.get_world_size(group)

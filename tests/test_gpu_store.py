@@ -80,4 +80,43 @@ def test_load_refuses_bad_files(tmp_path):
     assert L.ngsSaveIndex(987654, os.fsencode(str(tmp_path / "x.ngs"))) == -1
     with pytest.raises(TypeError):
         ssl.WideStringIndex.load(str(good))
+    # files whose counts agree but whose contents are inconsistent: each refused
+    for name, bad in _corruptions(data).items():
+        f = tmp_path / f"{name}.ngs"
+        f.write_bytes(bad)
+        assert L.ngsLoadIndex(os.fsencode(str(f))) == 0, name
     gi.dispose()
+
+
+def _corruptions(data: bytes) -> dict:
+    """Variants of a saved index file (layout: ngs_abi.cpp, "NGSIDX01" | 9 u32 scalars | 8 u32
+    validChar words | arrays as u64 count + elements) that keep every count consistent."""
+    import struct
+    pos = 8 + 9 * 4 + 8 * 4
+    arrays = {}
+    for name, width in [("term_off", 8), ("term_bytes", 1), ("tk_off", 4), ("tk", 8), ("key_off", 8),
+                        ("key_bytes", 1), ("wild_w", 4)]:
+        (n,) = struct.unpack_from("<Q", data, pos)
+        arrays[name] = (pos + 8, n, width)
+        pos += 8 + n * width
+    assert pos == len(data)
+    out = {}
+
+    def patch(off, fmt, val):
+        b = bytearray(data)
+        struct.pack_into(fmt, b, off, val)
+        return bytes(b)
+
+    o, n, _ = arrays["term_off"]
+    out["term_off_descending"] = patch(o + 8 * (n // 2), "<Q", 0)
+    o, n, _ = arrays["key_off"]
+    out["key_off_descending"] = patch(o + 8 * (n // 3), "<Q", 0)
+    o, n, _ = arrays["tk_off"]
+    out["tk_off_first_nonzero"] = patch(o, "<I", 1)
+    o, n, _ = arrays["key_bytes"]
+    out["key_without_nul"] = patch(o + n - 1, "<B", ord("X"))
+    out["short_term_len"] = patch(8 + 3 * 4, "<I", 5)
+    out["gram_mode"] = patch(8 + 2 * 4, "<I", 1)
+    (n_short,) = struct.unpack_from("<I", data, 8 + 7 * 4)
+    out["n_short"] = patch(8 + 7 * 4, "<I", n_short + 1)
+    return out

@@ -53,6 +53,10 @@ def _worker(rank, world, port, result_path):
         pad_b = shard.max_shard(world, len(queries))
         c, k, s = _device_layout(oi, queries[lo:hi], stride)
         got = shard.gather_to_root(c, k, s, stride, pad_b=pad_b)
+        # without pad_b the ranks agree on the largest slice themselves (ragged 33 + 32 here)
+        got_default = shard.gather_to_root(c, k, s, stride)
+        if rank == 0:
+            assert all(torch.equal(a, b) for x, y in zip(got, got_default) for a, b in zip(x, y))
         # the in-flight form bench.py uses: results written into a GatherBuffer's views (as
         # ngsSearchDevice does), gathered without any size exchange, decoded after wait()
         gb = shard.GatherBuffer(hi - lo, stride, pad_b)
