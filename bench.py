@@ -16,6 +16,7 @@ the step also gathers the compacted top-k records on rank 0 over RCCL.
 from __future__ import annotations
 
 import argparse
+import collections
 import ctypes as C
 import json
 import os
@@ -54,6 +55,17 @@ CONFIGS = {
     "c5": dict(rows=50_000_000, batch=131072, threshold=0.3, limit=100, weights=False,
                workload="C5: 50M-row ASCII corpus, gSize=3, rowSize=1, weight=NULL, batch=131072/GPU "
                         "(2^20 over 8 GPUs), threshold=0.3, limit=100"),
+}
+
+
+# The reference DLL (nGramSearch/dllmain.cpp, g++ -O2) timed in the survey container on the same
+# synthetic spec: BASELINE.md. It cannot run on the GPU box (the reference does not travel), so
+# it is quoted beside the oracle port that is timed there.
+REFERENCE_DLL = {
+    "c3": {"value": 58.5, "unit": "queries/s", "cores": 8, "hardware": "8-vCPU Xeon (survey container)",
+           "sample": "4,096 of the 65,536 C3 queries, 8 caller threads", "source": "BASELINE.md"},
+    "c2": {"value": 1376.6, "unit": "queries/s", "cores": 8, "hardware": "8-vCPU Xeon (survey container)",
+           "sample": "C2 batch of 4,096 queries, 8 caller threads (265.5 q/s on 1)", "source": "BASELINE.md"},
 }
 
 
@@ -234,6 +246,8 @@ def main():
     ap.add_argument("--batch", type=int, default=None, help="override per-GPU batch (debug only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-dropin", action="store_true", help="skip the scoreBatch / score() latency lines")
+    ap.add_argument("--depth", type=int, default=2,
+                    help="batches in flight (ngsSearchDeviceAsync); 1 = one blocking ngsSearchDevice per step")
     args = ap.parse_args()
     cfg = dict(CONFIGS[args.config])
     if args.rows:
@@ -269,44 +283,76 @@ def main():
         d_raw = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(dev)
         d_off = torch.tensor(offs, dtype=torch.int64, device=dev)
     stride = min(cfg["limit"], n_keys)
-    # results go straight into the fused gather buffers (shard.GatherBuffer); two of them in turn,
-    # so step i writes one while step i-1's gather still reads the other
-    gbs = [shard.GatherBuffer(B, stride, B, dev) for _ in range(2 if world > 1 else 1)]
+    depth = max(1, args.depth)
+    # results go straight into the fused gather buffers (shard.GatherBuffer), used in turn: a
+    # buffer is rewritten only after the batch that last wrote it was waited for and its gather
+    # (N > 1) ordered before the rewrite
+    nbuf = depth + 1 if depth > 1 else (2 if world > 1 else 1)
+    gbs = [shard.GatherBuffer(B, stride, B, dev) for _ in range(nbuf)]
     stream = torch.cuda.current_stream(dev).cuda_stream
     L.ngsSetTiming(h, 1)
     st = _native.NgsStats()
     pending = {}  # buffer index -> in-flight top-k gather (N > 1)
+    inflight = collections.deque()  # (ticket, buffer index) of queued batches (depth > 1)
     nstep = [0]
+    ktimes = []
+
+    def finished(i):  # batch in buffer i is complete: statistics, then its gather (N > 1)
+        L.ngsLastStats(h, C.byref(st))
+        ktimes.append((st.fast_kernel_ms, st.prep_kernel_ms, st.general_ms))
+        if world > 1:  # no size exchange, no host read-back: fixed-size buffers
+            pending[i] = shard.gather_to_root(gbs[i], async_op=True)  # overlaps the next batches
+
+    def wait_one():
+        t, i = inflight.popleft()
+        rc = L.ngsSearchDeviceWait(h, t)
+        if rc:
+            raise RuntimeError(f"ngsSearchDeviceWait -> {rc}")
+        finished(i)
 
     def step():
-        i = nstep[0] % len(gbs)
+        """One batch: with depth 1 a blocking ngsSearchDevice; with depth d the batch is queued
+        (ngsSearchDeviceAsync) and the oldest batch is waited for once d are in flight, so each
+        batch's tail overlaps the next batch's kernels."""
+        i = nstep[0] % nbuf
         nstep[0] += 1
         if i in pending:  # the gather that last read this buffer: ordered before it is rewritten
             pending.pop(i).complete()
         gb = gbs[i]
-        rc = L.ngsSearchDevice(h, d_raw.data_ptr(), d_off.data_ptr(), B, cfg["threshold"], cfg["limit"], stride,
-                               gb.counts.data_ptr(), gb.keys.data_ptr(), gb.scores.data_ptr(), stream)
+        args_ = (h, d_raw.data_ptr(), d_off.data_ptr(), B, cfg["threshold"], cfg["limit"], stride,
+                 gb.counts.data_ptr(), gb.keys.data_ptr(), gb.scores.data_ptr(), stream)
+        if depth == 1:
+            rc = L.ngsSearchDevice(*args_)
+            if rc:
+                raise RuntimeError(f"ngsSearchDevice -> {rc}")
+            finished(i)
+            return
+        t = C.c_uint64()
+        rc = L.ngsSearchDeviceAsync(*args_, C.byref(t))
         if rc:
-            raise RuntimeError(f"ngsSearchDevice -> {rc}")
-        L.ngsLastStats(h, C.byref(st))
-        if world > 1:  # no size exchange, no host read-back: fixed-size buffers
-            pending[i] = shard.gather_to_root(gb, async_op=True)  # overlaps the next batch
-        return st.fast_kernel_ms, st.prep_kernel_ms, st.general_ms
+            raise RuntimeError(f"ngsSearchDeviceAsync -> {rc}")
+        inflight.append((t.value, i))
+        while len(inflight) >= depth:
+            wait_one()
+
+    def drain():
+        while inflight:
+            wait_one()
+        for p in pending.values():
+            p.complete()
+        pending.clear()
 
     for _ in range(args.warmup):
         step()
-    for p in pending.values():
-        p.complete()
-    pending.clear()
+    drain()
+    ktimes.clear()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t_start = time.perf_counter()
-    ktimes = []
     for _ in range(args.steps):
-        ktimes.append(step())
-    for p in pending.values():  # every gather of the timed steps completes inside the timed region
-        p.complete()
+        step()
+    drain()  # every batch and gather of the timed steps completes inside the timed region
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -319,8 +365,12 @@ def main():
     # per-launch algorithmic bytes of the fused kernel
     qbytes = offs[-1] * (4 if corpus.wide else 1)
     alg_bytes = (4 * st.postings + 16 * st.lists + qbytes + 16 * st.survivors + 8 * st.results + 4 * B)
-    fast_ms = sum(k[0] for k in ktimes) / len(ktimes)
-    achieved = alg_bytes / (fast_ms * 1e-3) / 1e9
+    fast_ms = sum(k[0] for k in ktimes) / len(ktimes)  # per-batch tier-1 phase (HIP events)
+    step_ms = elapsed / args.steps * 1e3
+    # with batches pipelined the per-batch phases overlap: the roofline is taken over the whole
+    # step instead (every kernel of a batch, per GPU), the conservative figure
+    roof_ms = fast_ms if depth == 1 else step_ms
+    achieved = alg_bytes / (roof_ms * 1e-3) / 1e9
     total_q = B * world * args.steps
     value = total_q / elapsed / 1e6
     out = {
@@ -332,9 +382,15 @@ def main():
                    "parallelism": f"query-shard x{world}" + (" + RCCL gather of top-k" if world > 1 else "")},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(args.config),
-                     "kernel": "tier-1 phase: k_wave_lean over the batch + k_emit, beside it k_wave_lean + k_emit on the heavy list and k_wave on the full list (side streams), hand-over k_wave, k_fast (HIP events on the call stream)", "kernel_ms": round(fast_ms, 4), "alg_bytes_per_launch": alg_bytes,
+                     "kernel": ("tier-1 phase: k_wave_lean over the batch + k_emit, beside it k_wave_lean + k_emit on the "
+                                "heavy list and k_wave on the full list (side streams), hand-over k_wave, k_fast (HIP "
+                                "events on the call stream)" if depth == 1 else
+                                f"whole step: every kernel of one batch (k_prep, the tier-1 phase, k_fast), batches "
+                                f"pipelined {depth} deep (ngsSearchDeviceAsync); per-GPU step time"),
+                     "kernel_ms": round(roof_ms, 4), "alg_bytes_per_launch": alg_bytes,
                      "postings_per_query": round(st.postings / max(1, st.fast_queries), 1)},
-        "detail": {"prep_ms": round(sum(k[1] for k in ktimes) / len(ktimes), 4),
+        "detail": {"phase_ms": round(fast_ms, 4), "depth": depth,
+                   "prep_ms": round(sum(k[1] for k in ktimes) / len(ktimes), 4),
                    "general_ms": round(sum(k[2] for k in ktimes) / len(ktimes), 4),
                    "general_queries": int(st.general_queries), "results_per_query": round(st.results / B, 2),
                    "survivors_per_query": round(st.survivors / B, 2), "index_build_s": round(index_s, 1),
@@ -350,6 +406,8 @@ def main():
                                            "PCIe both ways, whole batch; score(): one query per call")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(corpus, cfg, raw, offs)
+        if args.config in REFERENCE_DLL:  # the reference itself, measured where it compiles
+            out["cpu_baseline"]["reference_dll"] = REFERENCE_DLL[args.config]
     else:
         out["cpu_baseline"] = None
     if rank == 0:

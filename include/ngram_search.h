@@ -158,6 +158,19 @@ NGS_API int ngsSearchDevice(uint32_t handle, const uint8_t* dQueryBytes, const u
                             uint32_t nQueries, float threshold, uint32_t limit, uint32_t outStride,
                             uint32_t* dCounts, uint32_t* dKeys, float* dScores, void* stream);
 
+/* Asynchronous ngsSearchDevice: the call is ordered after the work already queued on `stream`,
+ * runs on streams of its own and returns once it is queued, with a ticket. The results are
+ * complete when ngsSearchDeviceWait(handle, ticket) returns 0 (it waits, runs the library-wide
+ * path for the rare queries that need it and records the statistics); every ticket must be
+ * waited for once, and the output buffers must not be read or reused before. Calls in flight
+ * together overlap on the GPU (a batch's tail beside the next batch's counting). Return codes
+ * as ngsSearchDevice; Wait answers -3 for an unknown ticket. dispose() waits for calls in flight. */
+NGS_API int ngsSearchDeviceAsync(uint32_t handle, const uint8_t* dQueryBytes, const uint64_t* dQueryOffsets,
+                                 uint32_t nQueries, float threshold, uint32_t limit, uint32_t outStride,
+                                 uint32_t* dCounts, uint32_t* dKeys, float* dScores, void* stream,
+                                 uint64_t* ticket);
+NGS_API int ngsSearchDeviceWait(uint32_t handle, uint64_t ticket);
+
 /* Per-call statistics of the last search on `handle` (enable timing first). */
 typedef struct {
     uint64_t queries;          /* queries in the call */

@@ -16,7 +16,13 @@
 //   V <hex>                                    setValidChar(handle, bytes)
 //   Q <hex|=> <thr-bits-hex> <limit>           score(handle, q, ..., thr, limit)
 //   D                                          dispose
-// Answers: {"corpus":..,"size":..,"libSize":..} after I; one {"q":..} line per Q.
+//   S <rows> <seed> <minLen> <span> <rowSize> <hasWeights 0|1> <libngs_synth.so>
+//                                              generate the synthetic corpus of SURVEY.md §8(d)
+//                                              with the bench's own generator (csrc/synth.c,
+//                                              dlopen'ed) and call indexN on it: corpora of
+//                                              millions of rows without a request file of
+//                                              millions of lines
+// Answers: {"corpus":..,"size":..,"libSize":..} after I / S; one {"q":..} line per Q.
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -31,6 +37,8 @@ typedef void (*release_t)(uint32_t, char**, float*);
 typedef void (*dispose_t)(uint32_t);
 typedef uint64_t (*size_t_fn)(uint32_t);
 typedef void (*setvalid_t)(uint32_t, char*, int);
+typedef int (*synth_corpus_t)(uint64_t, uint64_t, uint32_t, uint32_t, uint32_t, char**, char***, float**, uint64_t*);
+typedef void (*synth_free_t)(void*);
 
 static std::string unhex(const char* h) {
     std::string s;
@@ -110,6 +118,29 @@ int main(int argc, char** argv) {
                             hasW ? weights.data() : nullptr);
             printf("{\"corpus\": %d, \"handle\": %u, \"size\": %llu, \"libSize\": %llu}\n", corpus, handle,
                    (unsigned long long)getSize(handle), (unsigned long long)getLibSize(handle));
+        } else if (tag == 'S') {
+            unsigned long long rows, seed;
+            unsigned minLen, span, rs, hw;
+            char path[4096];
+            sscanf(rest, "%llu %llu %u %u %u %u %4095s", &rows, &seed, &minLen, &span, &rs, &hw, path);
+            void* sl = dlopen(path, RTLD_NOW | RTLD_LOCAL);
+            if (!sl) { fprintf(stderr, "dlopen: %s\n", dlerror()); return 2; }
+            auto gen = (synth_corpus_t)dlsym(sl, "ngs_synth_corpus");
+            auto sfree = (synth_free_t)dlsym(sl, "ngs_synth_free");
+            if (!gen || !sfree) { fprintf(stderr, "missing synth export\n"); return 2; }
+            char* blob = nullptr;
+            char** words = nullptr;
+            float* w = nullptr;
+            uint64_t st = 0;
+            if (gen(rows, seed, minLen, span, rs, &blob, &words, &w, &st)) { fprintf(stderr, "synth failed\n"); return 2; }
+            ++corpus;
+            handle = indexN(words, rows * rs, (uint16_t)rs, hw ? w : nullptr);
+            printf("{\"corpus\": %d, \"handle\": %u, \"size\": %llu, \"libSize\": %llu}\n", corpus, handle,
+                   (unsigned long long)getSize(handle), (unsigned long long)getLibSize(handle));
+            fflush(stdout);
+            sfree(blob);  // the reference copied the strings (hpp:120-172)
+            sfree(words);
+            sfree(w);
         } else if (tag == 'V') {
             std::string v = unhex(rest);
             setValidChar(handle, (char*)v.data(), (int)v.size());

@@ -129,6 +129,12 @@ def lib():
     L.ngsSearchDevice.restype = C.c_int
     L.ngsSearchDevice.argtypes = [u32, C.c_void_p, C.c_void_p, u32, f32, u32, u32, C.c_void_p, C.c_void_p,
                                   C.c_void_p, C.c_void_p]
+    if hasattr(L, "ngsSearchDeviceAsync"):  # (experiment builds of older sources lack it)
+        L.ngsSearchDeviceAsync.restype = C.c_int
+        L.ngsSearchDeviceAsync.argtypes = [u32, C.c_void_p, C.c_void_p, u32, f32, u32, u32, C.c_void_p, C.c_void_p,
+                                           C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64)]
+        L.ngsSearchDeviceWait.restype = C.c_int
+        L.ngsSearchDeviceWait.argtypes = [u32, C.c_uint64]
     L.ngsSetTiming.restype = C.c_int
     L.ngsSetTiming.argtypes = [u32, C.c_int]
     if hasattr(L, "ngsLastError"):  # (experiment builds of older sources lack it)

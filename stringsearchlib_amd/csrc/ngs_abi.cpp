@@ -98,6 +98,7 @@ struct Context {
     hipStream_t side2 = nullptr;     // tier 1b on the full list (cmin 1, short search) beside both
     hipEvent_t fork = nullptr, join = nullptr, join2 = nullptr;
     hipEvent_t prep_ev = nullptr, lists_ev = nullptr;  // k_prep done (s), heavy / full lists merged (side)
+    hipEvent_t in_ev = nullptr;   // ngsSearchDeviceAsync: the caller's stream up to the call
     hipEvent_t ev[6] = {};
     size_t qcap = 0, bcap = 0, ncap = 0, ocap = 0;
     uint32_t ecap = kEmitCap;  // survivor slots per query in d_est / d_esc (ensure_queries, emit_cap)
@@ -156,7 +157,7 @@ struct Context {
         if (h_sio) hipHostFree(h_sio);
         for (hipEvent_t e : ev)
             if (e) hipEventDestroy(e);
-        for (hipEvent_t e : {fork, join, join2, prep_ev, lists_ev})
+        for (hipEvent_t e : {fork, join, join2, prep_ev, lists_ev, in_ev})
             if (e) hipEventDestroy(e);
         if (stream) hipStreamDestroy(stream);
         if (side) hipStreamDestroy(side);
@@ -212,7 +213,8 @@ struct Replica {
             !HIP_CHECK(hipEventCreateWithFlags(&c->join, hipEventDisableTiming)) ||
             !HIP_CHECK(hipEventCreateWithFlags(&c->join2, hipEventDisableTiming)) ||
             !HIP_CHECK(hipEventCreateWithFlags(&c->prep_ev, hipEventDisableTiming)) ||
-            !HIP_CHECK(hipEventCreateWithFlags(&c->lists_ev, hipEventDisableTiming)))
+            !HIP_CHECK(hipEventCreateWithFlags(&c->lists_ev, hipEventDisableTiming)) ||
+            !HIP_CHECK(hipEventCreateWithFlags(&c->in_ev, hipEventDisableTiming)))
             return nullptr;
         for (hipEvent_t& e : c->ev)
             if (!HIP_CHECK(hipEventCreate(&e))) return nullptr;
@@ -248,7 +250,30 @@ struct Library {
     bool tk_monotone = false;
     float w_max = 0.0f;
 
-    ~Library() { reps.clear(); }
+    // ngsSearchDeviceAsync calls in flight: their context stays out of the pool until
+    // ngsSearchDeviceWait (the general path and the statistics need the host afterwards)
+    struct Pending {
+        Replica* R = nullptr;
+        std::unique_ptr<Context> c;
+        SearchParams P{};
+        const uint8_t* dq = nullptr;
+        const uint64_t* doff = nullptr;
+        uint32_t B = 0, Lm = 0, stride = 0;
+        float thr = 0;
+        uint32_t *dn = nullptr, *dk = nullptr;
+        float* ds = nullptr;
+        int rc = 0;  // queueing already failed
+    };
+    std::mutex pend_mu;
+    std::unordered_map<uint64_t, Pending> pending;
+    uint64_t next_ticket = 1;
+
+    ~Library() {
+        for (auto& kv : pending)  // dispose: nothing may still run on the buffers freed below
+            if (kv.second.c) hipStreamSynchronize(kv.second.c->stream);
+        pending.clear();
+        reps.clear();
+    }
     // the replica on `dev`, or null
     Replica* replica_at(int dev) {
         for (auto& r : reps)
@@ -1196,6 +1221,97 @@ NGS_API int ngsSearchDevice(uint32_t handle, const uint8_t* dQueryBytes, const u
         if (rc == kRetryQcap) rc = -5;
     }
     R.give_back(std::move(c));
+    return rc;
+}
+
+// Asynchronous form (bench.py's pipeline; a server's batches): queue the search on a pooled
+// context's own streams, ordered after the work already queued on `stream`, and return. Two
+// calls in flight overlap on the GPU: one batch's tail (the last tier-1a waves, k_emit, tier 1b)
+// runs beside the next batch's counting.
+NGS_API int ngsSearchDeviceAsync(uint32_t handle, const uint8_t* dQueryBytes, const uint64_t* dQueryOffsets,
+                                 uint32_t nQueries, float threshold, uint32_t limit, uint32_t outStride,
+                                 uint32_t* dCounts, uint32_t* dKeys, float* dScores, void* stream, uint64_t* ticket) {
+    std::shared_lock<std::shared_mutex> lk(g_lock);
+    Library* L = find_lib(handle);
+    if (!L) return -1;
+    if (!L->host.indexed) return -2;
+    const uint32_t Lm = effective_limit(*L, limit);
+    if (!ticket || !dQueryOffsets || !dCounts || (nQueries && Lm && (!dKeys || !dScores || outStride < Lm))) return -3;
+    int cur = L->device;
+    if (!HIP_CHECK(hipGetDevice(&cur))) return -4;
+    Replica* Rp = L->replica_at(cur);
+    if (!Rp) return -3;
+    hipStream_t s = (hipStream_t)stream;
+    Library::Pending pd;
+    pd.R = Rp;
+    pd.dq = dQueryBytes;
+    pd.doff = dQueryOffsets;
+    pd.B = nQueries;
+    pd.Lm = Lm;
+    pd.stride = outStride;
+    pd.thr = threshold;
+    pd.dn = dCounts;
+    pd.dk = dKeys;
+    pd.ds = dScores;
+    if (Lm == 0 || nQueries == 0) {
+        if (!HIP_CHECK(hipMemsetAsync(dCounts, 0, sizeof(uint32_t) * nQueries, s))) return -4;
+    } else {
+        pd.c = Rp->acquire();
+        if (!pd.c) return -4;
+        Context& c = *pd.c;
+        uint64_t qbytes = 0;
+        if (!c.qcap && !(HIP_CHECK(hipMemcpyAsync(&qbytes, dQueryOffsets + nQueries, sizeof(uint64_t),
+                                                 hipMemcpyDeviceToHost, s)) &&
+                         HIP_CHECK(hipStreamSynchronize(s)))) {
+            Rp->give_back(std::move(pd.c));
+            return -4;
+        }
+        if (!HIP_CHECK(hipEventRecord(c.in_ev, s)) || !HIP_CHECK(hipStreamWaitEvent(c.stream, c.in_ev, 0))) {
+            Rp->give_back(std::move(pd.c));
+            return -4;
+        }
+        pd.rc = queue_search(*L, *Rp, c, dQueryBytes, dQueryOffsets, nQueries, qbytes, threshold, Lm, outStride,
+                             dCounts, dKeys, dScores, c.stream, pd.P, false);
+    }
+    std::lock_guard<std::mutex> g(L->pend_mu);
+    *ticket = L->next_ticket++;
+    L->pending.emplace(*ticket, std::move(pd));
+    return 0;
+}
+
+// Completes an ngsSearchDeviceAsync call: waits for its kernels, runs the general path for the
+// queries that need it, records the statistics (ngsLastStats). The results are then in place.
+// Same return codes as ngsSearchDevice; -3 for an unknown ticket.
+NGS_API int ngsSearchDeviceWait(uint32_t handle, uint64_t ticket) {
+    std::shared_lock<std::shared_mutex> lk(g_lock);
+    Library* L = find_lib(handle);
+    if (!L) return -1;
+    Library::Pending pd;
+    {
+        std::lock_guard<std::mutex> g(L->pend_mu);
+        auto it = L->pending.find(ticket);
+        if (it == L->pending.end()) return -3;
+        pd = std::move(it->second);
+        L->pending.erase(it);
+    }
+    if (!pd.c) return 0;  // nothing was queued (limit 0 or no queries): the counts were cleared
+    Replica& R = *pd.R;
+    Context& c = *pd.c;
+    if (!HIP_CHECK(hipSetDevice(R.device))) {
+        R.give_back(std::move(pd.c));
+        return -4;
+    }
+    int rc = pd.rc ? pd.rc : finish_search(*L, R, c, pd.B, pd.P, pd.doff, pd.dn, pd.dk, pd.ds, c.stream);
+    if (rc == kRetryQcap) {  // the batch outgrew the context's query buffer: rerun with its size
+        uint64_t qbytes = 0;
+        rc = HIP_CHECK(hipMemcpyAsync(&qbytes, pd.doff + pd.B, sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream)) &&
+                     HIP_CHECK(hipStreamSynchronize(c.stream))
+                 ? device_search(*L, R, c, pd.dq, pd.doff, pd.B, qbytes, pd.thr, pd.Lm, pd.stride, pd.dn, pd.dk,
+                                 pd.ds, c.stream)
+                 : -4;
+        if (rc == kRetryQcap) rc = -5;
+    }
+    R.give_back(std::move(pd.c));
     return rc;
 }
 

@@ -226,6 +226,23 @@ class StringIndex:
             raise RuntimeError(f"ngsSearchDevice failed: {rc}")
 
 
+    def search_device_async(self, d_bytes: int, d_offsets: int, n: int, threshold: float, limit: int,
+                            out_stride: int, d_counts: int, d_keys: int, d_scores: int, stream: int = 0) -> int:
+        """ngsSearchDeviceAsync: queues the search and returns its ticket (wait_device(ticket))."""
+        t = C.c_uint64()
+        rc = _native.lib().ngsSearchDeviceAsync(self.handle, d_bytes, d_offsets, n, threshold, limit, out_stride,
+                                                d_counts, d_keys, d_scores, stream or None, C.byref(t))
+        if rc:
+            raise RuntimeError(f"ngsSearchDeviceAsync failed: {rc}")
+        return t.value
+
+    def wait_device(self, ticket: int) -> None:
+        """ngsSearchDeviceWait: the results of that call are complete on return."""
+        rc = _native.lib().ngsSearchDeviceWait(self.handle, ticket)
+        if rc:
+            raise RuntimeError(f"ngsSearchDeviceWait failed: {rc}")
+
+
 # ---- wide strings (indexW extension) ---------------------------------------------------
 _U32P = C.POINTER(C.c_uint32)
 

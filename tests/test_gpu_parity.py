@@ -168,6 +168,44 @@ def test_device_api_matches_host_api():
         assert_exact(dv, h, f"device q={qs[i]!r}")
 
 
+def test_device_async_api_matches_host_api():
+    """ngsSearchDeviceAsync / ngsSearchDeviceWait: three batches in flight together (a limit-0
+    one among them), each answered like the host API; unknown and reused tickets are refused."""
+    torch = pytest.importorskip("torch")
+    words, wts, rng = ssl.synth.gen_corpus(5000, seed=22)
+    gi = ssl.StringIndex(words, 1, wts)
+    dev = torch.device("cuda:0")
+    stream = torch.cuda.current_stream().cuda_stream
+    batches = [ssl.synth.gen_queries(words, 1, n, rng) + [b"", b"*", b"AB"] for n in (300, 17, 120)]
+    limit = 40
+    calls = []
+    for qs, lim in zip(batches, (limit, 0, limit)):
+        raw = torch.tensor(list(b"".join(qs)), dtype=torch.uint8, device=dev)
+        offs = [0]
+        for q in qs:
+            offs.append(offs[-1] + len(q))
+        off = torch.tensor(offs, dtype=torch.int64, device=dev)
+        stride = limit if lim else gi.num_keys()
+        counts = torch.full((len(qs),), -1, dtype=torch.int32, device=dev)
+        keys = torch.zeros(len(qs) * stride, dtype=torch.int32, device=dev)
+        scores = torch.zeros(len(qs) * stride, dtype=torch.float32, device=dev)
+        t = gi.search_device_async(raw.data_ptr(), off.data_ptr(), len(qs), 0.3, lim, stride, counts.data_ptr(),
+                                   keys.data_ptr(), scores.data_ptr(), stream)
+        calls.append((t, qs, lim, stride, counts, keys, scores, raw, off))
+    for t, qs, lim, stride, counts, keys, scores, _, _ in reversed(calls):  # any order
+        gi.wait_device(t)
+        c, k, s = counts.cpu().tolist(), keys.cpu().tolist(), scores.cpu().tolist()
+        host = gi.score_batch(qs, 0.3, lim)
+        for i, h in enumerate(host):
+            dv = [(gi.key(k[i * stride + j]), s[i * stride + j]) for j in range(c[i])]
+            assert_exact(dv, h, f"async q={qs[i]!r} limit={lim}")
+    with pytest.raises(RuntimeError):
+        gi.wait_device(calls[0][0])  # already waited for
+    with pytest.raises(RuntimeError):
+        gi.wait_device(123456789)
+    gi.dispose()
+
+
 def test_device_api_query_buffer_grows():
     """ngsSearchDevice launches without reading the batch's byte count back once its context has a
     normalised-query buffer; a later, larger batch that does not fit is flagged by k_prep and the
