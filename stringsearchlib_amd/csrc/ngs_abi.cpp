@@ -749,124 +749,178 @@ size_t str_len(const CharT* p) {
     return n;
 }
 
+// One chunk of a host batch in flight on a context (host_search_one).
+struct HostChunk {
+    Context* c = nullptr;
+    uint32_t q0 = 0, B = 0;
+    bool small = false;
+    size_t block = 0;
+    SearchParams P{};
+    const uint8_t* d_raw = nullptr;
+    const uint64_t* d_off = nullptr;
+    uint32_t *d_n = nullptr, *d_k = nullptr;
+    float* d_s = nullptr;
+};
+
+// Queues chunk [q0, q0 + B) on context c: the queries packed into pinned staging, one H2D copy
+// (two for large chunks), the search kernels. Nothing waits.
+template <typename CharT>
+bool queue_host_chunk(Library& L, Replica& R, Context& c, const CharT* const* queries, uint32_t q0, uint32_t B,
+                      float thr, uint32_t Lm, HostChunk& h) {
+    constexpr size_t cs = sizeof(CharT);
+    const size_t stride = Lm;
+    h = HostChunk{};
+    h.c = &c;
+    h.q0 = q0;
+    h.B = B;
+    // query offsets into pinned staging
+    if (!c.h_off.grow(sizeof(uint64_t) * (B + 1))) return false;
+    uint64_t* ho = c.h_off.as<uint64_t>();
+    ho[0] = 0;
+    for (uint32_t i = 0; i < B; ++i) ho[i + 1] = ho[i] + (queries[q0 + i] ? str_len(queries[q0 + i]) * cs : 0);
+    const uint64_t qbytes = ho[B];
+    // small batches (score()'s latency path): one kernel per tier on one stream, the queries
+    // in with one copy and the statistics with the whole output block out with one copy,
+    // all through the context's latency block [statistics | results | offsets, bytes]
+    h.block = sizeof(uint32_t) * (B + 1 + 2 * (size_t)B * stride);
+    const size_t qspace = sizeof(uint64_t) * (B + 1) + qbytes;
+    h.small = B <= kSmallBatch && h.block <= kSmallBlock && qspace <= kSmallQ;
+    bool ok;
+    if (h.small) {
+        uint8_t* hq = c.h_sio + kSioStats + kSmallBlock;
+        std::memcpy(hq, ho, sizeof(uint64_t) * (B + 1));
+        for (uint32_t i = 0; i < B; ++i)
+            if (queries[q0 + i])
+                std::memcpy(hq + sizeof(uint64_t) * (B + 1) + ho[i], queries[q0 + i], ho[i + 1] - ho[i]);
+        uint8_t* dq = c.d_sio + kSioStats + kSmallBlock;
+        h.d_off = reinterpret_cast<const uint64_t*>(dq);
+        h.d_raw = dq + sizeof(uint64_t) * (B + 1);
+        h.d_n = reinterpret_cast<uint32_t*>(c.d_sio + kSioStats);
+        h.d_k = h.d_n + B + 1;
+        h.d_s = reinterpret_cast<float*>(h.d_k + (size_t)B * stride);
+        ok = HIP_CHECK(hipMemcpyAsync(dq, hq, qspace, hipMemcpyHostToDevice, c.stream));
+    } else {
+        if (!c.h_raw.grow(std::max<uint64_t>(qbytes, 1))) return false;
+        for (uint32_t i = 0; i < B; ++i)
+            if (queries[q0 + i]) std::memcpy(c.h_raw.as<uint8_t>() + ho[i], queries[q0 + i], ho[i + 1] - ho[i]);
+        ok = ensure_queries(c, B, qbytes, thr) && ensure_outputs(c, B, stride) &&
+             HIP_CHECK(hipMemcpyAsync(c.d_raw, c.h_raw.p, qbytes, hipMemcpyHostToDevice, c.stream)) &&
+             HIP_CHECK(hipMemcpyAsync(c.d_off, ho, sizeof(uint64_t) * (B + 1), hipMemcpyHostToDevice, c.stream));
+        h.d_raw = c.d_raw;
+        h.d_off = c.d_off;
+        h.d_n = c.d_n;
+        h.d_k = c.d_k;
+        h.d_s = c.d_s;
+    }
+    if (!ok) return false;
+    if (queue_search(L, R, c, h.d_raw, h.d_off, B, qbytes, thr, Lm, (uint32_t)stride, h.d_n, h.d_k, h.d_s, c.stream,
+                     h.P, h.small) != 0)
+        return false;
+    return !h.small || HIP_CHECK(hipMemcpyAsync(c.h_sio, c.d_sio, kSioStats + h.block, hipMemcpyDeviceToHost, c.stream));
+}
+
+// Completes a queued chunk: waits, runs the general path, reads back exactly the results
+// (packed on the device for large chunks) and appends them.
+bool finish_host_chunk(Library& L, Replica& R, HostChunk& h, uint32_t Lm, std::vector<uint32_t>& counts,
+                       std::vector<uint32_t>& keys, std::vector<float>& scores) {
+    Context& c = *h.c;
+    const uint32_t B = h.B, q0 = h.q0;
+    const size_t stride = Lm;
+    if (finish_search(L, R, c, B, h.P, h.d_off, h.d_n, h.d_k, h.d_s, c.stream, h.small) != 0) return false;
+    if (h.small) {
+        const uint32_t* counts3 = reinterpret_cast<const uint32_t*>(c.h_sio) + kStatSlots * 16;
+        if (counts3[0]) {  // the general path ran after the read-back: read the results again
+            if (!HIP_CHECK(hipMemcpyAsync(c.h_sio + kSioStats, c.d_sio + kSioStats, h.block, hipMemcpyDeviceToHost,
+                                          c.stream)) ||
+                !HIP_CHECK(hipStreamSynchronize(c.stream)))
+                return false;
+        }
+        const uint32_t* hn = reinterpret_cast<const uint32_t*>(c.h_sio + kSioStats);
+        const uint32_t* hk = hn + B + 1;
+        const float* hs = reinterpret_cast<const float*>(hk + (size_t)B * stride);
+        for (uint32_t i = 0; i < B; ++i) {
+            counts[q0 + i] = hn[i];
+            keys.insert(keys.end(), hk + (size_t)i * stride, hk + (size_t)i * stride + hn[i]);
+            scores.insert(scores.end(), hs + (size_t)i * stride, hs + (size_t)i * stride + hn[i]);
+        }
+        return true;
+    }
+    // large batches: pack on the device (prefix sum of the counts, one copy per query), read
+    // back the offsets, then exactly the packed records
+    if (!HIP_CHECK(hipMemsetAsync(c.d_n + B, 0, sizeof(uint32_t), c.stream)) ||
+        !HIP_CHECK(launch_pack(c.d_n, c.d_k, c.d_s, B, (uint32_t)stride, c.d_pos, c.d_pk, c.d_ps, c.d_ptemp,
+                               c.ptemp_bytes, c.stream)) ||
+        !c.h_res.grow(sizeof(uint32_t) * (B + 1)) ||
+        !HIP_CHECK(hipMemcpyAsync(c.h_res.p, c.d_pos, sizeof(uint32_t) * (B + 1), hipMemcpyDeviceToHost, c.stream)) ||
+        !HIP_CHECK(hipStreamSynchronize(c.stream)))
+        return false;
+    const uint32_t total = c.h_res.as<uint32_t>()[B];
+    for (uint32_t i = 0; i < B; ++i) counts[q0 + i] = c.h_res.as<uint32_t>()[i + 1] - c.h_res.as<uint32_t>()[i];
+    if (!c.h_res.grow(sizeof(uint32_t) * 2 * (size_t)total) ||
+        !HIP_CHECK(hipMemcpyAsync(c.h_res.p, c.d_pk, sizeof(uint32_t) * total, hipMemcpyDeviceToHost, c.stream)) ||
+        !HIP_CHECK(hipMemcpyAsync(c.h_res.as<uint32_t>() + total, c.d_ps, sizeof(float) * total, hipMemcpyDeviceToHost,
+                                  c.stream)) ||
+        !HIP_CHECK(hipStreamSynchronize(c.stream)))
+        return false;
+    // appended straight from the pinned buffer (no zero-filling resize first)
+    const uint32_t* pk = c.h_res.as<uint32_t>();
+    const float* ps = reinterpret_cast<const float*>(pk + total);
+    keys.insert(keys.end(), pk, pk + total);
+    scores.insert(scores.end(), ps, ps + total);
+    return true;
+}
+
+// A large host batch runs as about kPipeChunks chunks (of at least kPipeMinChunk queries) over
+// two contexts, one queued ahead: chunk k's packing, copies and read-back overlap chunk k + 1's
+// kernels, and the two chunks' kernels overlap each other on the GPU.
+constexpr uint32_t kPipeChunks = 4;
+constexpr uint32_t kPipeMinChunk = 8192;
+
 // Scores n queries (characters of the index's width) on one replica; fills counts and flat
 // (key, score) vectors.
 template <typename CharT>
 bool host_search_one(Library& L, Replica& R, const CharT* const* queries, uint32_t nq, float thr, uint32_t Lm,
                      std::vector<uint32_t>& counts, std::vector<uint32_t>& keys, std::vector<float>& scores) {
-    constexpr size_t cs = sizeof(CharT);
     counts.assign(nq, 0);
     keys.clear();
     scores.clear();
     if (Lm == 0 || nq == 0) return true;
     if (!HIP_CHECK(hipSetDevice(R.device))) return false;
-    std::unique_ptr<Context> c = R.acquire();
-    if (!c) return false;
     const size_t stride = Lm;
     size_t max_chunk = std::max<size_t>(1, std::min<size_t>(1 << 20, kOutBudget / (stride * 8)));
     if (Lm <= kWaveMaxLimit)  // sliced tier 1b's partial results fit the budget
         max_chunk = std::max<size_t>(1, std::min<size_t>(max_chunk, kPartBudget / (sizeof(uint64_t) * kSlices * Lm)));
-    bool ok = true;
-    for (uint32_t q0 = 0; q0 < nq && ok; q0 += (uint32_t)max_chunk) {
-        const uint32_t B = (uint32_t)std::min<size_t>(max_chunk, nq - q0);
-        // query offsets into pinned staging
-        ok = c->h_off.grow(sizeof(uint64_t) * (B + 1));
-        if (!ok) break;
-        uint64_t* ho = c->h_off.as<uint64_t>();
-        ho[0] = 0;
-        for (uint32_t i = 0; i < B; ++i) ho[i + 1] = ho[i] + (queries[q0 + i] ? str_len(queries[q0 + i]) * cs : 0);
-        const uint64_t qbytes = ho[B];
-        // small batches (score()'s latency path): one kernel per tier on one stream, the queries
-        // in with one copy and the statistics with the whole output block out with one copy,
-        // all through the context's latency block [statistics | results | offsets, bytes]
-        const size_t block = sizeof(uint32_t) * (B + 1 + 2 * (size_t)B * stride);
-        const size_t qspace = sizeof(uint64_t) * (B + 1) + qbytes;
-        const bool small = B <= kSmallBatch && block <= kSmallBlock && qspace <= kSmallQ;
-        const uint8_t* d_raw = c->d_raw;
-        const uint64_t* d_off = c->d_off;
-        uint32_t *d_n = c->d_n, *d_k = c->d_k;
-        float* d_s = c->d_s;
-        if (small) {
-            uint8_t* hq = c->h_sio + kSioStats + kSmallBlock;
-            std::memcpy(hq, ho, sizeof(uint64_t) * (B + 1));
-            for (uint32_t i = 0; i < B; ++i)
-                if (queries[q0 + i])
-                    std::memcpy(hq + sizeof(uint64_t) * (B + 1) + ho[i], queries[q0 + i], ho[i + 1] - ho[i]);
-            uint8_t* dq = c->d_sio + kSioStats + kSmallBlock;
-            d_off = reinterpret_cast<const uint64_t*>(dq);
-            d_raw = dq + sizeof(uint64_t) * (B + 1);
-            d_n = reinterpret_cast<uint32_t*>(c->d_sio + kSioStats);
-            d_k = d_n + B + 1;
-            d_s = reinterpret_cast<float*>(d_k + (size_t)B * stride);
-            ok = HIP_CHECK(hipMemcpyAsync(dq, hq, qspace, hipMemcpyHostToDevice, c->stream));
-        } else {
-            ok = c->h_raw.grow(std::max<uint64_t>(qbytes, 1));
-            if (!ok) break;
-            for (uint32_t i = 0; i < B; ++i)
-                if (queries[q0 + i]) std::memcpy(c->h_raw.as<uint8_t>() + ho[i], queries[q0 + i], ho[i + 1] - ho[i]);
-            ok = ensure_queries(*c, B, qbytes, thr) && ensure_outputs(*c, B, stride) &&
-                 HIP_CHECK(hipMemcpyAsync(c->d_raw, c->h_raw.p, qbytes, hipMemcpyHostToDevice, c->stream)) &&
-                 HIP_CHECK(hipMemcpyAsync(c->d_off, ho, sizeof(uint64_t) * (B + 1), hipMemcpyHostToDevice, c->stream));
-            d_raw = c->d_raw;
-            d_off = c->d_off;
-            d_n = c->d_n;
-            d_k = c->d_k;
-            d_s = c->d_s;
-        }
-        if (!ok) break;
-        SearchParams P;
-        ok = queue_search(L, R, *c, d_raw, d_off, B, qbytes, thr, Lm, (uint32_t)stride, d_n, d_k, d_s, c->stream, P,
-                          small) == 0;
-        if (!ok) break;
-        if (small) {
-            ok = HIP_CHECK(hipMemcpyAsync(c->h_sio, c->d_sio, kSioStats + block, hipMemcpyDeviceToHost, c->stream));
-            if (!ok) break;
-        }
-        ok = finish_search(L, R, *c, B, P, d_off, d_n, d_k, d_s, c->stream, small) == 0;
-        if (!ok) break;
-        if (small) {
-            const uint32_t* counts3 = reinterpret_cast<const uint32_t*>(c->h_sio) + kStatSlots * 16;
-            if (counts3[0]) {  // the general path ran after the read-back: read the results again
-                ok = HIP_CHECK(hipMemcpyAsync(c->h_sio + kSioStats, c->d_sio + kSioStats, block,
-                                              hipMemcpyDeviceToHost, c->stream)) &&
-                     HIP_CHECK(hipStreamSynchronize(c->stream));
-                if (!ok) break;
-            }
-            const uint32_t* hn = reinterpret_cast<const uint32_t*>(c->h_sio + kSioStats);
-            const uint32_t* hk = hn + B + 1;
-            const float* hs = reinterpret_cast<const float*>(hk + (size_t)B * stride);
-            for (uint32_t i = 0; i < B; ++i) {
-                counts[q0 + i] = hn[i];
-                keys.insert(keys.end(), hk + (size_t)i * stride, hk + (size_t)i * stride + hn[i]);
-                scores.insert(scores.end(), hs + (size_t)i * stride, hs + (size_t)i * stride + hn[i]);
-            }
-            continue;
-        }
-        // large batches: pack on the device (prefix sum of the counts, one copy per query), read
-        // back the offsets, then exactly the packed records
-        ok = HIP_CHECK(hipMemsetAsync(c->d_n + B, 0, sizeof(uint32_t), c->stream)) &&
-             HIP_CHECK(launch_pack(c->d_n, c->d_k, c->d_s, B, (uint32_t)stride, c->d_pos, c->d_pk, c->d_ps,
-                                   c->d_ptemp, c->ptemp_bytes, c->stream)) &&
-             c->h_res.grow(sizeof(uint32_t) * (B + 1)) &&
-             HIP_CHECK(hipMemcpyAsync(c->h_res.p, c->d_pos, sizeof(uint32_t) * (B + 1), hipMemcpyDeviceToHost,
-                                      c->stream)) &&
-             HIP_CHECK(hipStreamSynchronize(c->stream));
-        if (!ok) break;
-        const uint32_t total = c->h_res.as<uint32_t>()[B];
-        for (uint32_t i = 0; i < B; ++i) counts[q0 + i] = c->h_res.as<uint32_t>()[i + 1] - c->h_res.as<uint32_t>()[i];
-        ok = c->h_res.grow(sizeof(uint32_t) * 2 * (size_t)total) &&
-             HIP_CHECK(hipMemcpyAsync(c->h_res.p, c->d_pk, sizeof(uint32_t) * total, hipMemcpyDeviceToHost, c->stream)) &&
-             HIP_CHECK(hipMemcpyAsync(c->h_res.as<uint32_t>() + total, c->d_ps, sizeof(float) * total,
-                                      hipMemcpyDeviceToHost, c->stream)) &&
-             HIP_CHECK(hipStreamSynchronize(c->stream));
-        if (!ok) break;
-        // appended straight from the pinned buffer (no zero-filling resize first)
-        const uint32_t* pk = c->h_res.as<uint32_t>();
-        const float* ps = reinterpret_cast<const float*>(pk + total);
-        keys.insert(keys.end(), pk, pk + total);
-        scores.insert(scores.end(), ps, ps + total);
+    static const uint32_t pipe_chunks = [] {  // NGS_PIPE_CHUNKS=1: one chunk (no pipelining)
+        const char* e = std::getenv("NGS_PIPE_CHUNKS");
+        return e ? std::max<uint32_t>(1, (uint32_t)std::strtoul(e, nullptr, 0)) : kPipeChunks;
+    }();
+    const size_t want = std::max<size_t>(kPipeMinChunk, (nq + pipe_chunks - 1) / pipe_chunks);
+    const size_t chunk = std::min(max_chunk, want);
+    const uint32_t n_chunks = (uint32_t)((nq + chunk - 1) / chunk);
+    std::unique_ptr<Context> ctx[2];
+    ctx[0] = R.acquire();
+    if (!ctx[0]) return false;
+    if (n_chunks > 1 && !(ctx[1] = R.acquire())) {
+        R.give_back(std::move(ctx[0]));
+        return false;
     }
-    R.give_back(std::move(c));
+    HostChunk fl[2];
+    bool ok = true, pending = false;
+    for (uint32_t k = 0; k <= n_chunks && ok; ++k) {
+        // queue chunk k, then complete chunk k - 1 while k runs
+        if (k < n_chunks) {
+            const uint32_t q0 = (uint32_t)(k * chunk), B = (uint32_t)std::min<size_t>(chunk, nq - q0);
+            ok = queue_host_chunk(L, R, *ctx[k & 1], queries, q0, B, thr, Lm, fl[k & 1]);
+            if (!ok) break;
+        }
+        if (pending) ok = finish_host_chunk(L, R, fl[(k - 1) & 1], Lm, counts, keys, scores);
+        pending = k < n_chunks;
+    }
+    if (!ok)  // a chunk may still be queued: let it drain before its context is reused
+        for (auto& c : ctx)
+            if (c) hipStreamSynchronize(c->stream);
+    for (auto& c : ctx)
+        if (c) R.give_back(std::move(c));
     return ok;
 }
 

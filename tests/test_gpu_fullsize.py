@@ -14,6 +14,8 @@ import pytest
 from oracle_py import lib as olib
 from tiecheck import bits
 
+import scale_golden as sg
+
 import stringsearchlib_amd as ssl
 from stringsearchlib_amd import _native
 
@@ -139,9 +141,30 @@ def test_c3_full_sampled_exact_and_properties():
         assert_same(again[i], got[i], f"C3 rerun q#{i}")
     check_small_batches(h, qs, got, 0.3, 100, list(range(B, B + 8)) + list(range(88)), "C3")
     oh = olib().ngo_build(wp, rows, 1, wt)
-    sample = sorted(rng.sample(range(len(qs)), 768))
+    sample = sorted(rng.sample(range(len(qs)), 4096))
     ref = oracle_batch(oh, [qs[i] for i in sample], 0.3, 100)
     for i, r in zip(sample, ref):
         assert_same(got[i], r, f"C3 q#{i} {qs[i]!r}")
     olib().ngo_free(oh)
     _native.lib().dispose(h)
+
+
+@pytest.mark.parametrize("name", sg.available())
+def test_reference_answers_at_scale(name):
+    """The HIP path against the REFERENCE DLL's own answers at C2 / C3 scale (tie-aware;
+    tests/golden/scale, written by tests/golden/make_golden_scale.py)."""
+    fx = sg.load(name)
+    spec = fx["spec"]
+    S, blob, wp, wt, st = sg.corpus(spec)
+    h = _native.lib().indexN(wp, spec["rows"] * spec["row_size"], spec["row_size"], wt if spec["weights"] else None)
+    assert h
+    L = _native.lib()
+    assert L.getSize(h) == fx["size"] and L.getLibSize(h) == fx["libSize"]
+    qs = sg.queries(fx)
+    sg.check_answers(fx, gpu_batch(h, qs, spec["thr"], spec["limit"]), "GPU batch")
+    # the latency path (batches of <= 16, 32 term-id slices per query) on the same queries
+    for i0 in range(0, 64, 16):
+        sg.check_answers({"name": fx["name"], "cases": fx["cases"][i0:i0 + 16]},
+                         gpu_batch(h, qs[i0:i0 + 16], spec["thr"], spec["limit"]), "GPU small batch")
+    L.dispose(h)
+    sg.free(S, blob, wp, wt)
