@@ -224,6 +224,105 @@ def c1_latency(device: int, n: int = 2000):
     return {"c1_score_us_mean": round(sum(lat) / len(lat) * 1e6, 1), "c1_score_us_p50": round(lat[len(lat) // 2] * 1e6, 1)}
 
 
+class StepLoop:
+    """The timed loop of one rank: each step scores the rank's batch into a gather buffer
+    (shard.GatherBuffer); with depth 1 through a blocking ngsSearchDevice, with depth d through
+    ngsSearchDeviceAsync with up to d batches in flight (the oldest waited for with
+    ngsSearchDeviceWait), so each batch's tail overlaps the next batch's kernels. With N > 1 ranks
+    a finished batch's buffer is gathered to rank 0 (one RCCL collective, in flight beside the
+    next batches); a buffer is rewritten only after the batch that last wrote it was waited for
+    and its gather ordered before the rewrite (PendingGather.complete). `run` brackets the timed
+    steps with a barrier and a device synchronisation on both sides and returns the max over
+    ranks of the elapsed time. tests/test_bench_loop.py drives it on CPU (gloo, world size 2)
+    with the oracle standing in for the library."""
+
+    def __init__(self, L, h, d_raw, d_off, B, threshold, limit, stride, depth, world, dev, stream):
+        self.L, self.h, self.d_raw, self.d_off, self.B = L, h, d_raw, d_off, B
+        self.threshold, self.limit, self.stride = threshold, limit, stride
+        self.depth, self.world, self.dev, self.stream = max(1, depth), world, dev, stream
+        self.nbuf = self.depth + 1 if self.depth > 1 else (2 if world > 1 else 1)
+        self.gbs = [shard.GatherBuffer(B, stride, B, dev) for _ in range(self.nbuf)]
+        self.st = _native.NgsStats()
+        self.pending = {}  # buffer index -> in-flight top-k gather (N > 1)
+        self.inflight = collections.deque()  # (ticket, buffer index) of queued batches (depth > 1)
+        self.nstep = 0
+        self.ktimes = []
+        self.gathered = []  # rank 0, N > 1: the PendingGathers of the timed steps (tests decode them)
+        self.keep_gathers = False
+
+    def _finished(self, i):  # batch in buffer i is complete: statistics, then its gather (N > 1)
+        self.L.ngsLastStats(self.h, C.byref(self.st))
+        self.ktimes.append((self.st.fast_kernel_ms, self.st.prep_kernel_ms, self.st.general_ms))
+        if self.world > 1:  # no size exchange, no host read-back: fixed-size buffers
+            pg = shard.gather_to_root(self.gbs[i], async_op=True)  # overlaps the next batches
+            self.pending[i] = pg
+            if self.keep_gathers:
+                self.gathered.append(pg)
+
+    def _wait_one(self):
+        t, i = self.inflight.popleft()
+        rc = self.L.ngsSearchDeviceWait(self.h, t)
+        if rc:
+            raise RuntimeError(f"ngsSearchDeviceWait -> {rc}")
+        self._finished(i)
+
+    def step(self):
+        i = self.nstep % self.nbuf
+        self.nstep += 1
+        if i in self.pending:  # the gather that last read this buffer: ordered before it is rewritten
+            self.pending.pop(i).complete()
+        gb = self.gbs[i]
+        args_ = (self.h, self.d_raw.data_ptr(), self.d_off.data_ptr(), self.B, self.threshold, self.limit,
+                 self.stride, gb.counts.data_ptr(), gb.keys.data_ptr(), gb.scores.data_ptr(), self.stream)
+        if self.depth == 1:
+            rc = self.L.ngsSearchDevice(*args_)
+            if rc:
+                raise RuntimeError(f"ngsSearchDevice -> {rc}")
+            self._finished(i)
+            return
+        t = C.c_uint64()
+        rc = self.L.ngsSearchDeviceAsync(*args_, C.byref(t))
+        if rc:
+            raise RuntimeError(f"ngsSearchDeviceAsync -> {rc}")
+        self.inflight.append((t.value, i))
+        while len(self.inflight) >= self.depth:
+            self._wait_one()
+
+    def drain(self):
+        while self.inflight:
+            self._wait_one()
+        for p in self.pending.values():
+            p.complete()
+        self.pending.clear()
+
+    def _sync(self):
+        if self.dev.type == "cuda":
+            torch.cuda.synchronize(self.dev)
+
+    def run(self, steps, warmup):
+        for _ in range(warmup):
+            self.step()
+        self.drain()
+        self.ktimes.clear()
+        self.gathered.clear()
+        if self.world > 1:
+            dist.barrier()
+        self._sync()
+        t_start = time.perf_counter()
+        for _ in range(steps):
+            self.step()
+        self.drain()  # every batch and gather of the timed steps completes inside the timed region
+        self._sync()
+        if self.world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t_start
+        if self.world > 1:
+            e = torch.tensor([elapsed], dtype=torch.float64, device=self.dev)
+            dist.all_reduce(e, op=dist.ReduceOp.MAX)
+            elapsed = float(e.item())
+        return elapsed, self.ktimes
+
+
 def pmc_traffic(cfg_name: str):
     """HBM bytes per fused-kernel launch from a committed rocprofv3 PMC pass, if any."""
     p = os.path.join(ROOT, "profiles", f"pmc_{cfg_name}.json")
@@ -284,83 +383,11 @@ def main():
         d_off = torch.tensor(offs, dtype=torch.int64, device=dev)
     stride = min(cfg["limit"], n_keys)
     depth = max(1, args.depth)
-    # results go straight into the fused gather buffers (shard.GatherBuffer), used in turn: a
-    # buffer is rewritten only after the batch that last wrote it was waited for and its gather
-    # (N > 1) ordered before the rewrite
-    nbuf = depth + 1 if depth > 1 else (2 if world > 1 else 1)
-    gbs = [shard.GatherBuffer(B, stride, B, dev) for _ in range(nbuf)]
-    stream = torch.cuda.current_stream(dev).cuda_stream
     L.ngsSetTiming(h, 1)
-    st = _native.NgsStats()
-    pending = {}  # buffer index -> in-flight top-k gather (N > 1)
-    inflight = collections.deque()  # (ticket, buffer index) of queued batches (depth > 1)
-    nstep = [0]
-    ktimes = []
-
-    def finished(i):  # batch in buffer i is complete: statistics, then its gather (N > 1)
-        L.ngsLastStats(h, C.byref(st))
-        ktimes.append((st.fast_kernel_ms, st.prep_kernel_ms, st.general_ms))
-        if world > 1:  # no size exchange, no host read-back: fixed-size buffers
-            pending[i] = shard.gather_to_root(gbs[i], async_op=True)  # overlaps the next batches
-
-    def wait_one():
-        t, i = inflight.popleft()
-        rc = L.ngsSearchDeviceWait(h, t)
-        if rc:
-            raise RuntimeError(f"ngsSearchDeviceWait -> {rc}")
-        finished(i)
-
-    def step():
-        """One batch: with depth 1 a blocking ngsSearchDevice; with depth d the batch is queued
-        (ngsSearchDeviceAsync) and the oldest batch is waited for once d are in flight, so each
-        batch's tail overlaps the next batch's kernels."""
-        i = nstep[0] % nbuf
-        nstep[0] += 1
-        if i in pending:  # the gather that last read this buffer: ordered before it is rewritten
-            pending.pop(i).complete()
-        gb = gbs[i]
-        args_ = (h, d_raw.data_ptr(), d_off.data_ptr(), B, cfg["threshold"], cfg["limit"], stride,
-                 gb.counts.data_ptr(), gb.keys.data_ptr(), gb.scores.data_ptr(), stream)
-        if depth == 1:
-            rc = L.ngsSearchDevice(*args_)
-            if rc:
-                raise RuntimeError(f"ngsSearchDevice -> {rc}")
-            finished(i)
-            return
-        t = C.c_uint64()
-        rc = L.ngsSearchDeviceAsync(*args_, C.byref(t))
-        if rc:
-            raise RuntimeError(f"ngsSearchDeviceAsync -> {rc}")
-        inflight.append((t.value, i))
-        while len(inflight) >= depth:
-            wait_one()
-
-    def drain():
-        while inflight:
-            wait_one()
-        for p in pending.values():
-            p.complete()
-        pending.clear()
-
-    for _ in range(args.warmup):
-        step()
-    drain()
-    ktimes.clear()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t_start = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    drain()  # every batch and gather of the timed steps completes inside the timed region
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t_start
-    if world > 1:
-        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(e, op=dist.ReduceOp.MAX)
-        elapsed = float(e.item())
+    loop = StepLoop(L, h, d_raw, d_off, B, cfg["threshold"], cfg["limit"], stride, depth, world, dev,
+                    torch.cuda.current_stream(dev).cuda_stream)
+    elapsed, ktimes = loop.run(args.steps, args.warmup)
+    st = loop.st
 
     # per-launch algorithmic bytes of the fused kernel (DESIGN.md §Roofline)
     qbytes = offs[-1] * (4 if corpus.wide else 1)

@@ -203,6 +203,9 @@ NGS_API int ngsLastStats(uint32_t handle, ngs_stats* out);
  * (1 keys unique, 2 one pair per term, 4 term ids in key-rank order). Returns min(n, 17),
  * -1 (bad handle), -4 (HIP error). */
 NGS_API int ngsIndexDigest(uint32_t handle, uint64_t* out, int n);
+/* The same digests of replica `replica` (0 .. ngsReplicaCount - 1): every replica of an index
+ * placed on several devices holds the same arrays. -1 for a bad handle or replica. */
+NGS_API int ngsReplicaDigest(uint32_t handle, int replica, uint64_t* out, int n);
 
 /* Index files (an extension; the reference rebuilds on every indexN): ngsSaveIndex writes the
  * interned library of `handle` (terms, term -> (key, weight) pairs, keys, wildcard weights,

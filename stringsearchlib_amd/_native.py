@@ -144,6 +144,9 @@ def lib():
     L.ngsLastStats.argtypes = [u32, C.POINTER(NgsStats)]
     L.ngsIndexDigest.restype = C.c_int
     L.ngsIndexDigest.argtypes = [u32, C.POINTER(u64), C.c_int]
+    if hasattr(L, "ngsReplicaDigest"):
+        L.ngsReplicaDigest.restype = C.c_int
+        L.ngsReplicaDigest.argtypes = [u32, C.c_int, C.POINTER(u64), C.c_int]
     L.ngsVersion.restype = cp
     L.ngsVersion.argtypes = []
     L.ngsSaveIndex.restype = C.c_int

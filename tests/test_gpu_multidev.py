@@ -6,14 +6,23 @@ host thread and stream per replica) and join them in query order. Queries are in
 (nGramSearch.hpp:372-470 scores each one on its own), so the joined answer must equal the one-device
 answer exactly. A one-GPU box exercises the same code with several replicas on device 0.
 """
+import ctypes as C
+
 import pytest
 
 from oracle_py import OracleIndex
 from test_gpu_parity import assert_exact
 
 import stringsearchlib_amd as ssl
+from stringsearchlib_amd import _native
 
 pytestmark = pytest.mark.gpu
+
+
+def _digest(handle, replica):
+    out = (C.c_uint64 * 17)()
+    assert _native.lib().ngsReplicaDigest(handle, replica, out, 17) == 17
+    return list(out)
 
 
 def _corpus(n, seed):
@@ -30,6 +39,12 @@ def test_split_equals_single(replicas):
     multi = ssl.StringIndex(words, 1, weights, devices=[0] * replicas)
     assert one.replicas() == 1 and multi.replicas() == replicas
     assert multi.size() == one.size() and multi.lib_size() == one.lib_size()
+    # the replicas after the first are placed concurrently (one host thread each): every one of
+    # them holds exactly the arrays of the one-device index
+    want = _digest(one.handle, 0)
+    for r in range(replicas):
+        assert _digest(multi.handle, r) == want, f"replica {r} differs"
+    assert _native.lib().ngsReplicaDigest(multi.handle, replicas, (C.c_uint64 * 17)(), 17) == -1
     for thr, limit in [(0.3, 100), (0.0, 7), (0.5, 0)]:
         a = one.score_batch(batch, thr, limit)
         b = multi.score_batch(batch, thr, limit)
