@@ -5,6 +5,7 @@
 // (:22), smallest-free-handle allocation (:41-46), shared locks for searches (:63,84,100,122,
 // 135,147) and exclusive locks for indexN/dispose (:39,112).
 #include <hip/hip_runtime.h>
+#include <sys/mman.h>
 
 #include <algorithm>
 #include <atomic>
@@ -54,6 +55,46 @@ bool hip_ok(hipError_t e, const char* what) {
     return false;
 }
 #define HIP_CHECK(expr) hip_ok((expr), #expr)
+
+// NGS_HOST_TIMING=1 (diagnostics): the host batch path prints its phases (microseconds since
+// the previous mark) to stderr
+struct HostTimer {
+    bool on;
+    std::chrono::steady_clock::time_point t;
+    HostTimer() : on(std::getenv("NGS_HOST_TIMING") != nullptr), t(std::chrono::steady_clock::now()) {}
+    void mark(const char* what) {
+        if (!on) return;
+        const auto n = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[ngs host] %-28s %9.1f us\n", what, std::chrono::duration<double, std::micro>(n - t).count());
+        t = n;
+    }
+};
+
+// Largest host batch (queries x limit entries) whose result arrays are allocated at capacity and
+// filled as chunks finish (batch_query); larger ones collect the records first
+constexpr uint64_t kDirectMax = uint64_t(1) << 25;
+
+// Large result arrays fault in a 4 KB page at a time on first write (1.3M records at C3: ~2,600
+// faults per array); transparent huge pages, where the kernel offers them, take 2 MB at a time
+inline void advise_huge(void* p, size_t bytes) {
+    constexpr uintptr_t kHuge = uintptr_t(2) << 20;
+    const uintptr_t a = (reinterpret_cast<uintptr_t>(p) + kHuge - 1) & ~(kHuge - 1);
+    const uintptr_t e = (reinterpret_cast<uintptr_t>(p) + bytes) & ~(kHuge - 1);
+    if (e > a) (void)madvise(reinterpret_cast<void*>(a), e - a, MADV_HUGEPAGE);
+}
+
+// body(lo, hi) over [0, n) on up to 8 host threads (one below `serial_below` items)
+template <class F>
+void parallel_ranges(size_t n, size_t serial_below, F&& body) {
+    const size_t nt = n < serial_below ? 1 : std::min<size_t>(8, std::max(1u, std::thread::hardware_concurrency()));
+    if (nt <= 1) {
+        body(size_t(0), n);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (size_t t = 0; t < nt; ++t) th.emplace_back(body, n * t / nt, n * (t + 1) / nt);
+    for (auto& x : th) x.join();
+}
 
 template <class T>
 bool dev_alloc(T** p, size_t n) {
@@ -161,7 +202,7 @@ struct Context {
             if (e) hipEventDestroy(e);
         if (stream) hipStreamDestroy(stream);
         if (side) hipStreamDestroy(side);
-        if (side2) hipStreamDestroy(side2);
+        if (side2 && side2 != side) hipStreamDestroy(side2);
     }
 };
 
@@ -178,6 +219,21 @@ hipError_t make_side_stream(hipStream_t* s) {
     hipError_t e = hipDeviceGetStreamPriorityRange(&lo, &hi);
     if (e != hipSuccess) return e;
     return hipStreamCreateWithPriority(s, hipStreamNonBlocking, hi);
+}
+
+// The full list's tier 1b (cmin 1, short search) runs on the side stream after the heavy list's
+// chain (NGS_SIDE2=1: on a third stream of its own). Two contexts in flight (ngsSearchDeviceAsync,
+// the pipelined host path) then use four streams, one per hardware queue (HIP's default of
+// four): with three per context, one context's main stream shared a queue with the other's
+// side work and waited behind it (a pipelined scoreBatch measured 2x slower that way).
+hipError_t make_second_side(hipStream_t side, hipStream_t* s) {
+    static const bool own = [] {
+        const char* e = std::getenv("NGS_SIDE2");
+        return e && std::atoi(e) != 0;
+    }();
+    if (own) return make_side_stream(s);
+    *s = side;
+    return hipSuccess;
 }
 
 // One copy of the index in one device's HBM, with its pool of per-call contexts. An index built
@@ -208,7 +264,7 @@ struct Replica {
         auto c = std::make_unique<Context>();
         c->device = device;
         if (!HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) ||
-            !HIP_CHECK(make_side_stream(&c->side)) || !HIP_CHECK(make_side_stream(&c->side2)) ||
+            !HIP_CHECK(make_side_stream(&c->side)) || !HIP_CHECK(make_second_side(c->side, &c->side2)) ||
             !HIP_CHECK(hipEventCreateWithFlags(&c->fork, hipEventDisableTiming)) ||
             !HIP_CHECK(hipEventCreateWithFlags(&c->join, hipEventDisableTiming)) ||
             !HIP_CHECK(hipEventCreateWithFlags(&c->join2, hipEventDisableTiming)) ||
@@ -792,11 +848,15 @@ bool queue_host_chunk(Library& L, Replica& R, Context& c, const CharT* const* qu
     h.c = &c;
     h.q0 = q0;
     h.B = B;
-    // query offsets into pinned staging
+    HostTimer ht;
+    // query offsets into pinned staging: lengths on up to 8 threads, one prefix pass
     if (!c.h_off.grow(sizeof(uint64_t) * (B + 1))) return false;
     uint64_t* ho = c.h_off.as<uint64_t>();
     ho[0] = 0;
-    for (uint32_t i = 0; i < B; ++i) ho[i + 1] = ho[i] + (queries[q0 + i] ? str_len(queries[q0 + i]) * cs : 0);
+    parallel_ranges(B, 16384, [&](size_t a, size_t e) {
+        for (size_t i = a; i < e; ++i) ho[i + 1] = queries[q0 + i] ? str_len(queries[q0 + i]) * cs : 0;
+    });
+    for (uint32_t i = 0; i < B; ++i) ho[i + 1] += ho[i];
     const uint64_t qbytes = ho[B];
     // small batches (score()'s latency path): one kernel per tier on one stream, the queries
     // in with one copy and the statistics with the whole output block out with one copy,
@@ -820,8 +880,12 @@ bool queue_host_chunk(Library& L, Replica& R, Context& c, const CharT* const* qu
         ok = HIP_CHECK(hipMemcpyAsync(dq, hq, qspace, hipMemcpyHostToDevice, c.stream));
     } else {
         if (!c.h_raw.grow(std::max<uint64_t>(qbytes, 1))) return false;
-        for (uint32_t i = 0; i < B; ++i)
-            if (queries[q0 + i]) std::memcpy(c.h_raw.as<uint8_t>() + ho[i], queries[q0 + i], ho[i + 1] - ho[i]);
+        uint8_t* hr = c.h_raw.as<uint8_t>();
+        parallel_ranges(B, 16384, [&](size_t a, size_t e) {
+            for (size_t i = a; i < e; ++i)
+                if (queries[q0 + i]) std::memcpy(hr + ho[i], queries[q0 + i], ho[i + 1] - ho[i]);
+        });
+        ht.mark("pack queries");
         ok = ensure_queries(c, B, qbytes, thr) && ensure_outputs(c, B, stride) &&
              HIP_CHECK(hipMemcpyAsync(c.d_raw, c.h_raw.p, qbytes, hipMemcpyHostToDevice, c.stream)) &&
              HIP_CHECK(hipMemcpyAsync(c.d_off, ho, sizeof(uint64_t) * (B + 1), hipMemcpyHostToDevice, c.stream));
@@ -835,17 +899,21 @@ bool queue_host_chunk(Library& L, Replica& R, Context& c, const CharT* const* qu
     if (queue_search(L, R, c, h.d_raw, h.d_off, B, qbytes, thr, Lm, (uint32_t)stride, h.d_n, h.d_k, h.d_s, c.stream,
                      h.P, h.small) != 0)
         return false;
+    ht.mark("copy in + queue kernels");
     return !h.small || HIP_CHECK(hipMemcpyAsync(c.h_sio, c.d_sio, kSioStats + h.block, hipMemcpyDeviceToHost, c.stream));
 }
 
 // Completes a queued chunk: waits, runs the general path, reads back exactly the results
-// (packed on the device for large chunks) and appends them.
-bool finish_host_chunk(Library& L, Replica& R, HostChunk& h, uint32_t Lm, std::vector<uint32_t>& counts,
-                       std::vector<uint32_t>& keys, std::vector<float>& scores) {
+// (packed on the device for large chunks), fills the chunk's counts and hands its records to
+// `emit(keys, scores, n)`.
+template <class Emit>
+bool finish_host_chunk(Library& L, Replica& R, HostChunk& h, uint32_t Lm, std::vector<uint32_t>& counts, Emit&& emit) {
     Context& c = *h.c;
     const uint32_t B = h.B, q0 = h.q0;
     const size_t stride = Lm;
+    HostTimer ht;
     if (finish_search(L, R, c, B, h.P, h.d_off, h.d_n, h.d_k, h.d_s, c.stream, h.small) != 0) return false;
+    ht.mark("wait for kernels");
     if (h.small) {
         const uint32_t* counts3 = reinterpret_cast<const uint32_t*>(c.h_sio) + kStatSlots * 16;
         if (counts3[0]) {  // the general path ran after the read-back: read the results again
@@ -857,11 +925,14 @@ bool finish_host_chunk(Library& L, Replica& R, HostChunk& h, uint32_t Lm, std::v
         const uint32_t* hn = reinterpret_cast<const uint32_t*>(c.h_sio + kSioStats);
         const uint32_t* hk = hn + B + 1;
         const float* hs = reinterpret_cast<const float*>(hk + (size_t)B * stride);
+        std::vector<uint32_t> k;
+        std::vector<float> sc;
         for (uint32_t i = 0; i < B; ++i) {
             counts[q0 + i] = hn[i];
-            keys.insert(keys.end(), hk + (size_t)i * stride, hk + (size_t)i * stride + hn[i]);
-            scores.insert(scores.end(), hs + (size_t)i * stride, hs + (size_t)i * stride + hn[i]);
+            k.insert(k.end(), hk + (size_t)i * stride, hk + (size_t)i * stride + hn[i]);
+            sc.insert(sc.end(), hs + (size_t)i * stride, hs + (size_t)i * stride + hn[i]);
         }
+        emit(k.data(), sc.data(), (uint32_t)k.size());
         return true;
     }
     // large batches: pack on the device (prefix sum of the counts, one copy per query), read
@@ -873,6 +944,7 @@ bool finish_host_chunk(Library& L, Replica& R, HostChunk& h, uint32_t Lm, std::v
         !HIP_CHECK(hipMemcpyAsync(c.h_res.p, c.d_pos, sizeof(uint32_t) * (B + 1), hipMemcpyDeviceToHost, c.stream)) ||
         !HIP_CHECK(hipStreamSynchronize(c.stream)))
         return false;
+    ht.mark("pack + offsets back");
     const uint32_t total = c.h_res.as<uint32_t>()[B];
     for (uint32_t i = 0; i < B; ++i) counts[q0 + i] = c.h_res.as<uint32_t>()[i + 1] - c.h_res.as<uint32_t>()[i];
     if (!c.h_res.grow(sizeof(uint32_t) * 2 * (size_t)total) ||
@@ -881,11 +953,11 @@ bool finish_host_chunk(Library& L, Replica& R, HostChunk& h, uint32_t Lm, std::v
                                   c.stream)) ||
         !HIP_CHECK(hipStreamSynchronize(c.stream)))
         return false;
-    // appended straight from the pinned buffer (no zero-filling resize first)
+    ht.mark("records back");
+    // straight from the pinned buffer
     const uint32_t* pk = c.h_res.as<uint32_t>();
-    const float* ps = reinterpret_cast<const float*>(pk + total);
-    keys.insert(keys.end(), pk, pk + total);
-    scores.insert(scores.end(), ps, ps + total);
+    emit(pk, reinterpret_cast<const float*>(pk + total), total);
+    ht.mark("emit");
     return true;
 }
 
@@ -895,14 +967,12 @@ bool finish_host_chunk(Library& L, Replica& R, HostChunk& h, uint32_t Lm, std::v
 constexpr uint32_t kPipeChunks = 4;
 constexpr uint32_t kPipeMinChunk = 8192;
 
-// Scores n queries (characters of the index's width) on one replica; fills counts and flat
-// (key, score) vectors.
-template <typename CharT>
-bool host_search_one(Library& L, Replica& R, const CharT* const* queries, uint32_t nq, float thr, uint32_t Lm,
-                     std::vector<uint32_t>& counts, std::vector<uint32_t>& keys, std::vector<float>& scores) {
+// Scores n queries (characters of the index's width) on one replica; fills counts and hands
+// each chunk's records, in query order, to emit(keys, scores, n).
+template <typename CharT, class Emit>
+bool host_search_chunks(Library& L, Replica& R, const CharT* const* queries, uint32_t nq, float thr, uint32_t Lm,
+                        std::vector<uint32_t>& counts, Emit&& emit) {
     counts.assign(nq, 0);
-    keys.clear();
-    scores.clear();
     if (Lm == 0 || nq == 0) return true;
     if (!HIP_CHECK(hipSetDevice(R.device))) return false;
     const size_t stride = Lm;
@@ -932,7 +1002,7 @@ bool host_search_one(Library& L, Replica& R, const CharT* const* queries, uint32
             ok = queue_host_chunk(L, R, *ctx[k & 1], queries, q0, B, thr, Lm, fl[k & 1]);
             if (!ok) break;
         }
-        if (pending) ok = finish_host_chunk(L, R, fl[(k - 1) & 1], Lm, counts, keys, scores);
+        if (pending) ok = finish_host_chunk(L, R, fl[(k - 1) & 1], Lm, counts, emit);
         pending = k < n_chunks;
     }
     if (!ok)  // a chunk may still be queued: let it drain before its context is reused
@@ -941,6 +1011,18 @@ bool host_search_one(Library& L, Replica& R, const CharT* const* queries, uint32
     for (auto& c : ctx)
         if (c) R.give_back(std::move(c));
     return ok;
+}
+
+// ... into flat (key, score) vectors
+template <typename CharT>
+bool host_search_one(Library& L, Replica& R, const CharT* const* queries, uint32_t nq, float thr, uint32_t Lm,
+                     std::vector<uint32_t>& counts, std::vector<uint32_t>& keys, std::vector<float>& scores) {
+    keys.clear();
+    scores.clear();
+    return host_search_chunks(L, R, queries, nq, thr, Lm, counts, [&](const uint32_t* k, const float* sc, uint32_t n) {
+        keys.insert(keys.end(), k, k + n);
+        scores.insert(scores.end(), sc, sc + n);
+    });
 }
 
 // Queries per replica below which a batch is not split (a split costs a host thread and a
@@ -1049,9 +1131,49 @@ uint32_t batch_query(uint32_t handle, const CharT* const* queries, uint32_t nq, 
     if (!L || !L->host.indexed || !queries || !counts || L->host.csize != sizeof(CharT)) return 0;
     std::vector<uint32_t> cnt, keys;
     std::vector<float> sc;
+    HostTimer ht;
+    const uint32_t Lm = effective_limit(*L, limit);
+    const bool one_replica = L->reps.size() == 1 || nq / split_min() <= 1;
+    if (one_replica && Lm && (uint64_t)nq * Lm <= kDirectMax && nq >= kSmallBatch) {
+        // marshalled as the chunks finish, straight into the caller's arrays: new[]'d at the
+        // batch's capacity (nq x limit entries; only the pages written are ever touched), each
+        // chunk's key pointers and scores filled from the pinned read-back while the next chunk's
+        // kernels run
+        const size_t cap = (size_t)nq * Lm;
+        CharT** res = new CharT*[cap];
+        float* out_s = scores ? new float[cap] : nullptr;
+        advise_huge(res, cap * sizeof(CharT*));
+        if (out_s) advise_huge(out_s, cap * sizeof(float));
+        size_t off = 0;
+        const char* base = L->host.key_bytes.data();
+        const uint64_t* koff = L->host.key_off.data();
+        const bool ok = host_search_chunks(*L, *L->reps.front(), queries, nq, thr, Lm, cnt,
+                                           [&](const uint32_t* k, const float* sc, uint32_t n) {
+            parallel_ranges(n, size_t(1) << 16, [&](size_t a, size_t e) {
+                for (size_t i = a; i < e; ++i) {  // key_off gathered at random: memory-latency bound
+                    res[off + i] = reinterpret_cast<CharT*>(const_cast<char*>(base) + koff[k[i]] * sizeof(CharT));
+                    if (out_s) out_s[off + i] = sc[i];
+                }
+            });
+            off += n;
+        });
+        if (!ok) {
+            delete[] res;
+            delete[] out_s;
+            return 0;
+        }
+        ht.mark("search + marshal (chunks)");
+        std::copy(cnt.begin(), cnt.end(), counts);
+        *results = res;
+        if (scores) *scores = out_s;
+        return (uint32_t)off;
+    }
     if (!host_search(*L, queries, nq, thr, limit, cnt, keys, sc)) return 0;
+    ht.mark("search (all chunks)");
     std::copy(cnt.begin(), cnt.end(), counts);
-    return marshal(*L, keys, sc, results, scores);
+    const uint32_t n = marshal(*L, keys, sc, results, scores);
+    ht.mark("marshal");
+    return n;
 }
 
 }  // namespace

@@ -12,6 +12,7 @@
 // (-ffp-contract=off); threshold `s < thr` in fp32; promotion test `(double)s > 0.999`.
 #include <hipcub/hipcub.hpp>
 
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 
@@ -173,12 +174,6 @@ __global__ __launch_bounds__(64) void k_prep(const uint8_t* __restrict__ raw, co
     }
 }
 
-#ifndef NGS_G1S_CAP
-// workgroups of the sliced hand-over launches (grid-stride); C4, whose 26,594 hand-overs of a
-// batch run as 4 slices each: 65,536 -> 443-446 ms, 16,384 -> 457-463, 4,096 -> 541 per batch
-// (static striding balances worse than the hardware dispatcher); C3/C5 within noise
-#define NGS_G1S_CAP 65536
-#endif
 
 // ---------------------------------------------------------------- shared helpers -----
 // libStr = escapeBlank(key); trim; libStr == query (nGramSearch.hpp:330-334: the key is NOT
@@ -2369,6 +2364,27 @@ __global__ __launch_bounds__(64 * W, kWaveWavesPerSimd) void k_wave(DevIndex X, 
         return;
     }
     const uint32_t cnt = *qcount;
+    if (W == 1 && P.qhead) {
+        // a persistent grid of about one workgroup per slot of the GPU pulls (query, slice) items:
+        // a near-empty list no longer dispatches B x slices workgroups beside tier 1a, and a long
+        // one balances like the hardware dispatcher did. Workgroups beyond the item count leave
+        // without touching the counter (thousands of atomics on one address serialise: C2's
+        // empty lists cost 80 us that way)
+        const uint32_t items = cnt * nsl;
+        if (blockIdx.x >= items) return;
+        for (uint32_t t = blockIdx.x;;) {
+            if (t >= items) break;
+            const uint32_t i = t / nsl;
+            wave_query<W, false>(S, qlist[i], X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats,
+                                 nullptr, nullptr, t - i * nsl, nsl);
+            __syncthreads();
+            // the first gridDim.x items went one to a workgroup; the rest are pulled in turn
+            uint32_t nt = 0;
+            if (threadIdx.x == 0) nt = gridDim.x + atomicAdd(P.qhead, 1u);
+            t = __builtin_amdgcn_readfirstlane(nt);  // (every lane active: lane 0 holds it)
+        }
+        return;
+    }
     for (uint32_t t = blockIdx.x; t < cnt * nsl; t += gridDim.x) {
         const uint32_t i = t / nsl;
         wave_query<W, false>(S, qlist[i], X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats,
@@ -2783,6 +2799,20 @@ __global__ __launch_bounds__(256) void k_lists(const uint32_t* __restrict__ slot
 // NGS_SYNC_DEBUG=1 (diagnostics): every launch of a search is followed by a wait on its stream,
 // and the first kernel whose wait fails is named on stderr (a fault is otherwise reported by a
 // later, unrelated call)
+// workgroups of a persistent grid: one per slot of the GPU at `waves_per_simd` one-wave workgroups
+// per SIMD (CUs x 4 SIMDs x waves), for the device current on the calling thread
+static uint32_t persistent_slots(uint32_t waves_per_simd) {
+    static std::atomic<int> cu_count[64] = {};  // per device, read once
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+    int cus = cu_count[dev].load(std::memory_order_relaxed);
+    if (cus <= 0) {
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+        cu_count[dev].store(cus, std::memory_order_relaxed);
+    }
+    return (uint32_t)cus * 4u * waves_per_simd;
+}
+
 static bool sync_debug() {
     static const bool on = [] {
         const char* e = std::getenv("NGS_SYNC_DEBUG");
@@ -2831,10 +2861,17 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
         case 0: {
             // beside tier 1a: the heavy list through the lean kernel, k_emit and tier 1b on its
             // hand-overs (side), and the full list through tier 1b (side2)
-            const uint32_t g1b = std::min<uint32_t>(P.n_queries, 4096);  // grid-stride over the list
-            // sliced tier-1b launches: a wave per (query, slice)
-            const uint32_t g1s = std::min<uint32_t>(P.n_queries * std::max<uint32_t>(P.nslices, 1u), NGS_G1S_CAP);
+            const uint32_t g1b = std::min<uint32_t>(P.n_queries, 1024);  // k_merge: grid-stride over the list
+            // tier-1b launches over the hand-over and full lists: persistent grids of one workgroup
+            // per slot of the GPU (kWaveWavesPerSimd per SIMD), items from a counter in the
+            // path-count line (zeroed per call with it)
+            const uint32_t g1s = std::min<uint32_t>(P.n_queries * std::max<uint32_t>(P.nslices, 1u),
+                                                    persistent_slots(kWaveWavesPerSimd));
             const uint32_t gh = std::min<uint32_t>(P.n_queries, P.heavy_grid ? P.heavy_grid : 4096);
+            const uint32_t gfull = std::min<uint32_t>(P.n_queries, persistent_slots(kWaveWavesPerSimd));
+            SearchParams PM = P, PHO = P;  // the main and the heavy hand-over launches
+            PM.qhead = gcount + 8;
+            PHO.qhead = gcount + 9;
             // (esn[] was reset by k_prep)
             auto main_lean = [&]() {
                 hipLaunchKernelGGL(k_wave_lean<kDeferEmit>, dim3(P.n_queries), dim3(64), 0, s, X, P, qnorm, off, qm,
@@ -2857,7 +2894,7 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
                 hipLaunchKernelGGL(k_emit, dim3((gh + kEmitWaves - 1) / kEmitWaves), dim3(64 * kEmitWaves), 0, side,
                                    X, PH, qnorm, off, qm, out_n, out_k, out_s, stats, heavy, hcount);
                 dbg_check(side, "k_emit (heavy list)");
-                hipLaunchKernelGGL(k_wave<1>, dim3(g1s), dim3(64), 0, side, X, P, qnorm, off, qm, out_n, out_k,
+                hipLaunchKernelGGL(k_wave<1>, dim3(g1s), dim3(64), 0, side, X, PHO, qnorm, off, qm, out_n, out_k,
                                    out_s, list2, count2, stats, (const uint32_t*)fb2, (const uint32_t*)fbc2);
                 dbg_check(side, "k_wave<1> (heavy hand-overs)");
                 if (P.nslices > 1) {
@@ -2883,8 +2920,9 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
                 // measured 17 % slower than one wave (the hand-over lists below gain from slicing)
                 SearchParams PF = P;
                 PF.nslices = 1;
-                hipLaunchKernelGGL(k_wave<1>, dim3(gh), dim3(64), 0, side2, X, PF, qnorm, off, qm, out_n, out_k, out_s,
-                                   list2, count2, stats, full, fcount);
+                PF.qhead = gcount + 10;
+                hipLaunchKernelGGL(k_wave<1>, dim3(gfull), dim3(64), 0, side2, X, PF, qnorm, off, qm, out_n, out_k,
+                                   out_s, list2, count2, stats, full, fcount);
                 dbg_check(side2, "k_wave<1> (full list)");
             }
             if ((e = hipEventRecord(join2, side2)) != hipSuccess) return e;
@@ -2896,7 +2934,7 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
                 dbg_check(s, "k_emit");
             }
             // tier 1b over the queries tier 1a handed over
-            hipLaunchKernelGGL(k_wave<1>, dim3(g1s), dim3(64), 0, s, X, P, qnorm, off, qm, out_n, out_k, out_s,
+            hipLaunchKernelGGL(k_wave<1>, dim3(g1s), dim3(64), 0, s, X, PM, qnorm, off, qm, out_n, out_k, out_s,
                                list2, count2, stats, (const uint32_t*)fb, (const uint32_t*)fbc);
             dbg_check(s, "k_wave<1> (hand-overs)");
             if (P.nslices > 1) {
