@@ -171,6 +171,16 @@ NGS_API int ngsSearchDeviceAsync(uint32_t handle, const uint8_t* dQueryBytes, co
                                  uint64_t* ticket);
 NGS_API int ngsSearchDeviceWait(uint32_t handle, uint64_t ticket);
 
+/* Low-latency score()/search() (opt-in; narrow indexes): with enable != 0 a persistent one-wave
+ * server kernel answers single queries from a request block in pinned host memory, with no
+ * kernel launch, copy or stream wait per call. It serves libraries small enough that one wave
+ * searches a query (large libraries keep the sliced latency path) and limits up to 128; other
+ * calls take the regular path. The kernel leaves after 200 ms without a request and is relaunched
+ * on the next call; enable = 0 or dispose() stops it. Answers are the regular path's, bit for
+ * bit. Returns 0, -1 (bad handle), -2 (unbuilt index), -3 (wide index), -4 (HIP error). Calls
+ * through the server are serialised on the handle. */
+NGS_API int ngsServe(uint32_t handle, int enable);
+
 /* Per-call statistics of the last search on `handle` (enable timing first). */
 typedef struct {
     uint64_t queries;          /* queries in the call */

@@ -135,6 +135,9 @@ def lib():
                                            C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64)]
         L.ngsSearchDeviceWait.restype = C.c_int
         L.ngsSearchDeviceWait.argtypes = [u32, C.c_uint64]
+    if hasattr(L, "ngsServe"):
+        L.ngsServe.restype = C.c_int
+        L.ngsServe.argtypes = [u32, C.c_int]
     L.ngsSetTiming.restype = C.c_int
     L.ngsSetTiming.argtypes = [u32, C.c_int]
     if hasattr(L, "ngsLastError"):  # (experiment builds of older sources lack it)

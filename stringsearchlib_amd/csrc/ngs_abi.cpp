@@ -5,11 +5,12 @@
 // (:22), smallest-free-handle allocation (:41-46), shared locks for searches (:63,84,100,122,
 // 135,147) and exclusive locks for indexN/dispose (:39,112).
 #include <hip/hip_runtime.h>
-#include <sys/mman.h>
 
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <functional>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -74,26 +75,89 @@ struct HostTimer {
 // filled as chunks finish (batch_query); larger ones collect the records first
 constexpr uint64_t kDirectMax = uint64_t(1) << 25;
 
-// Large result arrays fault in a 4 KB page at a time on first write (1.3M records at C3: ~2,600
-// faults per array); transparent huge pages, where the kernel offers them, take 2 MB at a time
-inline void advise_huge(void* p, size_t bytes) {
-    constexpr uintptr_t kHuge = uintptr_t(2) << 20;
-    const uintptr_t a = (reinterpret_cast<uintptr_t>(p) + kHuge - 1) & ~(kHuge - 1);
-    const uintptr_t e = (reinterpret_cast<uintptr_t>(p) + bytes) & ~(kHuge - 1);
-    if (e > a) (void)madvise(reinterpret_cast<void*>(a), e - a, MADV_HUGEPAGE);
-}
 
 // body(lo, hi) over [0, n) on up to 8 host threads (one below `serial_below` items)
+// A fixed pool of host worker threads for the batch path's packing and marshalling: spawning
+// eight threads per use cost ~50 us each time (the pool's workers wait on a condition variable).
+class HostPool {
+  public:
+    static HostPool& get() {
+        static HostPool p;
+        return p;
+    }
+    size_t size() const { return workers_.size() + 1; }
+    // runs task(i) for i in [0, n) on the workers and the caller; returns when all are done
+    void run(size_t n, const std::function<void(size_t)>& task) {
+        std::unique_lock<std::mutex> lk(mu_);
+        busy_.wait(lk, [&] { return !task_; });  // one parallel section at a time
+        task_ = &task;
+        n_ = n;
+        next_ = 0;
+        left_ = n;
+        ++gen_;
+        work_.notify_all();
+        while (next_ < n_) {  // the caller takes items too
+            const size_t i = next_++;
+            lk.unlock();
+            task(i);
+            lk.lock();
+            --left_;
+        }
+        done_.wait(lk, [&] { return left_ == 0; });
+        task_ = nullptr;
+        busy_.notify_all();
+    }
+
+  private:
+    HostPool() {
+        const size_t nt = std::min<size_t>(8, std::max(1u, std::thread::hardware_concurrency()));
+        for (size_t t = 1; t < nt; ++t) workers_.emplace_back([this] { loop(); });
+    }
+    ~HostPool() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            quit_ = true;
+        }
+        work_.notify_all();
+        for (auto& w : workers_) w.join();
+    }
+    void loop() {
+        std::unique_lock<std::mutex> lk(mu_);
+        uint64_t seen = 0;
+        for (;;) {
+            work_.wait(lk, [&] { return quit_ || (task_ && gen_ != seen && next_ < n_); });
+            if (quit_) return;
+            seen = gen_;
+            while (task_ && next_ < n_) {
+                const size_t i = next_++;
+                const std::function<void(size_t)>* t = task_;
+                lk.unlock();
+                (*t)(i);
+                lk.lock();
+                if (--left_ == 0) done_.notify_all();
+            }
+        }
+    }
+    std::vector<std::thread> workers_;
+    std::mutex mu_;
+    std::condition_variable work_, done_, busy_;
+    const std::function<void(size_t)>* task_ = nullptr;
+    size_t n_ = 0, next_ = 0, left_ = 0;
+    uint64_t gen_ = 0;
+    bool quit_ = false;
+};
+
+// body(lo, hi) over [0, n) on the host pool (serially below `serial_below` items)
 template <class F>
 void parallel_ranges(size_t n, size_t serial_below, F&& body) {
-    const size_t nt = n < serial_below ? 1 : std::min<size_t>(8, std::max(1u, std::thread::hardware_concurrency()));
+    HostPool& pool = HostPool::get();
+    const size_t nt = n < serial_below ? 1 : pool.size();
     if (nt <= 1) {
         body(size_t(0), n);
         return;
     }
-    std::vector<std::thread> th;
-    for (size_t t = 0; t < nt; ++t) th.emplace_back(body, n * t / nt, n * (t + 1) / nt);
-    for (auto& x : th) x.join();
+    const std::function<void(size_t)> task = [&](size_t t) { body(n * t / nt, n * (t + 1) / nt); };
+    pool.run(nt, task);
 }
 
 template <class T>
@@ -293,7 +357,58 @@ struct Replica {
     }
 };
 
+// ngsServe: the low-latency score() path. A persistent one-wave kernel (k_serve) on a stream of
+// its own polls a request block in coherent pinned host memory; score() writes the normalised
+// query there, publishes a request number and spins until the kernel publishes it back with the
+// results: no launch, no copy, no stream wait per call. The kernel exits on stop, after
+// kServeIdleMs without a request or after kServeLifeMs, and is relaunched on demand.
+constexpr uint32_t kServeIdleMs = 200;
+constexpr uint32_t kServeLifeMs = 10000;
+
+struct Server {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    ServeBlock* h = nullptr;  // coherent pinned host memory
+    ServeBlock* d = nullptr;  // its device view
+    DevStats* scratch = nullptr;
+    uint32_t* list2 = nullptr;
+    uint64_t seq = 0;
+    bool launched = false;
+
+    bool init(int dev) {
+        device = dev;
+        if (!HIP_CHECK(hipSetDevice(dev)) || !HIP_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking)) ||
+            !HIP_CHECK(hipHostMalloc((void**)&h, sizeof(ServeBlock), hipHostMallocCoherent | hipHostMallocMapped)) ||
+            !HIP_CHECK(hipHostGetDevicePointer((void**)&d, h, 0)) ||
+            !HIP_CHECK(hipMalloc((void**)&scratch, sizeof(DevStats) * (kStatSlots + 1))) ||
+            !HIP_CHECK(hipMalloc((void**)&list2, sizeof(uint32_t) * 4)))
+            return false;
+        std::memset((void*)h, 0, sizeof(ServeBlock));
+        return HIP_CHECK(hipMemset(scratch, 0, sizeof(DevStats) * (kStatSlots + 1)));
+    }
+    // the kernel has left (idle, lifetime, stop) or was never launched
+    bool stopped() { return !launched || hipStreamQuery(stream) == hipSuccess; }
+    void stop() {
+        if (!h) return;
+        __atomic_store_n(&h->stop, 1u, __ATOMIC_RELEASE);
+        if (stream) hipStreamSynchronize(stream);  // it exits within one poll
+        launched = false;
+        __atomic_store_n(&h->stop, 0u, __ATOMIC_RELEASE);
+    }
+    ~Server() {
+        if (h) stop();
+        hipSetDevice(device);
+        if (stream) hipStreamDestroy(stream);
+        if (h) hipHostFree(h);
+        if (scratch) hipFree(scratch);
+        if (list2) hipFree(list2);
+    }
+};
+
 struct Library {
+    std::unique_ptr<Server> server;  // ngsServe (null: off)
+    std::atomic<bool> serving{false};  // server != null, for the unlocked test in one_query
+    std::mutex server_mu;            // creating / dropping it
     HostIndex host;
     int device = 0;                              // first replica's device (or the build device)
     std::vector<std::unique_ptr<Replica>> reps;  // empty until the index is on a GPU
@@ -325,6 +440,7 @@ struct Library {
     uint64_t next_ticket = 1;
 
     ~Library() {
+        server.reset();  // stops the kernel before the index it reads is freed
         for (auto& kv : pending)  // dispose: nothing may still run on the buffers freed below
             if (kv.second.c) hipStreamSynchronize(kv.second.c->stream);
         pending.clear();
@@ -907,7 +1023,8 @@ bool queue_host_chunk(Library& L, Replica& R, Context& c, const CharT* const* qu
 // (packed on the device for large chunks), fills the chunk's counts and hands its records to
 // `emit(keys, scores, n)`.
 template <class Emit>
-bool finish_host_chunk(Library& L, Replica& R, HostChunk& h, uint32_t Lm, std::vector<uint32_t>& counts, Emit&& emit) {
+bool finish_host_chunk(Library& L, Replica& R, HostChunk& h, uint32_t Lm, std::vector<uint32_t>& counts, bool last,
+                       Emit&& emit) {
     Context& c = *h.c;
     const uint32_t B = h.B, q0 = h.q0;
     const size_t stride = Lm;
@@ -932,7 +1049,7 @@ bool finish_host_chunk(Library& L, Replica& R, HostChunk& h, uint32_t Lm, std::v
             k.insert(k.end(), hk + (size_t)i * stride, hk + (size_t)i * stride + hn[i]);
             sc.insert(sc.end(), hs + (size_t)i * stride, hs + (size_t)i * stride + hn[i]);
         }
-        emit(k.data(), sc.data(), (uint32_t)k.size());
+        emit(k.data(), sc.data(), (uint32_t)k.size(), last);
         return true;
     }
     // large batches: pack on the device (prefix sum of the counts, one copy per query), read
@@ -956,15 +1073,17 @@ bool finish_host_chunk(Library& L, Replica& R, HostChunk& h, uint32_t Lm, std::v
     ht.mark("records back");
     // straight from the pinned buffer
     const uint32_t* pk = c.h_res.as<uint32_t>();
-    emit(pk, reinterpret_cast<const float*>(pk + total), total);
+    emit(pk, reinterpret_cast<const float*>(pk + total), total, last);
     ht.mark("emit");
     return true;
 }
 
-// A large host batch runs as about kPipeChunks chunks (of at least kPipeMinChunk queries) over
-// two contexts, one queued ahead: chunk k's packing, copies and read-back overlap chunk k + 1's
-// kernels, and the two chunks' kernels overlap each other on the GPU.
-constexpr uint32_t kPipeChunks = 4;
+// A large host batch can run as about kPipeChunks chunks (of at least kPipeMinChunk queries; env
+// NGS_PIPE_CHUNKS) over two contexts, one queued ahead, so that chunk k's copies and read-back
+// overlap chunk k + 1's kernels. Measured slower than one chunk at C3 (the chunks' read-backs
+// waited behind the other chunk's kernels), so one chunk is the default; the batch is still cut
+// into chunks where its outputs would exceed kOutBudget / kPartBudget.
+constexpr uint32_t kPipeChunks = 1;  // measured: 4 chunks 6.1-6.6 ms against 4.4-4.6 for one at C3
 constexpr uint32_t kPipeMinChunk = 8192;
 
 // Scores n queries (characters of the index's width) on one replica; fills counts and hands
@@ -1002,7 +1121,7 @@ bool host_search_chunks(Library& L, Replica& R, const CharT* const* queries, uin
             ok = queue_host_chunk(L, R, *ctx[k & 1], queries, q0, B, thr, Lm, fl[k & 1]);
             if (!ok) break;
         }
-        if (pending) ok = finish_host_chunk(L, R, fl[(k - 1) & 1], Lm, counts, emit);
+        if (pending) ok = finish_host_chunk(L, R, fl[(k - 1) & 1], Lm, counts, k == n_chunks, emit);
         pending = k < n_chunks;
     }
     if (!ok)  // a chunk may still be queued: let it drain before its context is reused
@@ -1019,7 +1138,8 @@ bool host_search_one(Library& L, Replica& R, const CharT* const* queries, uint32
                      std::vector<uint32_t>& counts, std::vector<uint32_t>& keys, std::vector<float>& scores) {
     keys.clear();
     scores.clear();
-    return host_search_chunks(L, R, queries, nq, thr, Lm, counts, [&](const uint32_t* k, const float* sc, uint32_t n) {
+    return host_search_chunks(L, R, queries, nq, thr, Lm, counts, [&](const uint32_t* k, const float* sc, uint32_t n,
+                                                                       bool) {
         keys.insert(keys.end(), k, k + n);
         scores.insert(scores.end(), sc, sc + n);
     });
@@ -1109,6 +1229,83 @@ uint32_t marshal(const Library& L, const std::vector<uint32_t>& keys, const std:
     return (uint32_t)n;
 }
 
+// The query normalised as k_prep does it (escapeBlank with the index's validChar set, C-locale
+// trim, toUpper; nGramSearch.hpp:372-376): its length (kQueryWildcard for "" and "*"), false if
+// it does not fit `cap` characters.
+bool host_normalise(const uint32_t* valid, const char* q, uint8_t* out, uint32_t cap, uint32_t& m) {
+    const size_t n = std::strlen(q);
+    if (n == 0 || (n == 1 && q[0] == '*')) {  // nGramSearch.hpp:356
+        m = kQueryWildcard;
+        return true;
+    }
+    auto esc = [&](uint8_t c) -> uint8_t { return ((valid[c >> 5] >> (c & 31)) & 1u) ? c : (uint8_t)' '; };
+    auto space = [](uint8_t c) { return c == ' ' || (c >= 9 && c <= 13); };
+    size_t a = 0, e = n;
+    while (a < e && space(esc((uint8_t)q[a]))) ++a;
+    while (e > a && space(esc((uint8_t)q[e - 1]))) --e;
+    if (e - a > cap) return false;
+    m = (uint32_t)(e - a);
+    for (size_t i = a; i < e; ++i) {
+        const uint8_t c = esc((uint8_t)q[i]);
+        out[i - a] = (c >= 'a' && c <= 'z') ? (uint8_t)(c - 32) : c;
+    }
+    return true;
+}
+
+// score() through the server (ngsServe): false when the call must take the regular path (a
+// limit above the wave search's, a library large enough for the sliced latency path, a query
+// the server routes to tier 2 or the general path, or a server that cannot be reached).
+bool serve_query(Library& L, const char* query, float thr, uint32_t limit, std::vector<uint32_t>& keys,
+                 std::vector<float>& sc) {
+    std::lock_guard<std::mutex> g(L.server_mu);  // one request in flight; ngsServe(0) waits for it
+    Server* sv = L.server.get();
+    const uint32_t Lm = effective_limit(L, limit);
+    Replica& R = *L.reps.front();
+    if (!sv || Lm == 0 || Lm > kWaveMaxLimit || R.dev.n_buckets / 8 > 1) return false;
+    ServeBlock* b = sv->h;
+    uint32_t m = 0;
+    {
+        std::lock_guard<std::mutex> gv(L.valid_mu);
+        if (!host_normalise(L.valid, query, b->q, kServeMaxQuery, m)) return false;
+        std::memcpy(b->valid, L.valid, sizeof(b->valid));
+    }
+    b->thr = thr;
+    b->limit = Lm;
+    b->m = m;
+    b->off[0] = 0;
+    b->off[1] = m == kQueryWildcard ? 0 : m;
+    const uint64_t seq = ++sv->seq;
+    auto launch = [&]() -> bool {
+        if (!HIP_CHECK(hipSetDevice(sv->device))) return false;
+        SearchParams P{};
+        P.n_queries = 1;
+        P.nslices = 1;
+        sv->launched = HIP_CHECK(launch_serve(R.dev, P, sv->d, sv->scratch, sv->list2, kServeIdleMs, kServeLifeMs,
+                                              sv->stream));
+        return sv->launched;
+    };
+    if (sv->stopped() && !launch()) return false;
+    __atomic_store_n(&b->req_seq, seq, __ATOMIC_RELEASE);  // the fields above first (x86 stores stay in order)
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint64_t spin = 1; __atomic_load_n(&b->done_seq, __ATOMIC_ACQUIRE) != seq; ++spin) {
+        if ((spin & 1023) == 0) {
+            // the kernel left (its idle time ran out as the request came in): relaunch, it
+            // answers the posted request
+            if (sv->stopped() && !launch()) return false;
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+                sv->stop();  // unreachable: leave it to the regular path
+                return false;
+            }
+        }
+        __builtin_ia32_pause();
+    }
+    if (__atomic_load_n(&b->status, __ATOMIC_ACQUIRE) != 0) return false;
+    const uint32_t n = std::min(b->n, Lm);
+    keys.assign(b->keys, b->keys + n);
+    sc.assign(b->scores, b->scores + n);
+    return true;
+}
+
 // A narrow call on a wide index (or the reverse) is answered like an unknown handle.
 template <typename CharT>
 uint32_t one_query(uint32_t handle, const CharT* query, CharT*** results, float** scores, float thr,
@@ -1118,6 +1315,8 @@ uint32_t one_query(uint32_t handle, const CharT* query, CharT*** results, float*
     if (!L || !L->host.indexed || !query || L->host.csize != sizeof(CharT)) return 0;  // dllmain.cpp:69, hpp:417-418
     std::vector<uint32_t> counts, keys;
     std::vector<float> sc;
+    if (sizeof(CharT) == 1 && L->serving.load(std::memory_order_acquire) && serve_query(*L, reinterpret_cast<const char*>(query), thr, limit, keys, sc))
+        return marshal(*L, keys, sc, results, scores);
     if (!host_search(*L, &query, 1, thr, limit, counts, keys, sc)) return 0;
     return marshal(*L, keys, sc, results, scores);
 }
@@ -1139,24 +1338,38 @@ uint32_t batch_query(uint32_t handle, const CharT* const* queries, uint32_t nq, 
         // batch's capacity (nq x limit entries; only the pages written are ever touched), each
         // chunk's key pointers and scores filled from the pinned read-back while the next chunk's
         // kernels run
-        const size_t cap = (size_t)nq * Lm;
-        CharT** res = new CharT*[cap];
-        float* out_s = scores ? new float[cap] : nullptr;
-        advise_huge(res, cap * sizeof(CharT*));
-        if (out_s) advise_huge(out_s, cap * sizeof(float));
-        size_t off = 0;
+        // one chunk (the common case): the arrays at the exact size, filled from the pinned
+        // read-back; several chunks: at the batch's capacity (nq x limit entries; only the pages
+        // written are touched)
+        CharT** res = nullptr;
+        float* out_s = nullptr;
+        size_t off = 0, cap = 0;
         const char* base = L->host.key_bytes.data();
         const uint64_t* koff = L->host.key_off.data();
         const bool ok = host_search_chunks(*L, *L->reps.front(), queries, nq, thr, Lm, cnt,
-                                           [&](const uint32_t* k, const float* sc, uint32_t n) {
+                                           [&](const uint32_t* k, const float* sc, uint32_t n, bool last) {
+            if (!res) {
+                cap = (off == 0 && last) ? std::max<size_t>(n, 1) : (size_t)nq * Lm;
+                res = new CharT*[cap];
+                out_s = scores ? new float[cap] : nullptr;
+            }
             parallel_ranges(n, size_t(1) << 16, [&](size_t a, size_t e) {
-                for (size_t i = a; i < e; ++i) {  // key_off gathered at random: memory-latency bound
+                // key_off is gathered at random (80 MB at C3): memory-latency bound, so the
+                // gathers run kPrefetch entries ahead
+                constexpr size_t kPrefetch = 24;
+                for (size_t i = a; i < std::min(e, a + kPrefetch); ++i) __builtin_prefetch(koff + k[i]);
+                for (size_t i = a; i < e; ++i) {
+                    if (i + kPrefetch < e) __builtin_prefetch(koff + k[i + kPrefetch]);
                     res[off + i] = reinterpret_cast<CharT*>(const_cast<char*>(base) + koff[k[i]] * sizeof(CharT));
                     if (out_s) out_s[off + i] = sc[i];
                 }
             });
             off += n;
         });
+        if (ok && !res) {  // no chunk ran (cannot happen with nq >= kSmallBatch): empty arrays
+            res = new CharT*[1];
+            out_s = scores ? new float[1] : nullptr;
+        }
         if (!ok) {
             delete[] res;
             delete[] out_s;
@@ -1508,6 +1721,26 @@ NGS_API int ngsSearchDeviceWait(uint32_t handle, uint64_t ticket) {
     }
     R.give_back(std::move(pd.c));
     return rc;
+}
+
+NGS_API int ngsServe(uint32_t handle, int enable) {
+    std::shared_lock<std::shared_mutex> lk(g_lock);
+    Library* L = find_lib(handle);
+    if (!L) return -1;
+    if (!L->host.indexed || L->reps.empty()) return -2;
+    if (L->host.csize != 1) return -3;
+    std::lock_guard<std::mutex> g(L->server_mu);
+    if (!enable) {
+        L->serving.store(false, std::memory_order_release);
+        L->server.reset();
+        return 0;
+    }
+    if (L->server) return 0;
+    auto sv = std::make_unique<Server>();
+    if (!sv->init(L->reps.front()->device)) return -4;
+    L->server = std::move(sv);
+    L->serving.store(true, std::memory_order_release);
+    return 0;
 }
 
 NGS_API int ngsLastError(int clear) {

@@ -277,6 +277,32 @@ struct SearchParams {
 constexpr uint32_t kSlices = NGS_SLICES;
 constexpr uint32_t kNoPart = 0xFFFFFFFFu;  // pcnt[q * nslices]: the query was answered unsliced
 
+// ---- low-latency score() (ngsServe, opt-in): a persistent one-wave server kernel polls a
+// request block in coherent pinned host memory, answers the query with the tier-1 wave search
+// and writes the results back into the same block; no launch, copy or wait per call.
+constexpr uint32_t kServeMaxQuery = 256;   // normalised query characters the block holds
+struct alignas(64) ServeBlock {
+    // host -> device
+    uint64_t req_seq;          // the host stores the request's number last (release)
+    uint32_t stop;             // != 0: the server exits
+    uint32_t pad0;
+    float thr;
+    uint32_t limit;            // effective limit (<= kWaveMaxLimit)
+    uint32_t m;                // normalised length, or kQueryWildcard
+    uint32_t pad1;
+    uint64_t off[2];           // {0, m}: the query's offsets into q (wave_query's qoff)
+    uint32_t valid[8];         // the index's validChar set at the call (setValidChar)
+    uint8_t q[kServeMaxQuery]; // the normalised query
+    // device -> host
+    uint64_t done_seq;         // the server stores the answered request's number last (release)
+    uint32_t alive;            // 1 while the server runs (set at start, cleared at exit)
+    uint32_t status;           // 0 answered; 1 the query needs the host path (tier 2 / general)
+    uint32_t n;                // results
+    uint32_t pad2[3];
+    uint32_t keys[kWaveMaxLimit];
+    float scores[kWaveMaxLimit];
+};
+
 // per-query normalised length sentinels written by the prep kernel
 constexpr uint32_t kQueryWildcard = 0xFFFFFFFFu;
 

@@ -892,6 +892,8 @@ struct alignas(16) WaveSmem {
 static_assert(kWaveSlots * 4 >= kWaveCand * 8, "tier 1a keeps the candidate buffer in the table");
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
 
+constexpr uint32_t kQueryInGlobal = 0xFFFFFFFEu;  // wave_query: read the query from qnorm / qoff / qm
+
 // popcount of the ballot bits of the lanes below this one (v_mbcnt_lo/hi)
 __device__ __forceinline__ uint32_t rank_below(unsigned long long b) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
@@ -1587,7 +1589,7 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
                                            uint32_t* __restrict__ list2, uint32_t* __restrict__ count2,
                                            DevStats* __restrict__ stats, uint32_t* __restrict__ fb,
                                            uint32_t* __restrict__ fbc, const uint32_t slice = 0,
-                                           const uint32_t nsl = 1) {
+                                           const uint32_t nsl = 1, const uint32_t m_in_lds = kQueryInGlobal) {
     const uint32_t lane = lane_id(), tid = threadIdx.x;
     // sliced tier 1b: this wave takes the term ids of skip-table buckets [K * slice / nsl,
     // K * (slice + 1) / nsl) and leaves its top-L records for k_merge (SearchParams.prec)
@@ -1607,7 +1609,8 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     };
     const uint32_t wid = W == 1 ? 0u : __builtin_amdgcn_readfirstlane(tid >> 6);
-    const uint32_t m = qm[q];
+    // m_in_lds: the caller (k_serve) put the normalised query in S.q already
+    const uint32_t m = m_in_lds != kQueryInGlobal ? m_in_lds : qm[q];
     const uint32_t L = P.limit;
     const size_t ob = (size_t)q * P.out_stride;
     if (m == kQueryWildcard) {  // nGramSearch.hpp:356-369, answer precomputed at index time
@@ -1633,8 +1636,10 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
     unsigned long long wt_ = __builtin_amdgcn_s_memtime();
     unsigned long long wacc_[16] = {};
 #endif
-    const uint8_t* qg = qnorm + qoff[q];
-    for (uint32_t i = tid; i < m; i += 64 * W) S.q[i] = char_at(qg, i, X.csize);
+    if (m_in_lds == kQueryInGlobal) {
+        const uint8_t* qg = qnorm + qoff[q];
+        for (uint32_t i = tid; i < m; i += 64 * W) S.q[i] = char_at(qg, i, X.csize);
+    }
     if (tid == 0) {
         S.surv_total = 0;
         S.ncand = 0;
@@ -2395,6 +2400,87 @@ __global__ __launch_bounds__(64 * W, kWaveWavesPerSimd) void k_wave(DevIndex X, 
 
 
 
+// ngsServe: the persistent low-latency server. One wave polls the request block (coherent pinned
+// host memory) with system-scope loads, answers each request with wave_query (the tier-1 wave
+// search, unsliced) writing the results straight into the block, then publishes the request's
+// number behind a system-scope release. It exits on blk->stop, after idle_ms without a request
+// or after life_ms in all (the host relaunches it on the next call), so it can never outlive its
+// process by more than that. s_memrealtime (100 MHz) is read through the scalar unit: a read.
+__device__ __forceinline__ uint64_t sys_load64(const uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint32_t sys_load32(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(64) void k_serve(DevIndex X, SearchParams P0, ServeBlock* blk, DevStats* scratch,
+                                              uint32_t* list2, uint32_t idle_ms, uint32_t life_ms) {
+    __shared__ WaveSmem<1> S;
+    const uint32_t lane = lane_id();
+    uint32_t* count2 = reinterpret_cast<uint32_t*>(scratch + kStatSlots);
+    if (lane == 0) __hip_atomic_store(&blk->alive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    uint64_t last = sys_load64(&blk->done_seq);
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    uint64_t t_req = t0;
+    for (;;) {
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+        if (sys_load32(&blk->stop) || now - t_req > (uint64_t)idle_ms * 100000u ||
+            now - t0 > (uint64_t)life_ms * 100000u)
+            break;
+        const uint64_t r = sys_load64(&blk->req_seq);
+        const uint64_t seq = (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)r) |
+                             ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(r >> 32)) << 32);
+        if (seq == last) {
+            __builtin_amdgcn_s_sleep(2);
+            continue;
+        }
+        // the request's fields were stored before req_seq (host release): the wave reads the
+        // block's request half in ONE round trip, a system-scope 8-byte load per lane (64 x 8 B
+        // covers the header and the query), and keeps it in LDS (S.q holds the query for the
+        // search; the header words go through readlane)
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        static_assert(offsetof(ServeBlock, q) + kServeMaxQuery <= 64 * 8, "the request half fits one load per lane");
+        const uint64_t* req = reinterpret_cast<const uint64_t*>(blk);
+        const uint64_t wv = sys_load64(req + lane);
+        auto hdr32 = [&](uint32_t byte_off) -> uint32_t {  // 4-byte header field at byte_off (< 512)
+            const uint64_t w = (uint64_t)__builtin_amdgcn_readlane((uint32_t)wv, byte_off >> 3) |
+                               ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(wv >> 32), byte_off >> 3) << 32);
+            return (uint32_t)(w >> (8 * (byte_off & 7)));
+        };
+        SearchParams P = P0;
+        P.thr = __uint_as_float(hdr32(offsetof(ServeBlock, thr)));
+        P.limit = hdr32(offsetof(ServeBlock, limit));
+        P.out_stride = P.limit;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) P.valid[i] = hdr32(offsetof(ServeBlock, valid) + 4 * i);
+        const uint32_t m = hdr32(offsetof(ServeBlock, m));
+        {  // the query's bytes to S.q (one code point per entry), lanes over the 8-byte words
+            constexpr uint32_t q0 = offsetof(ServeBlock, q);
+            uint8_t* raw = reinterpret_cast<uint8_t*>(S.surv_t);  // scratch: free until the search starts
+            reinterpret_cast<uint64_t*>(raw)[lane] = wv;
+            wave_sync();
+            const uint32_t mq = m == kQueryWildcard ? 0u : min(m, kServeMaxQuery);
+            for (uint32_t i = lane; i < mq; i += 64) S.q[i] = raw[q0 + i];
+            wave_sync();
+        }
+        if (lane == 0) __hip_atomic_store(count2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        wave_sync();
+        wave_query<1, false>(S, 0u, X, P, blk->q, blk->off, &blk->m, &blk->n, blk->keys, blk->scores, list2, count2,
+                             scratch, nullptr, nullptr, 0u, 1u, m);
+        const uint32_t routed = __hip_atomic_load(count2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0) {
+            __hip_atomic_store(&blk->status, routed ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // every result store before the number
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(&blk->done_seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        last = seq;
+        t_req = __builtin_amdgcn_s_memrealtime();
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_store(&blk->alive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // Tier 1a: the lean wave kernel over every query (qlist == nullptr), or over the heavy list.
 // DEFER: survivors spill to HBM for k_emit (the heavy launch always; the main one if kDeferEmit).
 // ONES: the heavy list's launch, which also takes cmin-1 queries (part_ones); the main launch
@@ -2972,6 +3058,12 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
     hipLaunchKernelGGL(k_fast, dim3(grid2), dim3(kFastThreads), 0, s, X, P, qnorm, off, qm, out_n, out_k, out_s,
                        (const uint32_t*)list2, (const uint32_t*)count2, glist, gcount, stats);
     dbg_check(s, "k_fast");
+    return hipGetLastError();
+}
+
+hipError_t launch_serve(const DevIndex& X, const SearchParams& P, ServeBlock* blk, DevStats* scratch,
+                        uint32_t* list2, uint32_t idle_ms, uint32_t life_ms, hipStream_t s) {
+    hipLaunchKernelGGL(k_serve, dim3(1), dim3(64), 0, s, X, P, blk, scratch, list2, idle_ms, life_ms);
     return hipGetLastError();
 }
 

@@ -209,6 +209,12 @@ class StringIndex:
     def gram_size(self) -> int:
         return _native.lib().ngsGramSize(self.handle)
 
+    def serve(self, enable: bool = True) -> None:
+        """ngsServe: single score()/search() calls through the persistent low-latency server."""
+        rc = _native.lib().ngsServe(self.handle, int(enable))
+        if rc:
+            raise RuntimeError(f"ngsServe failed: {rc}")
+
     def set_timing(self, enable: bool = True) -> None:
         _native.lib().ngsSetTiming(self.handle, int(enable))
 
