@@ -242,7 +242,7 @@ struct Context {
     uint32_t* d_k = nullptr;
     float* d_s = nullptr;
     uint32_t* d_pos = nullptr;  // [ncap + 1] packed offsets
-    uint32_t* d_pk = nullptr;   // [ocap] packed keys
+    uint32_t* d_pk = nullptr;   // [2 * ocap] packed keys, or (pointer mode) u64 result pointers
     float* d_ps = nullptr;      // [ocap] packed scores
     void* d_ptemp = nullptr;    // scan scratch
     size_t ptemp_bytes = 0;
@@ -712,7 +712,7 @@ bool ensure_outputs(Context& c, size_t B, size_t stride) {
         c.d_n = c.d_k = nullptr;
         c.d_s = nullptr;
         const size_t nb = std::max(B, c.ncap), ob = std::max(need, c.ocap);
-        if (!dev_alloc(&c.d_out, nb + 1 + 2 * ob) || !dev_alloc(&c.d_pos, nb + 1) || !dev_alloc(&c.d_pk, ob) ||
+        if (!dev_alloc(&c.d_out, nb + 1 + 2 * ob) || !dev_alloc(&c.d_pos, nb + 1) || !dev_alloc(&c.d_pk, 2 * ob) ||
             !dev_alloc(&c.d_ps, ob))
             return false;
         c.ptemp_bytes = pack_temp_bytes((uint32_t)nb);
@@ -951,16 +951,21 @@ struct HostChunk {
     const uint64_t* d_off = nullptr;
     uint32_t *d_n = nullptr, *d_k = nullptr;
     float* d_s = nullptr;
+    // pointer mode (pcs != 0): records go out as result pointers pbase + key_off[key] * pcs
+    uint64_t pbase = 0;
+    uint32_t pcs = 0;
 };
 
 // Queues chunk [q0, q0 + B) on context c: the queries packed into pinned staging, one H2D copy
 // (two for large chunks), the search kernels. Nothing waits.
 template <typename CharT>
 bool queue_host_chunk(Library& L, Replica& R, Context& c, const CharT* const* queries, uint32_t q0, uint32_t B,
-                      float thr, uint32_t Lm, HostChunk& h) {
+                      float thr, uint32_t Lm, HostChunk& h, uint64_t pbase) {
     constexpr size_t cs = sizeof(CharT);
     const size_t stride = Lm;
     h = HostChunk{};
+    h.pbase = pbase;
+    h.pcs = pbase ? (uint32_t)cs : 0u;
     h.c = &c;
     h.q0 = q0;
     h.B = B;
@@ -1021,7 +1026,8 @@ bool queue_host_chunk(Library& L, Replica& R, Context& c, const CharT* const* qu
 
 // Completes a queued chunk: waits, runs the general path, reads back exactly the results
 // (packed on the device for large chunks), fills the chunk's counts and hands its records to
-// `emit(keys, scores, n)`.
+// `emit(recs, scores, n, last)`: recs are u32 key ranks, or in pointer mode (h.pcs) u64 result
+// pointers.
 template <class Emit>
 bool finish_host_chunk(Library& L, Replica& R, HostChunk& h, uint32_t Lm, std::vector<uint32_t>& counts, bool last,
                        Emit&& emit) {
@@ -1049,14 +1055,22 @@ bool finish_host_chunk(Library& L, Replica& R, HostChunk& h, uint32_t Lm, std::v
             k.insert(k.end(), hk + (size_t)i * stride, hk + (size_t)i * stride + hn[i]);
             sc.insert(sc.end(), hs + (size_t)i * stride, hs + (size_t)i * stride + hn[i]);
         }
-        emit(k.data(), sc.data(), (uint32_t)k.size(), last);
+        if (h.pcs) {  // a few records: their pointers made here
+            const uint64_t* koff = L.host.key_off.data();
+            std::vector<uint64_t> ptr(k.size());
+            for (size_t i = 0; i < k.size(); ++i) ptr[i] = h.pbase + koff[k[i]] * h.pcs;
+            emit(static_cast<const void*>(ptr.data()), sc.data(), (uint32_t)k.size(), last);
+        } else {
+            emit(static_cast<const void*>(k.data()), sc.data(), (uint32_t)k.size(), last);
+        }
         return true;
     }
     // large batches: pack on the device (prefix sum of the counts, one copy per query), read
     // back the offsets, then exactly the packed records
+    uint64_t* pp = h.pcs ? reinterpret_cast<uint64_t*>(c.d_pk) : nullptr;
     if (!HIP_CHECK(hipMemsetAsync(c.d_n + B, 0, sizeof(uint32_t), c.stream)) ||
         !HIP_CHECK(launch_pack(c.d_n, c.d_k, c.d_s, B, (uint32_t)stride, c.d_pos, c.d_pk, c.d_ps, c.d_ptemp,
-                               c.ptemp_bytes, c.stream)) ||
+                               c.ptemp_bytes, c.stream, R.dev.key_off, h.pbase, h.pcs, pp)) ||
         !c.h_res.grow(sizeof(uint32_t) * (B + 1)) ||
         !HIP_CHECK(hipMemcpyAsync(c.h_res.p, c.d_pos, sizeof(uint32_t) * (B + 1), hipMemcpyDeviceToHost, c.stream)) ||
         !HIP_CHECK(hipStreamSynchronize(c.stream)))
@@ -1064,16 +1078,16 @@ bool finish_host_chunk(Library& L, Replica& R, HostChunk& h, uint32_t Lm, std::v
     ht.mark("pack + offsets back");
     const uint32_t total = c.h_res.as<uint32_t>()[B];
     for (uint32_t i = 0; i < B; ++i) counts[q0 + i] = c.h_res.as<uint32_t>()[i + 1] - c.h_res.as<uint32_t>()[i];
-    if (!c.h_res.grow(sizeof(uint32_t) * 2 * (size_t)total) ||
-        !HIP_CHECK(hipMemcpyAsync(c.h_res.p, c.d_pk, sizeof(uint32_t) * total, hipMemcpyDeviceToHost, c.stream)) ||
-        !HIP_CHECK(hipMemcpyAsync(c.h_res.as<uint32_t>() + total, c.d_ps, sizeof(float) * total, hipMemcpyDeviceToHost,
+    const size_t rb = (h.pcs ? sizeof(uint64_t) : sizeof(uint32_t)) * (size_t)total;  // record bytes
+    if (!c.h_res.grow(rb + sizeof(float) * (size_t)total) ||
+        !HIP_CHECK(hipMemcpyAsync(c.h_res.p, c.d_pk, rb, hipMemcpyDeviceToHost, c.stream)) ||
+        !HIP_CHECK(hipMemcpyAsync(c.h_res.as<uint8_t>() + rb, c.d_ps, sizeof(float) * total, hipMemcpyDeviceToHost,
                                   c.stream)) ||
         !HIP_CHECK(hipStreamSynchronize(c.stream)))
         return false;
     ht.mark("records back");
     // straight from the pinned buffer
-    const uint32_t* pk = c.h_res.as<uint32_t>();
-    emit(pk, reinterpret_cast<const float*>(pk + total), total, last);
+    emit(static_cast<const void*>(c.h_res.p), reinterpret_cast<const float*>(c.h_res.as<uint8_t>() + rb), total, last);
     ht.mark("emit");
     return true;
 }
@@ -1090,7 +1104,7 @@ constexpr uint32_t kPipeMinChunk = 8192;
 // each chunk's records, in query order, to emit(keys, scores, n).
 template <typename CharT, class Emit>
 bool host_search_chunks(Library& L, Replica& R, const CharT* const* queries, uint32_t nq, float thr, uint32_t Lm,
-                        std::vector<uint32_t>& counts, Emit&& emit) {
+                        std::vector<uint32_t>& counts, Emit&& emit, uint64_t pbase = 0) {
     counts.assign(nq, 0);
     if (Lm == 0 || nq == 0) return true;
     if (!HIP_CHECK(hipSetDevice(R.device))) return false;
@@ -1118,7 +1132,7 @@ bool host_search_chunks(Library& L, Replica& R, const CharT* const* queries, uin
         // queue chunk k, then complete chunk k - 1 while k runs
         if (k < n_chunks) {
             const uint32_t q0 = (uint32_t)(k * chunk), B = (uint32_t)std::min<size_t>(chunk, nq - q0);
-            ok = queue_host_chunk(L, R, *ctx[k & 1], queries, q0, B, thr, Lm, fl[k & 1]);
+            ok = queue_host_chunk(L, R, *ctx[k & 1], queries, q0, B, thr, Lm, fl[k & 1], pbase);
             if (!ok) break;
         }
         if (pending) ok = finish_host_chunk(L, R, fl[(k - 1) & 1], Lm, counts, k == n_chunks, emit);
@@ -1138,8 +1152,9 @@ bool host_search_one(Library& L, Replica& R, const CharT* const* queries, uint32
                      std::vector<uint32_t>& counts, std::vector<uint32_t>& keys, std::vector<float>& scores) {
     keys.clear();
     scores.clear();
-    return host_search_chunks(L, R, queries, nq, thr, Lm, counts, [&](const uint32_t* k, const float* sc, uint32_t n,
+    return host_search_chunks(L, R, queries, nq, thr, Lm, counts, [&](const void* recs, const float* sc, uint32_t n,
                                                                        bool) {
+        const uint32_t* k = static_cast<const uint32_t*>(recs);
         keys.insert(keys.end(), k, k + n);
         scores.insert(scores.end(), sc, sc + n);
     });
@@ -1334,38 +1349,30 @@ uint32_t batch_query(uint32_t handle, const CharT* const* queries, uint32_t nq, 
     const uint32_t Lm = effective_limit(*L, limit);
     const bool one_replica = L->reps.size() == 1 || nq / split_min() <= 1;
     if (one_replica && Lm && (uint64_t)nq * Lm <= kDirectMax && nq >= kSmallBatch) {
-        // marshalled as the chunks finish, straight into the caller's arrays: new[]'d at the
-        // batch's capacity (nq x limit entries; only the pages written are ever touched), each
-        // chunk's key pointers and scores filled from the pinned read-back while the next chunk's
-        // kernels run
-        // one chunk (the common case): the arrays at the exact size, filled from the pinned
-        // read-back; several chunks: at the batch's capacity (nq x limit entries; only the pages
-        // written are touched)
+        // marshalled as the chunks finish, straight into the caller's arrays. One chunk (the
+        // common case): the arrays at the exact size, filled from the pinned read-back; several
+        // chunks: at the batch's capacity (nq x limit entries; only the pages written are touched)
         CharT** res = nullptr;
         float* out_s = nullptr;
         size_t off = 0, cap = 0;
-        const char* base = L->host.key_bytes.data();
-        const uint64_t* koff = L->host.key_off.data();
+        // pointer mode: k_pack writes each record as its result pointer into the host key bytes
+        // (key_off gathered on the device), so marshalling is two parallel copies
+        const uint64_t pbase = (uint64_t)(uintptr_t)L->host.key_bytes.data();
+        static_assert(sizeof(CharT*) == sizeof(uint64_t), "result pointers are 64-bit");
         const bool ok = host_search_chunks(*L, *L->reps.front(), queries, nq, thr, Lm, cnt,
-                                           [&](const uint32_t* k, const float* sc, uint32_t n, bool last) {
+                                           [&](const void* recs, const float* sc, uint32_t n, bool last) {
             if (!res) {
                 cap = (off == 0 && last) ? std::max<size_t>(n, 1) : (size_t)nq * Lm;
                 res = new CharT*[cap];
                 out_s = scores ? new float[cap] : nullptr;
             }
+            const uint64_t* p = static_cast<const uint64_t*>(recs);
             parallel_ranges(n, size_t(1) << 16, [&](size_t a, size_t e) {
-                // key_off is gathered at random (80 MB at C3): memory-latency bound, so the
-                // gathers run kPrefetch entries ahead
-                constexpr size_t kPrefetch = 24;
-                for (size_t i = a; i < std::min(e, a + kPrefetch); ++i) __builtin_prefetch(koff + k[i]);
-                for (size_t i = a; i < e; ++i) {
-                    if (i + kPrefetch < e) __builtin_prefetch(koff + k[i + kPrefetch]);
-                    res[off + i] = reinterpret_cast<CharT*>(const_cast<char*>(base) + koff[k[i]] * sizeof(CharT));
-                    if (out_s) out_s[off + i] = sc[i];
-                }
+                std::memcpy(res + off + a, p + a, (e - a) * sizeof(uint64_t));
+                if (out_s) std::memcpy(out_s + off + a, sc + a, (e - a) * sizeof(float));
             });
             off += n;
-        });
+        }, pbase);
         if (ok && !res) {  // no chunk ran (cannot happen with nq >= kSmallBatch): empty arrays
             res = new CharT*[1];
             out_s = scores ? new float[1] : nullptr;

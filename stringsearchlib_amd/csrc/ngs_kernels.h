@@ -43,7 +43,8 @@ hipError_t launch_serve(const DevIndex& X, const SearchParams& P, ServeBlock* bl
 // pk / ps at pos[q]. The host then copies pos and the pos[B] packed records, not B * stride.
 size_t pack_temp_bytes(uint32_t B);
 hipError_t launch_pack(const uint32_t* n, const uint32_t* k, const float* s, uint32_t B, uint32_t stride,
-                       uint32_t* pos, uint32_t* pk, float* ps, void* temp, size_t temp_bytes, hipStream_t st);
+                       uint32_t* pos, uint32_t* pk, float* ps, void* temp, size_t temp_bytes, hipStream_t st,
+                       const uint64_t* koff = nullptr, uint64_t pbase = 0, uint32_t cs = 0, uint64_t* pp = nullptr);
 
 // Wildcard answer (nGramSearch.hpp:356-369): keys sorted by (weight desc, rank asc).
 hipError_t build_wildcard(const float* d_w, uint32_t n_keys, uint32_t* d_keys, float* d_scores, hipStream_t s);

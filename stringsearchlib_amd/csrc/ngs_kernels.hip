@@ -3067,17 +3067,23 @@ hipError_t launch_serve(const DevIndex& X, const SearchParams& P, ServeBlock* bl
     return hipGetLastError();
 }
 
-// one wave per query: its records to the packed arrays
+// one wave per query: its records to the packed arrays. With pp, each key goes out as the
+// caller's result pointer instead, pbase + key_off[key] * cs (the host image of the key bytes):
+// the random key_off gathers happen here, in HBM, not in the host's marshalling loop
 __global__ __launch_bounds__(256) void k_pack(const uint32_t* __restrict__ n, const uint32_t* __restrict__ k,
                                               const float* __restrict__ s, uint32_t B, uint32_t stride,
                                               const uint32_t* __restrict__ pos, uint32_t* __restrict__ pk,
-                                              float* __restrict__ ps) {
+                                              float* __restrict__ ps, const uint64_t* __restrict__ koff,
+                                              uint64_t pbase, uint32_t cs, uint64_t* __restrict__ pp) {
     const uint32_t q = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
     if (q >= B) return;
     const uint32_t c = n[q], o = pos[q];
     const size_t src = (size_t)q * stride;
     for (uint32_t i = lane; i < c; i += 64) {
-        pk[o + i] = k[src + i];
+        if (pp)
+            pp[o + i] = pbase + koff[k[src + i]] * cs;
+        else
+            pk[o + i] = k[src + i];
         ps[o + i] = s[src + i];
     }
 }
@@ -3089,10 +3095,12 @@ size_t pack_temp_bytes(uint32_t B) {
 }
 
 hipError_t launch_pack(const uint32_t* n, const uint32_t* k, const float* s, uint32_t B, uint32_t stride,
-                       uint32_t* pos, uint32_t* pk, float* ps, void* temp, size_t temp_bytes, hipStream_t st) {
+                       uint32_t* pos, uint32_t* pk, float* ps, void* temp, size_t temp_bytes, hipStream_t st,
+                       const uint64_t* koff, uint64_t pbase, uint32_t cs, uint64_t* pp) {
     hipError_t e = hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, n, pos, (int)B + 1, st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_pack, dim3((B + 3) / 4), dim3(256), 0, st, n, k, s, B, stride, pos, pk, ps);
+    hipLaunchKernelGGL(k_pack, dim3((B + 3) / 4), dim3(256), 0, st, n, k, s, B, stride, pos, pk, ps, koff, pbase, cs,
+                       pp);
     return hipGetLastError();
 }
 

@@ -2,6 +2,14 @@
 over the dispatches of that kernel with the largest grid (the main launch of each call), plus
 derived ratios.
 
+Durations come from the same dispatches' own timestamps in the counter CSVs (so the heavy or
+hand-over launches of the same kernel, which have smaller grids, never mix in). Normalisation
+(MI355X_MICROARCH.md, "Wave scheduling" and the PMC units row):
+- SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* count quad-cycles, summed over waves;
+- a wave64 VALU instruction issues over 2 cycles on its SIMD (32 lanes per cycle);
+- the effective clock is GRBM_GUI_ACTIVE / 8 (summed over the 8 XCDs) / kernel wall time;
+- 256 CUs x 4 SIMDs.
+
 usage: python tools/pmc_summary.py <dir with p*/.../run_counter_collection.csv> [kernel substring]
 """
 import csv
@@ -10,10 +18,15 @@ import os
 import sys
 from collections import defaultdict
 
+N_CU = 256
+N_SIMD = 4 * N_CU
+VALU_ISSUE_CYCLES = 2
+NOMINAL_GHZ = 2.4
+
 
 def main(root, kernel_substr="k_wave_lean"):
     per = defaultdict(lambda: defaultdict(float))
-    grid = {}
+    grid, span = {}, {}
     for f in sorted(glob.glob(os.path.join(root, "p*", "**", "run_counter_collection.csv"), recursive=True)):
         with open(f) as fh:
             for r in csv.DictReader(fh):
@@ -22,33 +35,48 @@ def main(root, kernel_substr="k_wave_lean"):
                 key = (f, r["Dispatch_Id"])
                 per[r["Counter_Name"]][key] += float(r["Counter_Value"])
                 grid[key] = int(r["Grid_Size"])
+                span[key] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
     gmax = max(grid.values(), default=0)
     out = {}
     for c, d in per.items():
         vals = [v for k, v in d.items() if grid[k] == gmax]
         if vals:
             out[c] = sum(vals) / len(vals)
-    dur = []
-    for f in sorted(glob.glob(os.path.join(root, "p*", "**", "run_kernel_trace.csv"), recursive=True)):
-        with open(f) as fh:
-            for r in csv.DictReader(fh):
-                if kernel_substr in r["Kernel_Name"] and int(r.get("Grid_Size", gmax) or gmax) == gmax:
-                    dur.append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
-    print(f"kernel {kernel_substr}, grid {gmax}, per dispatch:")
+    dur = [span[k] for k in span if grid[k] == gmax]
+    print(f"kernel {kernel_substr}, grid {gmax}, {len(dur)} dispatches over all passes, per dispatch:")
     for c in sorted(out):
-        print(f"{c:40s} {out[c]:.4g}")
-    if dur:
-        print(f"{'duration_ns (profiled, mean)':40s} {sum(dur)/len(dur):.4g}")
+        print(f"{c:44s} {out[c]:.4g}")
     g = out.get
+    t_ns = sum(dur) / len(dur) if dur else 0.0
+    if t_ns:
+        print(f"{'duration_ns (profiled, mean)':44s} {t_ns:.4g}")
+    # effective clock: GRBM_GUI_ACTIVE counts GPU-busy cycles summed over the 8 XCDs
+    ghz = g("GRBM_GUI_ACTIVE", 0) / 8 / t_ns if t_ns and g("GRBM_GUI_ACTIVE") else 0.0
+    if ghz:
+        print(f"{'effective clock GHz (GRBM_GUI_ACTIVE/8/wall)':44s} {ghz:.3f}")
+    else:
+        ghz = NOMINAL_GHZ
+        print(f"{'effective clock GHz (no GRBM pass: nominal)':44s} {ghz:.3f}")
+    cyc = t_ns * ghz  # shader cycles of the dispatch
     if g("SQ_LDS_IDX_ACTIVE"):
-        print(f"{'LDS bank-conflict share':40s} {g('SQ_LDS_BANK_CONFLICT', 0) / g('SQ_LDS_IDX_ACTIVE'):.3f}")
+        print(f"{'LDS bank-conflict share':44s} {g('SQ_LDS_BANK_CONFLICT', 0) / g('SQ_LDS_IDX_ACTIVE'):.3f}")
     if g("SQ_WAVE_CYCLES"):
         for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_LDS"):
             if g(k):
-                print(f"{k + ' / WAVE_CYCLES':40s} {g(k) / g('SQ_WAVE_CYCLES'):.3f}")
-    if g("SQ_BUSY_CYCLES") and g("SQ_ACTIVE_INST_VALU"):
-        print(f"{'VALU active / (busy cycles x 4 SIMD)':40s} "
-              f"{g('SQ_ACTIVE_INST_VALU') / (g('SQ_BUSY_CYCLES') * 4):.3f}")
+                print(f"{k + ' / WAVE_CYCLES':44s} {g(k) / g('SQ_WAVE_CYCLES'):.3f}")
+        if cyc:
+            print(f"{'mean resident waves per SIMD':44s} {g('SQ_WAVE_CYCLES') * 4 / (N_SIMD * cyc):.2f}")
+    if cyc and g("SQ_INSTS_VALU"):
+        share = g("SQ_INSTS_VALU") * VALU_ISSUE_CYCLES / (N_SIMD * cyc)
+        print(f"{'VALU issue share (2 cyc/instr, all SIMDs)':44s} {share:.3f}")
+    if cyc and g("SQ_INSTS_SALU"):
+        print(f"{'SALU instrs per CU-cycle':44s} {g('SQ_INSTS_SALU') / (N_CU * cyc):.3f}")
+    if cyc and g("SQ_LDS_IDX_ACTIVE"):
+        print(f"{'LDS_IDX_ACTIVE per CU-cycle':44s} {g('SQ_LDS_IDX_ACTIVE') / (N_CU * cyc):.3f}")
+    if g("SQ_WAVES"):
+        for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD"):
+            if g(k):
+                print(f"{k + ' per wave':44s} {g(k) / g('SQ_WAVES'):.4g}")
     return out
 
 
