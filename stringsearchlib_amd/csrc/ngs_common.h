@@ -46,7 +46,10 @@ constexpr uint32_t kFastMaxGrams = 255;  // u8 counts in the table slot
 constexpr uint32_t kMaxPartSpan = (1u << 24) - 2;  // 24-bit relative term id in the slot
 
 // bucket skip table: K <= kMaxBuckets term-id buckets of >= kMinBucketTerms terms each
-constexpr uint32_t kMaxBuckets = 256;
+#ifndef NGS_MAX_BUCKETS
+#define NGS_MAX_BUCKETS 256
+#endif
+constexpr uint32_t kMaxBuckets = NGS_MAX_BUCKETS;
 constexpr uint32_t kMinBucketTerms = 4096;
 constexpr uint64_t kDenseBucketLen = 16;          // dense lists: postings of the longest list per bucket
 constexpr uint64_t kSkipBudget = 512ull << 20;    // ... within this many bytes of skip table
@@ -139,6 +142,12 @@ constexpr bool kSketchLoose = NGS_SKETCH_LOOSE != 0;
 #endif
 #ifndef NGS_LEAN_G4
 #define NGS_LEAN_G4 0  // 1: tier-1a staging reads each list's chunk base from LDS (measured 1.5 % slower)
+#endif
+#ifndef NGS_RADIX_SELECT
+#define NGS_RADIX_SELECT 1  // top-L buffer refills by radix select (wave_select); 0: bitonic sort
+#endif
+#ifndef NGS_LEAN_STAGE_BATCH
+#define NGS_LEAN_STAGE_BATCH 0  // 1: tier-1a staging reads every round's lookups before its loads
 #endif
 #ifndef NGS_LEAN_DEFER_SKIP
 #define NGS_LEAN_DEFER_SKIP 0  // 1: tier 1a issues the next skip-table read after the part's loads (1 % slower)

@@ -970,11 +970,102 @@ __device__ __forceinline__ uint32_t wave_incl_max_scan(uint32_t v) {
     return v;
 }
 
-// Wave-local running top-L over the candidate buffer (same algorithm as flush()).
-// unique: no two records share a key (DevIndex.keys_unique): only the second pass runs.
+// OR of v over the wave (the inclusive-scan steps of wave_incl_scan; lane 63 holds the total)
+__device__ __forceinline__ uint32_t wave_or_u32(uint32_t v) {
+    v |= dpp_mov_rows<0x111, 0xf>(v);
+    v |= dpp_mov_rows<0x112, 0xf>(v);
+    v |= dpp_mov_rows<0x114, 0xf>(v);
+    v |= dpp_mov_rows<0x118, 0xf>(v);
+    v |= dpp_mov_rows<0x142, 0xa>(v);
+    v |= dpp_mov_rows<0x143, 0xc>(v);
+    return __builtin_amdgcn_readlane(v, 63);
+}
+
+// Radix select of the limit cutoff (hpp:397-401 keeps the first L of the ScoreComparer order):
+// the buffer's n >= L records (all distinct: DevIndex.keys_unique, one record per key) are
+// trimmed to the L smallest, unsorted, and tau becomes the L-th. The records sit in registers (4
+// per lane); each pass histograms one 8-bit digit of the records still tied with the L-th (a
+// 256-bin LDS histogram over the buffer's own first KB), taken just below the highest bit in
+// which those records differ (OR / AND-NOT reductions), so equal score bits cost no pass; the
+// boundary bin's prefix sum fixes 8 more bits of the L-th record, until one record is left. At
+// threshold 0 (thousands of equal-score survivors, C2) this replaces a 256-record bitonic sort
+// per buffer refill with ~3 histogram passes; the final order comes from one sort of the L.
 template <class SM>
+__device__ void wave_select(SM& S, uint32_t& cand_n, uint64_t& tau, uint32_t L) {
+    static_assert(kWaveCand == 256, "wave_select holds the buffer as 4 records per lane");
+    const uint32_t lane = lane_id();
+    const uint32_t n = min(cand_n, (uint32_t)kWaveCand);
+    uint64_t r[4];
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u) r[u] = lane + 64 * u < n ? S.cand()[lane + 64 * u] : kNoCand;
+    wave_sync();  // the buffer is free: its first KB holds the histogram
+    uint32_t* hist = reinterpret_cast<uint32_t*>(S.cand());
+    uint64_t pre = 0, pm = 0;  // bits of the L-th record fixed so far (mask pm)
+    uint32_t k = L;            // rank of the L-th record among the records matching pre
+    uint64_t kth = kNoCand;
+    for (;;) {
+        uint32_t o_lo = 0, o_hi = 0, z_lo = 0, z_hi = 0;  // OR of the matches and of their complements
+#pragma unroll
+        for (uint32_t u = 0; u < 4; ++u) {
+            if (lane + 64 * u < n && (r[u] & pm) == pre) {
+                o_lo |= (uint32_t)r[u];
+                o_hi |= (uint32_t)(r[u] >> 32);
+                z_lo |= ~(uint32_t)r[u];
+                z_hi |= ~(uint32_t)(r[u] >> 32);
+            }
+        }
+        const uint64_t o = ((uint64_t)wave_or_u32(o_hi) << 32) | wave_or_u32(o_lo);
+        const uint64_t a = ~(((uint64_t)wave_or_u32(z_hi) << 32) | wave_or_u32(z_lo));  // AND of the matches
+        const uint64_t d = o ^ a;  // bits in which the matching records differ
+        if (!d) {                  // one record left: the L-th
+            kth = o;
+            break;
+        }
+        const uint32_t top = 63u - (uint32_t)__clzll((long long)d);
+        const uint32_t sh = top >= 7u ? top - 7u : 0u;
+        const uint64_t above = top == 63u ? 0ull : ~((2ull << top) - 1ull);  // shared by every match
+        reinterpret_cast<uint4*>(hist)[lane] = make_uint4(0, 0, 0, 0);
+        wave_sync();
+#pragma unroll
+        for (uint32_t u = 0; u < 4; ++u)
+            if (lane + 64 * u < n && (r[u] & pm) == pre) atomicAdd(&hist[(uint32_t)(r[u] >> sh) & 255u], 1u);
+        wave_sync();
+        const uint4 h = reinterpret_cast<const uint4*>(hist)[lane];
+        const uint32_t e0 = h.x, e1 = e0 + h.y, e2 = e1 + h.z, e3 = e2 + h.w;
+        const uint32_t incl = wave_incl_scan(e3), excl = incl - e3;
+        const unsigned long long hit = __ballot(excl < k && k <= incl);  // the lane holding the boundary bin
+        const uint32_t src = (uint32_t)__ffsll((long long)hit) - 1u;
+        const uint32_t j = k <= excl + e0 ? 0u : k <= excl + e1 ? 1u : k <= excl + e2 ? 2u : 3u;
+        const uint32_t below = excl + (j == 0u ? 0u : j == 1u ? e0 : j == 2u ? e1 : e2);
+        const uint32_t b = 4u * src + __builtin_amdgcn_readlane(j, (int)src);
+        k -= __builtin_amdgcn_readlane(below, (int)src);
+        pre = (o & above) | ((uint64_t)b << sh);
+        pm = above | (0xFFull << sh);
+        wave_sync();  // the histogram is read before the next pass clears it
+    }
+    // the L smallest: every record <= the L-th (distinct records: exactly L of them)
+    uint32_t base = 0;
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u) {
+        const bool f = lane + 64 * u < n && r[u] <= kth;
+        const unsigned long long b = __ballot(f);
+        if (f) S.cand()[base + rank_below(b)] = r[u];
+        base += (uint32_t)__popcll(b);
+    }
+    wave_sync();
+    cand_n = L;
+    tau = kth;
+}
+
+// Wave-local running top-L over the candidate buffer (same algorithm as flush()), sorted.
+// unique: no two records share a key (DevIndex.keys_unique): only the second pass runs, after a
+// radix select has cut a buffer of more than L records to its L smallest (wave_select).
+// (RADIX: the deferred emit and merge kernels; the fused tier-1b kernel keeps the sort alone,
+// since the select's registers would push its calcScore out of line)
+template <bool RADIX = false, class SM>
 __device__ void wave_flush(SM& S, uint32_t& cand_n, uint64_t& tau, uint32_t L, bool unique = false) {
     const uint32_t lane = lane_id();
+    if (RADIX && NGS_RADIX_SELECT && unique && cand_n > L && L) wave_select(S, cand_n, tau, L);
     const uint32_t n = min(cand_n, (uint32_t)kWaveCand);
     const uint32_t P2 = next_pow2(max(n, 2u));
     for (uint32_t i = lane; i < P2; i += 64) {
@@ -1020,6 +1111,16 @@ __device__ void wave_flush(SM& S, uint32_t& cand_n, uint64_t& tau, uint32_t L, b
     wave_sync();
 }
 
+// The refill of a full buffer (and raised_cmin's settling of tau): only the L smallest records
+// and tau are needed, not their order, so distinct-key buffers take the radix select alone.
+template <bool RADIX = false, class SM>
+__device__ __forceinline__ void wave_trim(SM& S, uint32_t& cand_n, uint64_t& tau, uint32_t L, bool unique) {
+    if (RADIX && NGS_RADIX_SELECT && unique && cand_n >= L && L)
+        wave_select(S, cand_n, tau, L);
+    else
+        wave_flush(S, cand_n, tau, L, unique);
+}
+
 // (defined below)
 template <class SM>
 __device__ void wave_emit(SM& S, const DevIndex& X, const SearchParams& P, uint32_t m, uint32_t L,
@@ -1039,7 +1140,7 @@ __device__ uint32_t raised_cmin(SM& S, const DevIndex& X, const SearchParams& P,
                                 uint64_t& tau) {
     if (tau == kNoCand && cand_n + surv_n >= L) {  // full enough: settle tau now
         if (surv_n) wave_emit(S, X, P, m, L, sc_long, sc_short, surv_n, cand_n, tau);
-        if (tau == kNoCand && cand_n >= L) wave_flush(S, cand_n, tau, L, X.keys_unique != 0);
+        if (tau == kNoCand && cand_n >= L) wave_trim(S, cand_n, tau, L, X.keys_unique != 0);
     }
     if (tau == kNoCand) return cmin;
     const uint32_t lane = lane_id(), te = ~(uint32_t)(tau >> 32);
@@ -1076,7 +1177,7 @@ __device__ void wave_emit(SM& S, const DevIndex& X, const SearchParams& P, uint3
                 const uint32_t enc = pair_enc(kw, s, promo, X, S.q, 4u, m, P.valid);
                 rec = ((uint64_t)(~enc) << 32) | kw.x;
             }
-            if (cand_n + 64 > (uint32_t)kWaveCand) wave_flush(S, cand_n, tau, L, X.keys_unique != 0);
+            if (cand_n + 64 > (uint32_t)kWaveCand) wave_trim(S, cand_n, tau, L, X.keys_unique != 0);
             const bool want = rec < tau;
             const unsigned long long b = __ballot(want);
             if (want) S.cand()[cand_n + rank_below(b)] = rec;
@@ -2051,6 +2152,38 @@ __device__ __forceinline__ void lean_stage(WaveSmem<1, true>& S, gptr<uint4> pos
     vmask = 0;
     uint32_t lo = lane;  // opaque: chunk positions are made per round, not hoisted (and spilled)
     asm volatile("" : "+v"(lo));
+#if NGS_LEAN_STAGE_BATCH
+    // every round's list-start word, then every round's segtab entry, read before the first load
+    // goes out: two dependent LDS round trips per part instead of two per round (the words of
+    // rounds past mt are clear, their lookups harmless)
+    uint32_t idx[kDmaRounds];
+#pragma unroll
+    for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) {
+        const unsigned long long wd = S.lstart[r];
+        const uint32_t wlo = __builtin_amdgcn_readfirstlane((uint32_t)wd);
+        const uint32_t whi = __builtin_amdgcn_readfirstlane((uint32_t)(wd >> 32));
+        idx[r] = __builtin_amdgcn_mbcnt_hi(whi, __builtin_amdgcn_mbcnt_lo(wlo, below)) & 63u;
+        below += (uint32_t)__popc(wlo) + (uint32_t)__popc(whi);
+    }
+    uint2 segs[kDmaRounds];
+#pragma unroll
+    for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) segs[r] = S.segtab[0][idx[r]];
+#pragma unroll
+    for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) {
+        if (64 * r < mt) {
+            const uint32_t c = 64 * r + lo;
+            const bool ok = c < mt;
+            const uint2 seg = segs[r];
+            if (ok) v[r] = post4[seg.x + c];
+            const int y = (int)(seg.y & 0xFFFFu), z = (int)(seg.y >> 16);
+            const uint32_t lo_e = (uint32_t)min(max(y - (int)(4 * c), 0), 4);
+            const uint32_t hi_e = (uint32_t)min(max(z - (int)(4 * c), 0), 4);
+            const uint32_t bits = ((1u << hi_e) - 1u) & ~((1u << lo_e) - 1u);
+            vmask |= (ok ? bits : 0u) << (4 * r);
+        }
+    }
+    return;
+#endif
 #pragma unroll
     for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) {
         if (64 * r < mt) {
@@ -2524,6 +2657,7 @@ struct EmitSmem {
 // (the heavy list's k_emit measured 1.8 ms against 0.32 ms)
 constexpr uint32_t kEmitWaves = 1;
 
+template <bool RADIX>
 __device__ __forceinline__ void emit_query(EmitSmem& S, const uint32_t q, const bool heavy_launch, const DevIndex& X,
                                            const SearchParams& P, const uint8_t* __restrict__ qnorm,
                                            const uint64_t* __restrict__ qoff, const uint32_t* __restrict__ qm,
@@ -2580,7 +2714,7 @@ __device__ __forceinline__ void emit_query(EmitSmem& S, const uint32_t q, const 
             if (i < sn) term_pairs(X, t0, s, promo, tau, p, pe);  // p == t0 unless pruned
             uint64_t rec = kNoCand;
             if (p < pe) rec = ((uint64_t)(~pair_enc(k0, s, promo, X, S.q, 4u, m, P.valid)) << 32) | k0.x;
-            if (cand_n + 64 > (uint32_t)kWaveCand) wave_flush(S, cand_n, tau, L, X.keys_unique != 0);
+            if (cand_n + 64 > (uint32_t)kWaveCand) wave_trim<RADIX>(S, cand_n, tau, L, X.keys_unique != 0);
             const bool want = rec < tau;
             const unsigned long long bw = __ballot(want);
             if (want) S.cand()[cand_n + rank_below(bw)] = rec;
@@ -2620,7 +2754,7 @@ __device__ __forceinline__ void emit_query(EmitSmem& S, const uint32_t q, const 
                 const uint32_t enc = pair_enc(kw, s, promo, X, S.q, 4u, m, P.valid);
                 rec = ((uint64_t)(~enc) << 32) | kw.x;
             }
-            if (cand_n + 64 > (uint32_t)kWaveCand) wave_flush(S, cand_n, tau, L, X.keys_unique != 0);
+            if (cand_n + 64 > (uint32_t)kWaveCand) wave_trim<RADIX>(S, cand_n, tau, L, X.keys_unique != 0);
             const bool want = rec < tau;
             const unsigned long long bw = __ballot(want);
             if (want) S.cand()[cand_n + rank_below(bw)] = rec;
@@ -2629,7 +2763,7 @@ __device__ __forceinline__ void emit_query(EmitSmem& S, const uint32_t q, const 
         t = t_next;
         code = code_next;
     }
-    wave_flush(S, cand_n, tau, L, X.keys_unique != 0);
+    wave_flush<RADIX>(S, cand_n, tau, L, X.keys_unique != 0);
     const size_t ob = (size_t)q * P.out_stride;
     for (uint32_t i = lane; i < cand_n; i += 64) {
         const uint64_t r = S.cand()[i];
@@ -2643,7 +2777,9 @@ __device__ __forceinline__ void emit_query(EmitSmem& S, const uint32_t q, const 
     }
 }
 
-// every query (qlist == nullptr), or the heavy list grid-stride
+// every query (qlist == nullptr), or the heavy list grid-stride (RADIX: the heavy list's launch,
+// whose thousands of survivors per query refill the top-L buffer many times)
+template <bool RADIX>
 __global__ __launch_bounds__(64 * kEmitWaves) void k_emit(DevIndex X, SearchParams P, const uint8_t* __restrict__ qnorm,
                                                           const uint64_t* __restrict__ qoff,
                                                           const uint32_t* __restrict__ qm, uint32_t* __restrict__ out_n,
@@ -2655,12 +2791,12 @@ __global__ __launch_bounds__(64 * kEmitWaves) void k_emit(DevIndex X, SearchPara
     EmitSmem& S = SS[threadIdx.x >> 6];
     const uint32_t j0 = blockIdx.x * kEmitWaves + (threadIdx.x >> 6);
     if (!qlist) {
-        if (j0 < P.n_queries) emit_query(S, j0, false, X, P, qnorm, qoff, qm, out_n, out_k, out_s, stats);
+        if (j0 < P.n_queries) emit_query<RADIX>(S, j0, false, X, P, qnorm, qoff, qm, out_n, out_k, out_s, stats);
         return;
     }
     const uint32_t cnt = *qcount;
     for (uint32_t j = j0; j < cnt; j += gridDim.x * kEmitWaves) {
-        emit_query(S, qlist[j], true, X, P, qnorm, qoff, qm, out_n, out_k, out_s, stats);
+        emit_query<RADIX>(S, qlist[j], true, X, P, qnorm, qoff, qm, out_n, out_k, out_s, stats);
         wave_sync();
     }
 }
@@ -2685,14 +2821,14 @@ __global__ __launch_bounds__(64) void k_merge(DevIndex X, SearchParams P, const 
             const uint64_t* pr = P.prec + ((size_t)q * nsl + j) * L;
             for (uint32_t b = 0; b < nj; b += 64) {
                 const uint64_t rec = b + lane < nj ? pr[b + lane] : kNoCand;
-                if (cand_n + 64 > (uint32_t)kWaveCand) wave_flush(S, cand_n, tau, L, X.keys_unique != 0);
+                if (cand_n + 64 > (uint32_t)kWaveCand) wave_trim<true>(S, cand_n, tau, L, X.keys_unique != 0);
                 const bool want = rec < tau;
                 const unsigned long long bw = __ballot(want);
                 if (want) S.cand()[cand_n + rank_below(bw)] = rec;
                 cand_n += __popcll(bw);
             }
         }
-        wave_flush(S, cand_n, tau, L, X.keys_unique != 0);
+        wave_flush<true>(S, cand_n, tau, L, X.keys_unique != 0);
         const size_t ob = (size_t)q * P.out_stride;
         for (uint32_t k = lane; k < cand_n; k += 64) {
             const uint64_t r = S.cand()[k];
@@ -2977,7 +3113,7 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
                 hipLaunchKernelGGL((k_wave_lean<true, kLeanOnes>), dim3(gh), dim3(64), 0, side, X, PH, qnorm, off, qm, out_n,
                                    out_k, out_s, list2, count2, stats, fb2, fbc2, heavy, hcount);
                 dbg_check(side, "k_wave_lean (heavy list)");
-                hipLaunchKernelGGL(k_emit, dim3((gh + kEmitWaves - 1) / kEmitWaves), dim3(64 * kEmitWaves), 0, side,
+                hipLaunchKernelGGL(k_emit<true>, dim3((gh + kEmitWaves - 1) / kEmitWaves), dim3(64 * kEmitWaves), 0, side,
                                    X, PH, qnorm, off, qm, out_n, out_k, out_s, stats, heavy, hcount);
                 dbg_check(side, "k_emit (heavy list)");
                 hipLaunchKernelGGL(k_wave<1>, dim3(g1s), dim3(64), 0, side, X, PHO, qnorm, off, qm, out_n, out_k,
@@ -3014,7 +3150,7 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
             if ((e = hipEventRecord(join2, side2)) != hipSuccess) return e;
             if (!kMainFirst) main_lean();
             if (kDeferEmit) {
-                hipLaunchKernelGGL(k_emit, dim3((P.n_queries + kEmitWaves - 1) / kEmitWaves), dim3(64 * kEmitWaves), 0,
+                hipLaunchKernelGGL(k_emit<false>, dim3((P.n_queries + kEmitWaves - 1) / kEmitWaves), dim3(64 * kEmitWaves), 0,
                                    s, X, P, qnorm, off, qm, out_n, out_k, out_s, stats, (const uint32_t*)nullptr,
                                    (const uint32_t*)nullptr);
                 dbg_check(s, "k_emit");

@@ -49,6 +49,7 @@ def main(src, cfg, kernel="k_wave_lean"):
         "source": os.path.relpath(src, ROOT),
     }
     dst = os.path.join(ROOT, "profiles", f"pmc_{cfg}.json")
+    os.makedirs(os.path.dirname(dst), exist_ok=True)
     with open(dst, "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out))
