@@ -637,13 +637,15 @@ bool upload(Library& L, const std::vector<int>& devs) {
     return true;
 }
 
-// Survivor slots per query of tier 1a (d_est / d_esc, 5 bytes each): the wide cap only where a
-// typical query can be counted at cmin 1 (part_ones: thousands of one-hit survivors at C2's
-// threshold 0), i.e. thr <= 1/8 (queries of >= 8 grams), and for batches up to kEmitWideBatch:
-// 1.25 GiB per context at 65,536 queries. Above thr 1/8 only queries of < 8 grams can reach
-// cmin 1, and those of them with more survivors than kEmitCap go to tier 1b.
+// Survivor slots per query of tier 1a (d_est / d_esc, 5 bytes each): the wide cap for batches
+// up to kEmitWideBatch, at every threshold: 1.25 GiB per context at 65,536 queries (2.5 GiB at
+// C5's 131,072; two contexts when two batches are in flight). A query with more survivors than
+// its slots is handed to tier 1b, and large libraries have them at any threshold: sizing the
+// cap by threshold (wide only at thr <= 1/8) handed 26,594 C4 and 7,871 C5 queries per batch
+// to tier 1b (C4 420 -> 452 ms, C5 20.3 -> 21.7 ms per batch, profiles/r03_s4_ab_ecap.txt).
 uint32_t emit_cap(size_t B, float thr) {
-    return (thr <= 0.125f && B <= kEmitWideBatch) ? std::max(kEmitCap, kEmitCapWide) : kEmitCap;
+    (void)thr;
+    return B <= kEmitWideBatch ? std::max(kEmitCap, kEmitCapWide) : kEmitCap;
 }
 
 bool ensure_queries(Context& c, size_t B, size_t bytes, float thr) {
