@@ -486,18 +486,36 @@ bool upload_replica(Library& L, Replica& R, bool keys_unique, bool first) {
     uint2* tk;
     float *wild_w, *wild_score;
     // from here on the replica's destructor frees what was allocated
+    PhaseTimer pt;
     bool ok = dev_upload(&term_off, H.term_off, R.owned) && dev_upload(&term_bytes, H.term_bytes, R.owned, 4) /* whole dwords */ &&
               dev_upload(&tk_off, H.tk_off, R.owned) && dev_upload(&tk, H.tk, R.owned) &&
               dev_upload(&key_off, H.key_off, R.owned) && dev_upload(&key_bytes, kb, R.owned) &&
               dev_upload(&wild_w, H.wild_w, R.owned);
     if (!ok) return false;
+    pt.mark("replica: arrays to HBM");
     bool dev_built = false;
     if (!H.grams_built) {
-        // the gram CSR and skip table from the terms now in HBM (ngs_build.hip); on failure the
-        // host builds them
+        // the gram CSR and skip table from the terms now in HBM (ngs_build.hip); dictionary
+        // indexes first find their distinct gram keys there and the host lays out the lookup table
+        // from them (the first replica; the others reuse it). On failure the host builds them.
         DeviceGrams dg;
         const auto t0 = std::chrono::steady_clock::now();
-        const hipError_t e = build_grams_device(term_off, term_bytes, H.n_short, H.n_terms, dg);
+        hipError_t e = hipSuccess;
+        uint64_t* dict = nullptr;
+        if (H.gram_mode == 1) {
+            if (first) {
+                std::vector<uint64_t> keys;
+                e = gram_keys_device(term_off, term_bytes, H.n_short, H.n_terms, H.csize, H.gsz, keys);
+                if (e == hipSuccess) set_gram_dict(H, std::move(keys));
+            }
+            if (e == hipSuccess) e = hipMalloc(&dict, sizeof(uint64_t) * std::max<size_t>(H.gram_keys.size(), 1));
+            if (e == hipSuccess && !H.gram_keys.empty())
+                e = hipMemcpy(dict, H.gram_keys.data(), sizeof(uint64_t) * H.gram_keys.size(), hipMemcpyHostToDevice);
+        }
+        if (e == hipSuccess)
+            e = build_grams_device(term_off, term_bytes, H.n_short, H.n_terms, dg, dict, (uint32_t)H.gram_keys.size(),
+                                   H.csize, H.gsz);
+        if (dict) (void)hipFree(dict);
         if (std::getenv("NGS_BUILD_TIMING"))
             std::fprintf(stderr, "[ngs build] %-22s %8.3f s\n", "gram CSR + skip (GPU)",
                          std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
@@ -522,7 +540,7 @@ bool upload_replica(Library& L, Replica& R, bool keys_unique, bool first) {
             if (!H.grams_built) return false;
         }
     }
-    if (!dev_built)  // host-built gram CSR (dictionary indexes, NGS_HOST_GRAMS, device-build failure)
+    if (!dev_built)  // host-built gram CSR (NGS_HOST_GRAMS, device-build failure)
         ok = dev_upload(&gram_off, H.gram_off, R.owned) && dev_upload(&post, H.post, R.owned, 4) /* k_wave stages whole 16-byte chunks */ &&
              dev_upload(&gram_row, H.gram_row, R.owned) && dev_upload(&skip, H.skip, R.owned);
     if (!ok) return false;
@@ -543,6 +561,7 @@ bool upload_replica(Library& L, Replica& R, bool keys_unique, bool first) {
     R.owned.push_back(wild_key);
     if (!dev_alloc(&wild_score, H.n_keys)) return false;
     R.owned.push_back(wild_score);
+    pt.mark("replica: gram CSR");
     if (!HIP_CHECK(build_wildcard(wild_w, H.n_keys, wild_key, wild_score, nullptr))) return false;
     X.gram_off = gram_off;
     X.post = post;
@@ -559,7 +578,9 @@ bool upload_replica(Library& L, Replica& R, bool keys_unique, bool first) {
     X.wild_key = wild_key;
     X.wild_score = wild_score;
     // the build's null-stream work completes before any search stream (non-blocking) reads it
-    return HIP_CHECK(hipDeviceSynchronize());
+    const bool synced = HIP_CHECK(hipDeviceSynchronize());
+    pt.mark("replica: wildcard answer");
+    return synced;
 }
 
 // The device copies are authoritative for the search; keep only what marshalling needs.
@@ -575,12 +596,14 @@ void free_uploaded(HostIndex& H) {
     std::vector<float>().swap(H.wild_w);
     std::vector<uint64_t>().swap(H.ghash_key);
     std::vector<uint32_t>().swap(H.ghash_val);
+    std::vector<uint64_t>().swap(H.gram_keys);
 }
 
 // One replica per device in `devs` (repeats allowed: several replicas on one device split a batch
 // like several devices do, which the one-GPU tests use).
 bool upload(Library& L, const std::vector<int>& devs) {
     const HostIndex& H = L.host;
+    PhaseTimer pt;
     bool keys_unique = true;
     {
         std::vector<uint8_t> seen(H.n_keys, 0);
@@ -615,6 +638,7 @@ bool upload(Library& L, const std::vector<int>& devs) {
         std::memcpy(&w, &kw.y, sizeof w);
         if (w > L.w_max) L.w_max = w;  // NaN weights score +0 (pair_enc) and never raise the bound
     }
+    pt.mark("upload: index shape checks");
     for (int d : devs) {
         L.reps.push_back(std::make_unique<Replica>());
         L.reps.back()->device = d;
@@ -634,6 +658,7 @@ bool upload(Library& L, const std::vector<int>& devs) {
     }
     L.device = devs.front();
     free_uploaded(L.host);
+    pt.mark("upload: replicas placed");
     return true;
 }
 
@@ -1422,7 +1447,9 @@ uint32_t new_library(Build&& build) {
         devs.push_back(dev);
     }
     (void)hipSetDevice(devs.front());  // the build's device kernels run on the first replica's device
+    PhaseTimer pt;
     build(L->host);
+    pt.mark("build (intern + layout)");
     if (L->host.indexed && !upload(*L, devs)) {
         std::fprintf(stderr, "ngram_search: indexN could not place the index on a GPU\n");
         return 0;
@@ -1964,8 +1991,7 @@ NGS_API uint32_t ngsLoadIndex(const char* path) {
     H.indexed = true;
     H.grams_built = false;
     const uint32_t handle = new_library([&](HostIndex& dst) {
-        dst = std::move(H);
-        if (dst.gram_mode == 1) build_grams_host(dst);  // dictionary indexes: the gram CSR on the host
+        dst = std::move(H);  // the gram CSR (and a dictionary index's gram table) built at upload
     });
     if (handle) {
         std::shared_lock<std::shared_mutex> lk(g_lock);

@@ -13,17 +13,6 @@
 namespace ngs {
 namespace {
 
-// NGS_BUILD_TIMING=1 prints the host build phases to stderr
-struct PhaseTimer {
-    bool on = std::getenv("NGS_BUILD_TIMING") != nullptr;
-    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
-    void mark(const char* what) {
-        if (!on) return;
-        const auto n = std::chrono::steady_clock::now();
-        std::fprintf(stderr, "[ngs build] %-22s %8.3f s\n", what, std::chrono::duration<double>(n - t).count());
-        t = n;
-    }
-};
 
 // nGramSearch.h:307-313
 constexpr char kDefaultValid[] = ".%$ @0123456789abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ";
@@ -230,15 +219,12 @@ static void build_grams_impl(HostIndex& ix, unsigned threads, PhaseTimer& pt) {
         sets.clear();
         std::sort(all.begin(), all.end());
         all.erase(std::unique(all.begin(), all.end()), all.end());
-        dict.init(all.size() + 1);
-        for (uint32_t i = 0; i < all.size(); ++i) dict.insert(all[i]);
-        for (size_t i = 0; i < dict.key.size(); ++i)
-            if (dict.key[i] != ~0ull)
-                dict.val[i] = (uint32_t)(std::lower_bound(all.begin(), all.end(), dict.key[i]) - all.begin());
-        nspace = (uint32_t)all.size();
-        ix.ghash_key = dict.key;
-        ix.ghash_val = dict.val;
-        ix.ghash_bits = dict.bits;
+        set_gram_dict(ix, std::move(all));
+        nspace = (uint32_t)ix.gram_keys.size();
+        dict.key = ix.ghash_key;
+        dict.val = ix.ghash_val;
+        dict.bits = ix.ghash_bits;
+        dict.n = nspace;
     }
     // distinct grams of one long term (ngrams[h].insert(id) deduplicates per term, hpp:13-21)
     auto grams_of = [&](uint32_t id, std::vector<uint32_t>& gv) -> uint32_t {
@@ -359,7 +345,7 @@ static void build_impl(HostIndex& ix, const CharT* const* words, uint64_t size, 
             pt.mark("intern + CSR (GPU)");
             ix.indexed = true;  // hpp:45
             ix.grams_built = false;
-            if (ix.gram_mode == 0 && !std::getenv("NGS_HOST_GRAMS")) return;
+            if (!std::getenv("NGS_HOST_GRAMS")) return;  // the GPU builds them at upload (ngs_build.hip)
             build_grams_impl<CharT>(ix, threads, pt);
             return;
         }
@@ -510,11 +496,25 @@ static void build_impl(HostIndex& ix, const CharT* const* words, uint64_t size, 
 
     pt.mark("term->key CSR");
     ix.indexed = true;                                                    // hpp:45
-    // narrow 3-grams: the GPU builds the gram CSR and the skip table at upload (ngs_build.hip)
-    // unless NGS_HOST_GRAMS is set; every other shape builds them here
+    // the GPU builds the gram CSR, the gram dictionary and the skip table at upload
+    // (ngs_build.hip) unless NGS_HOST_GRAMS is set
     ix.grams_built = false;
-    if (ix.gram_mode == 0 && !std::getenv("NGS_HOST_GRAMS")) return;
+    if (!std::getenv("NGS_HOST_GRAMS")) return;
     build_grams_impl<CharT>(ix, threads, pt);
+}
+
+void set_gram_dict(HostIndex& ix, std::vector<uint64_t> sorted_keys) {
+    U64Map dict;
+    dict.init(sorted_keys.size() + 1);
+    for (uint64_t k : sorted_keys) dict.insert(k);  // ascending: the table layout is a function of the key set
+    for (size_t i = 0; i < dict.key.size(); ++i)
+        if (dict.key[i] != ~0ull)
+            dict.val[i] = (uint32_t)(std::lower_bound(sorted_keys.begin(), sorted_keys.end(), dict.key[i]) -
+                                     sorted_keys.begin());
+    ix.ghash_key = std::move(dict.key);
+    ix.ghash_val = std::move(dict.val);
+    ix.ghash_bits = dict.bits;
+    ix.gram_keys = std::move(sorted_keys);
 }
 
 void build_grams_host(HostIndex& ix, unsigned threads) {

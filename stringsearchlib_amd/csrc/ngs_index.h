@@ -10,13 +10,28 @@
 //   gram CSR   21-bit gram code -> sorted long-term ids (ngrams, nGramSearch.h:296)
 #pragma once
 
+#include <chrono>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <mutex>
 #include <vector>
 
 #include "ngs_common.h"
 
 namespace ngs {
+
+// NGS_BUILD_TIMING=1 prints the index build's phases (seconds since the previous mark) to stderr
+struct PhaseTimer {
+    bool on = std::getenv("NGS_BUILD_TIMING") != nullptr;
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    void mark(const char* what) {
+        if (!on) return;
+        const auto n = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[ngs build] %-26s %8.3f s\n", what, std::chrono::duration<double>(n - t).count());
+        t = n;
+    }
+};
 
 struct HostIndex {
     bool indexed = false;                   // nGramSearch.h:301
@@ -26,6 +41,7 @@ struct HostIndex {
     // 0: gram = 21-bit code of 3 ASCII bytes, direct-indexed; 1: gram dictionary (ghash)
     uint32_t gram_mode = 0;
     uint32_t short_term_len = 6, short_query_len = 9, full_scan_len = 3;  // 2g, 3g, g
+    std::vector<uint64_t> gram_keys;        // dictionary mode: the distinct gram keys, ascending (id = rank)
     std::vector<uint64_t> ghash_key;        // dictionary mode: open addressing, ~0 = empty
     std::vector<uint32_t> ghash_val;        // -> gram id (CSR row of gram_off)
     uint32_t ghash_bits = 0;
@@ -59,6 +75,11 @@ void build_index_w(HostIndex& ix, const uint32_t* const* words, uint64_t size, u
 // The gram CSR and skip table of an index whose terms are laid out (grams_built == false): the
 // host fallback of the device build.
 void build_grams_host(HostIndex& ix, unsigned threads = 0);
+
+// Dictionary mode: the gram ids of the sorted distinct keys (id = rank) and the open-addressing
+// table the device looks them up in (ghash_key / ghash_val / ghash_bits), as build_grams_impl
+// makes them; the device build (ngs_build.hip) computes the keys and hands them here.
+void set_gram_dict(HostIndex& ix, std::vector<uint64_t> sorted_keys);
 
 // Wildcard answer: keys sorted by (wild_w desc, rank asc).
 void wildcard_order(const HostIndex& ix, std::vector<uint32_t>& keys, std::vector<float>& scores);

@@ -448,6 +448,7 @@ hipError_t intern_impl(HostIndex& ix, const CharT* const* words, uint64_t size, 
     });
     // a row's head word past size cannot exist; woff needs entries up to nrows * rowSize + 1
     woff.resize(nrows * rowSize + 1, chars);
+    PhaseTimer pt;
 
     Arena A;
     Temp tmp;
@@ -475,6 +476,7 @@ hipError_t intern_impl(HostIndex& ix, const CharT* const* words, uint64_t size, 
         TRY(A.get(&d_w, size));
         TRY(hipMemcpy(d_w, weight, size * sizeof(float), hipMemcpyHostToDevice));
     }
+    pt.mark("intern: blob to HBM");
     std::vector<uint8_t>().swap(isnull);
     std::vector<CharT>().swap(blob);
     TRY(hipMemset(d_rowany, 0, nrows));
@@ -660,6 +662,7 @@ hipError_t intern_impl(HostIndex& ix, const CharT* const* words, uint64_t size, 
     if (err) return hipErrorNotSupported;  // hash collision or NaN weight: the host build decides
     TRY(hipMemcpy(&n_short, d_nshort, sizeof(uint32_t), hipMemcpyDeviceToHost));
 
+    pt.mark("intern: GPU phases");
     // ---- 6. to the host index ----
     ix.n_terms = n_terms;
     ix.n_short = n_short;
@@ -671,6 +674,7 @@ hipError_t intern_impl(HostIndex& ix, const CharT* const* words, uint64_t size, 
     TRY(download(ix.key_off, d_koff, (size_t)n_keys + 1));
     TRY(download(ix.key_bytes, reinterpret_cast<const char*>(d_kbytes), kchars * cs));
     TRY(download(ix.wild_w, d_wild, n_keys));
+    pt.mark("intern: arrays to host");
     return hipSuccess;
 }
 

@@ -370,7 +370,7 @@ struct FastSmem {
     uint32_t btot[kMaxBuckets];    // postings per term-id bucket
     uint2 part[kMaxBuckets];       // parts: bucket range [x, y & 0x7fffffff), y >> 31 = oversized
     uint32_t pre[260];             // segment prefix sums
-    uint8_t q[264];
+    uint32_t q[264];               // the normalised query, one character (byte or code point) per entry
     uint8_t peq[256];              // Myers match masks of the query (short search)
     uint64_t tau;                  // records >= tau cannot enter the top-L
     uint64_t p_left;
@@ -450,7 +450,7 @@ __device__ __forceinline__ bool emit_pending(EmitState& st, FastSmem& S, const D
                                              uint32_t m, const uint32_t* valid) {
     while (st.p < st.pe) {
         const uint2 kw = X.tk[st.p];
-        const uint32_t enc = pair_enc(kw, st.s, st.promo, X, S.q, 1u, m, valid);
+        const uint32_t enc = pair_enc(kw, st.s, st.promo, X, S.q, 4u, m, valid);
         const uint64_t rec = ((uint64_t)(~enc) << 32) | kw.x;
         if (rec < tau) {
             const uint32_t idx = atomicAdd(&S.cand_n, 1u);
@@ -621,15 +621,17 @@ __device__ void fast_one(const uint32_t q, FastSmem& S, const DevIndex& X, const
         if (tid == 0) out_n[q] = 0;
         return;
     }
-    // tier 2 handles indexN libraries (3-grams of bytes) only; indexG / indexW go to the general path
-    if (m <= kFullScanQueryLen || m - 2 > kFastMaxGrams || L > kFastMaxLimit || X.gram_mode != 0) {
+    // every index shape: grams of g characters (bytes or code points), looked up by gram_at (the
+    // 21-bit code of indexN, the dictionary of indexG / indexW); the full-library scan (m <= g)
+    // and what exceeds the block's tables go to the general path
+    if (m <= X.full_scan_len || m - X.gsz + 1 > kFastMaxGrams || L > kFastMaxLimit) {
         if (tid == 0) glist[atomicAdd(gcount, 1u)] = q;  // library-wide path
         return;
     }
-    const uint32_t n = m - 2;
+    const uint32_t n = m - X.gsz + 1;
     const uint32_t n_long = X.n_terms - X.n_short;
     const uint8_t* qg = qnorm + qoff[q];
-    for (uint32_t i = tid; i < m; i += kFastThreads) S.q[i] = qg[i];
+    for (uint32_t i = tid; i < m; i += kFastThreads) S.q[i] = char_at(qg, i, X.csize);
     for (uint32_t i = tid; i < (uint32_t)kTableSlots; i += kFastThreads) S.table[i] = 0;
     if (tid == 0) {
         S.cand_n = 0;
@@ -644,11 +646,11 @@ __device__ void fast_one(const uint32_t q, FastSmem& S, const DevIndex& X, const
     uint32_t surv = 0;  // terms of this thread that passed the threshold (stats only)
 
     // ---- searchShort over shortLib (nGramSearch.hpp:262-270), 4 <= m < 9 ----
-    if (m < kShortQueryLen && X.n_short) {
+    if (m < X.short_query_len && X.n_short) {
         uint32_t qc[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) qc[i] = (uint32_t)i < m ? S.q[i] : 0;
-        build_peq(S.peq, [&](uint32_t i) { return (uint32_t)S.q[i]; }, m, tid, kFastThreads);
+        build_peq(S.peq, [&](uint32_t i) { return S.q[i]; }, m, tid, kFastThreads);
         __syncthreads();
         uint32_t t = tid;
         const float fm = (float)m;
@@ -670,10 +672,7 @@ __device__ void fast_one(const uint32_t q, FastSmem& S, const DevIndex& X, const
     STAMP(1);
     // ---- searchLong (nGramSearch.hpp:278-301) ----
     // distinct grams with multiplicity
-    if (tid < n) {
-        const uint32_t c0 = S.q[tid], c1 = S.q[tid + 1], c2 = S.q[tid + 2];
-        S.g_code[tid] = ((c0 | c1 | c2) & 0x80u) ? 0xFFFFFFFFu : (c0 << 14) | (c1 << 7) | c2;
-    }
+    if (tid < n) S.g_code[tid] = gram_at(X, [&](uint32_t i) { return S.q[i]; }, tid);  // UINT32_MAX: no list
     if (tid < kMaxBuckets) S.btot[tid] = 0;
     __syncthreads();
     uint64_t my_len = 0;

@@ -94,6 +94,17 @@ def test_c4_full_wide_g2_rowsize4():
     ref = oracle_batch_w(oh, [qs[i] for i in sample], cfg["threshold"], cfg["limit"])
     for i, r in zip(sample, ref):
         assert_same(got[i], r, f"C4 q#{i} {bytes(qs[i])!r}")
+    # limit 500: tier 2 (k_fast) on the dictionary-mode index, not the library-wide general path
+    wide500 = [qs[i] for i in sample[:24]]
+    L.ngsSetTiming(h, 1)
+    got500 = gpu_batch_w(h, wide500, cfg["threshold"], 500)
+    st = _native.NgsStats()
+    L.ngsLastStats(h, C.byref(st))
+    assert st.tier2_queries > 0 and st.general_queries == 0, (st.tier2_queries, st.general_queries)
+    ref500 = oracle_batch_w(oh, wide500, cfg["threshold"], 500)
+    for j, (g500, r) in enumerate(zip(got500, ref500)):
+        check_properties(g500, 500, f"C4 limit 500 q#{j}")
+        assert_same(g500, r, f"C4 limit 500 q#{j}")
     lib_g().ngog_free(oh)
     L.dispose(h)
     corpus4.free()

@@ -119,6 +119,59 @@ def test_narrow_gram_size_parity(g):
     gi.dispose()
 
 
+@pytest.mark.parametrize("g", [1, 2, 3])
+def test_wide_tier2_limit_500_and_long_queries(g):
+    """Tier 2 (k_fast) on dictionary-mode indexes: limits of 129..1024 and queries of 64..255
+    grams are taken by k_fast (tier2_queries) instead of the library-wide general path, exact
+    against the generic oracle; queries past 255 grams still go to the general path."""
+    rng = random.Random(zlib.crc32(f"tier2w{g}".encode()))
+    words, wts = _shape(wide_corpus(rng, 3000, 2, 6, 24), rng)
+    gi = ssl.WideStringIndex(words, 2, wts, gram_size=g)
+    gi.set_timing(True)  # per-call statistics (last_stats)
+    oi = OracleIndexG(words, 2, wts, g=g, wide=True)
+    keys = [w for w in words[::2] if w and w.strip()]
+    qs = [q for q in wide_queries(rng, keys, 64) if isinstance(q, str) and len(q.strip()) > 3 * g + 2]
+    for thr, limit in [(0.0, 500), (0.2, 1024), (0.4, 129)]:
+        got = gi.score_batch(qs, thr, limit)
+        st = gi.last_stats()
+        assert st["tier2_queries"] > 0 and st["general_queries"] == 0, (thr, limit, st)
+        for q, r in zip(qs, got):
+            assert_exact(r, oi.score(q, thr, limit), f"tier2 g={g} q={q!r} thr={thr} limit={limit}")
+    long_qs = []
+    for i in range(12):
+        src = rng.choice(keys)
+        long_qs.append(((src + " ") * (300 // (len(src) + 1) + 1))[: 80 + 15 * i])  # 80..245 characters
+    got = gi.score_batch(long_qs, 0.1, 100)
+    st = gi.last_stats()
+    assert st["tier2_queries"] == len(long_qs) and st["general_queries"] == 0, st
+    for q, r in zip(long_qs, got):
+        assert_exact(r, oi.score(q, 0.1, 100), f"tier2 long g={g} len={len(q)}")
+    over = [(keys[0] + " ") * 40][:1]  # > 255 grams: the general path
+    over = [over[0][: 256 + g + 4]]
+    gi.score_batch(over, 0.1, 100)
+    assert gi.last_stats()["general_queries"] == 1
+    assert_exact(gi.score_batch(over, 0.1, 100)[0], oi.score(over[0], 0.1, 100), "tier2 over")
+    gi.dispose()
+
+
+@pytest.mark.parametrize("g", [1, 2])
+def test_narrow_gram_size_tier2(g):
+    """k_fast on narrow indexG libraries (dictionary of 1- or 2-byte grams) at limit 500."""
+    rng = random.Random(70 + g)
+    words, wts, _ = ssl.synth.gen_corpus(5000, seed=10 + g, min_len=4, span=20, row_size=1)
+    gi = ssl.StringIndex(words, 1, wts, gram_size=g)
+    gi.set_timing(True)
+    oi = OracleIndexG(words, 1, wts, g=g)
+    keys = [w for w in words if w]
+    qs = [rng.choice(keys) for _ in range(40)] + [keys[1] + b" " + keys[2] for _ in range(4)]
+    got = gi.score_batch(qs, 0.3, 500)
+    st = gi.last_stats()
+    assert st["tier2_queries"] == len(qs) and st["general_queries"] == 0, st
+    for q, r in zip(qs, got):
+        assert_exact(r, oi.score(q, 0.3, 500), f"narrow tier2 g={g} q={q!r}")
+    gi.dispose()
+
+
 def test_skewed_wide_lists_several_parts():
     # a 5-symbol alphabet of CJK characters: long lists split into several term-id parts
     rng = random.Random(77)
