@@ -668,12 +668,9 @@ bool upload(Library& L, const std::vector<int>& devs) {
 // its slots is handed to tier 1b, and large libraries have them at any threshold: sizing the
 // cap by threshold (wide only at thr <= 1/8) handed 26,594 C4 and 7,871 C5 queries per batch
 // to tier 1b (C4 420 -> 452 ms, C5 20.3 -> 21.7 ms per batch, profiles/r03_s4_ab_ecap.txt).
-uint32_t emit_cap(size_t B, float thr) {
-    (void)thr;
-    return B <= kEmitWideBatch ? std::max(kEmitCap, kEmitCapWide) : kEmitCap;
-}
+uint32_t emit_cap(size_t B) { return B <= kEmitWideBatch ? std::max(kEmitCap, kEmitCapWide) : kEmitCap; }
 
-bool ensure_queries(Context& c, size_t B, size_t bytes, float thr) {
+bool ensure_queries(Context& c, size_t B, size_t bytes) {
     if (B > c.bcap) {
         for (void** p : {(void**)&c.d_off, (void**)&c.d_qm, (void**)&c.d_glist, (void**)&c.d_list2, (void**)&c.d_fb,
                          (void**)&c.d_fb2, (void**)&c.d_heavy, (void**)&c.d_full, (void**)&c.d_lslots, (void**)&c.d_esn})
@@ -686,7 +683,7 @@ bool ensure_queries(Context& c, size_t B, size_t bytes, float thr) {
         c.bcap = nb;
     }
     // the survivor slots: (re)allocated when the batch or the cap this call needs outgrows them
-    const uint32_t want = emit_cap(B, thr);
+    const uint32_t want = emit_cap(B);
     if (!c.d_est || B > c.ebcap || want > c.ecap) {
         for (void** p : {(void**)&c.d_est, (void**)&c.d_esc})
             if (*p) { hipFree(*p); *p = nullptr; }
@@ -824,7 +821,7 @@ int queue_search(Library& L, Replica& R, Context& c, const uint8_t* d_raw, const
         std::lock_guard<std::mutex> g(L.valid_mu);
         std::memcpy(P.valid, L.valid, sizeof(P.valid));
     }
-    if (!ensure_queries(c, B, qbytes, thr)) return -4;
+    if (!ensure_queries(c, B, qbytes)) return -4;
     P.esn = c.d_esn;
     P.est = c.d_est;
     P.esc = c.d_esc;
@@ -1034,7 +1031,7 @@ bool queue_host_chunk(Library& L, Replica& R, Context& c, const CharT* const* qu
                 if (queries[q0 + i]) std::memcpy(hr + ho[i], queries[q0 + i], ho[i + 1] - ho[i]);
         });
         ht.mark("pack queries");
-        ok = ensure_queries(c, B, qbytes, thr) && ensure_outputs(c, B, stride) &&
+        ok = ensure_queries(c, B, qbytes) && ensure_outputs(c, B, stride) &&
              HIP_CHECK(hipMemcpyAsync(c.d_raw, c.h_raw.p, qbytes, hipMemcpyHostToDevice, c.stream)) &&
              HIP_CHECK(hipMemcpyAsync(c.d_off, ho, sizeof(uint64_t) * (B + 1), hipMemcpyHostToDevice, c.stream));
         h.d_raw = c.d_raw;
