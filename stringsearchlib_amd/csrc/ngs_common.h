@@ -143,6 +143,9 @@ constexpr bool kSketchLoose = NGS_SKETCH_LOOSE != 0;
 #ifndef NGS_LEAN_G4
 #define NGS_LEAN_G4 0  // 1: tier-1a staging reads each list's chunk base from LDS (measured 1.5 % slower)
 #endif
+#ifndef NGS_EMIT_DEPTH
+#define NGS_EMIT_DEPTH 1  // batches of survivor pairs in flight in the heavy list's k_emit
+#endif
 #ifndef NGS_RADIX_SELECT
 #define NGS_RADIX_SELECT 1  // top-L buffer refills by radix select (wave_select); 0: bitonic sort
 #endif

@@ -2656,7 +2656,7 @@ struct EmitSmem {
 // (the heavy list's k_emit measured 1.8 ms against 0.32 ms)
 constexpr uint32_t kEmitWaves = 1;
 
-template <bool RADIX>
+template <bool RADIX, int D = 1>
 __device__ __forceinline__ void emit_query(EmitSmem& S, const uint32_t q, const bool heavy_launch, const DevIndex& X,
                                            const SearchParams& P, const uint8_t* __restrict__ qnorm,
                                            const uint64_t* __restrict__ qoff, const uint32_t* __restrict__ qm,
@@ -2682,24 +2682,36 @@ __device__ __forceinline__ void emit_query(EmitSmem& S, const uint32_t q, const 
     // the query's characters only for an exact-match test (a survivor scoring > 0.999), rare
     bool have_q = false;
     // one pair per term (DevIndex.tk_identity): a software pipeline over the batches of 64: while
-    // batch b is scored, batch b + 1's pairs and batch b + 2's survivors load (a threshold-0
-    // query has thousands of survivors, and a batch is otherwise two dependent round trips)
+    // batch b is scored, the pairs of batches b + 1 .. b + D and the survivors of batches up to
+    // b + 2D + 1 are in flight (a threshold-0 query has thousands of survivors, and a batch is
+    // otherwise two dependent round trips). D = 1 in the main launch; the heavy launch, whose
+    // queries are few per SIMD and long, keeps more in flight (NGS_EMIT_DEPTH)
     uint32_t base0 = 0;
     if (X.tk_identity && sn > 64) {
-        uint32_t t0 = t, c0 = code, t1 = 0, c1 = 0;
-        if (64 + lane < sn) {
-            t1 = et[64 + lane];
-            c1 = ec[64 + lane];
+        uint32_t T[2 * D + 1], Cc[2 * D + 1];  // survivors of batches b .. b + 2D
+        uint2 K[D];                            // pairs of batches b .. b + D - 1
+        T[0] = t;
+        Cc[0] = code;
+#pragma unroll
+        for (int j = 1; j <= 2 * D; ++j) {
+            T[j] = 0;
+            Cc[j] = 0;
+            if (64u * j + lane < sn) {
+                T[j] = et[64u * j + lane];
+                Cc[j] = ec[64u * j + lane];
+            }
         }
-        uint2 k0 = X.tk[lane < sn ? t0 : 0u];
+#pragma unroll
+        for (int j = 0; j < D; ++j) K[j] = X.tk[64u * j + lane < sn ? T[j] : 0u];
         for (uint32_t base = 0; base < sn; base += 64) {
             const uint32_t i = base + lane;
-            uint32_t t2 = 0, c2 = 0;
-            if (i + 128 < sn) {
-                t2 = et[i + 128];
-                c2 = ec[i + 128];
+            uint32_t tn = 0, cn = 0;
+            if (i + 64u * (2 * D + 1) < sn) {
+                tn = et[i + 64u * (2 * D + 1)];
+                cn = ec[i + 64u * (2 * D + 1)];
             }
-            const uint2 k1 = X.tk[i + 64 < sn ? t1 : 0u];
+            const uint2 kn = X.tk[i + 64u * D < sn ? T[D] : 0u];
+            const uint32_t c0 = Cc[0];
             const float s_l = __shfl(sc_long, (int)(c0 & 63u)), s_s = __shfl(sc_short, (int)(c0 & 63u));
             const float s = (c0 & 0x80u) ? s_s : s_l;
             const bool promo = (double)s > 0.999;  // nGramSearch.hpp:328
@@ -2710,19 +2722,24 @@ __device__ __forceinline__ void emit_query(EmitSmem& S, const uint32_t q, const 
                 have_q = true;
             }
             uint32_t p = 0, pe = 0;
-            if (i < sn) term_pairs(X, t0, s, promo, tau, p, pe);  // p == t0 unless pruned
+            if (i < sn) term_pairs(X, T[0], s, promo, tau, p, pe);  // p == T[0] unless pruned
             uint64_t rec = kNoCand;
-            if (p < pe) rec = ((uint64_t)(~pair_enc(k0, s, promo, X, S.q, 4u, m, P.valid)) << 32) | k0.x;
+            if (p < pe) rec = ((uint64_t)(~pair_enc(K[0], s, promo, X, S.q, 4u, m, P.valid)) << 32) | K[0].x;
             if (cand_n + 64 > (uint32_t)kWaveCand) wave_trim<RADIX>(S, cand_n, tau, L, X.keys_unique != 0);
             const bool want = rec < tau;
             const unsigned long long bw = __ballot(want);
             if (want) S.cand()[cand_n + rank_below(bw)] = rec;
             cand_n += __popcll(bw);
-            t0 = t1;
-            c0 = c1;
-            k0 = k1;
-            t1 = t2;
-            c1 = c2;
+#pragma unroll
+            for (int j = 0; j < 2 * D; ++j) {
+                T[j] = T[j + 1];
+                Cc[j] = Cc[j + 1];
+            }
+            T[2 * D] = tn;
+            Cc[2 * D] = cn;
+#pragma unroll
+            for (int j = 0; j + 1 < D; ++j) K[j] = K[j + 1];
+            K[D - 1] = kn;
         }
         base0 = sn;
     }
@@ -2795,7 +2812,8 @@ __global__ __launch_bounds__(64 * kEmitWaves) void k_emit(DevIndex X, SearchPara
     }
     const uint32_t cnt = *qcount;
     for (uint32_t j = j0; j < cnt; j += gridDim.x * kEmitWaves) {
-        emit_query<RADIX>(S, qlist[j], true, X, P, qnorm, qoff, qm, out_n, out_k, out_s, stats);
+        emit_query<RADIX, RADIX ? NGS_EMIT_DEPTH : 1>(S, qlist[j], true, X, P, qnorm, qoff, qm, out_n, out_k, out_s,
+                                                      stats);
         wave_sync();
     }
 }
