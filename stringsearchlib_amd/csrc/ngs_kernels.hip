@@ -2616,8 +2616,10 @@ __global__ __launch_bounds__(64) void k_serve(DevIndex X, SearchParams P0, Serve
 // Tier 1a: the lean wave kernel over every query (qlist == nullptr), or over the heavy list.
 // DEFER: survivors spill to HBM for k_emit (the heavy launch always; the main one if kDeferEmit).
 // ONES: the heavy list's launch, which also takes cmin-1 queries (part_ones); the main launch
-// is compiled without that path
-template <bool DEFER, bool ONES = false>
+// is compiled without that path. LISTED: the launch walks a query list (the heavy list); the
+// main launch (one workgroup per query) is compiled with the part loop once, not twice
+// (NGS_LEAN_ONE_COPY=0 restores both paths in every instantiation)
+template <bool DEFER, bool ONES = false, bool LISTED = true>
 __global__ __launch_bounds__(64, kLeanWavesPerSimd) void k_wave_lean(DevIndex X, SearchParams P,
                                                                     const uint8_t* __restrict__ qnorm,
                                                                     const uint64_t* __restrict__ qoff,
@@ -2632,7 +2634,7 @@ __global__ __launch_bounds__(64, kLeanWavesPerSimd) void k_wave_lean(DevIndex X,
                                                                     const uint32_t* __restrict__ qlist,
                                                                     const uint32_t* __restrict__ qcount) {
     __shared__ WaveSmem<1, true> S;
-    if (!qlist) {
+    if (!LISTED || !qlist) {
         lean_query<ONES>(S, blockIdx.x, X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats, fb, fbc);
         return;
     }
@@ -3113,7 +3115,8 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
             PHO.qhead = gcount + 9;
             // (esn[] was reset by k_prep)
             auto main_lean = [&]() {
-                hipLaunchKernelGGL(k_wave_lean<kDeferEmit>, dim3(P.n_queries), dim3(64), 0, s, X, P, qnorm, off, qm,
+                hipLaunchKernelGGL((k_wave_lean<kDeferEmit, false, !NGS_LEAN_ONE_COPY>), dim3(P.n_queries), dim3(64), 0, s, X,
+                                   P, qnorm, off, qm,
                                    out_n, out_k, out_s, list2, count2, stats, fb, fbc, (const uint32_t*)nullptr,
                                    (const uint32_t*)nullptr);
                 dbg_check(s, "k_wave_lean");
