@@ -143,9 +143,6 @@ constexpr bool kSketchLoose = NGS_SKETCH_LOOSE != 0;
 #ifndef NGS_LEAN_G4
 #define NGS_LEAN_G4 0  // 1: tier-1a staging reads each list's chunk base from LDS (measured 1.5 % slower)
 #endif
-#ifndef NGS_LEAN_ONE_COPY
-#define NGS_LEAN_ONE_COPY 1  // the main tier-1a launch compiled without the query-list path
-#endif
 #ifndef NGS_EMIT_DEPTH
 #define NGS_EMIT_DEPTH 1  // batches of survivor pairs in flight in the heavy list's k_emit
 #endif

@@ -1572,7 +1572,9 @@ __device__ __forceinline__ uint32_t part_sketch(WaveSmem<W, LEAN>& S, const uint
     if (wid == 0 && nc && nc <= 64 && !(dbg & 4u)) {
         // lane l < nc holds candidate l; its term's exact count is the number of candidates with
         // that term (every entry of a term lands in the same cell), owned by the first of them
-        const uint32_t t = lane < nc ? S.cbuf[lane] : kStray;
+        uint32_t lc = lane;  // opaque: the slot address is made here, not kept across the part loop (spilled)
+        asm volatile("" : "+v"(lc));
+        const uint32_t t = lc < nc ? S.cbuf[lc] : kStray;
         uint32_t cnt = 0;
         bool first = true;
         for (uint32_t j = 0; j < nc; ++j) {
@@ -1662,7 +1664,9 @@ __device__ __forceinline__ uint32_t part_ones(WaveSmem<1, true>& S, const uint4 
         return 65;
     }
     if (nw) {  // exact counts of the candidates (as part_sketch), every one of them a survivor
-        const uint32_t t = lane < nw ? S.cbuf[lane] : kStray;
+        uint32_t lc = lane;  // opaque, as in part_sketch
+        asm volatile("" : "+v"(lc));
+        const uint32_t t = lc < nw ? S.cbuf[lc] : kStray;
         uint32_t cnt = 0;
         bool first = true;
         for (uint32_t j = 0; j < nw; ++j) {
@@ -2116,6 +2120,7 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
 // map's bits below lane l in word c / 64 (v_mbcnt_lo/hi) plus those of the earlier words; the
 // non-empty lists' {first chunk - pre, entry bounds} sit in segtab by ordinal. (stage_part, the
 // full kernel's staging, spends a marker array and a max-scan per round on the same lookup.)
+template <bool G4 = (NGS_LEAN_G4 != 0)>
 __device__ __forceinline__ void lean_stage(WaveSmem<1, true>& S, gptr<uint4> post4, uint64_t gbase,
                                            uint32_t a0, uint32_t cur, uint32_t len, uint32_t nch, uint32_t incl,
                                            uint32_t mt, uint4 (&v)[kDmaRounds], uint32_t& vmask) {
@@ -2125,15 +2130,18 @@ __device__ __forceinline__ void lean_stage(WaveSmem<1, true>& S, gptr<uint4> pos
     const uint32_t ord = rank_below(__ballot(nch != 0));
     mt = __builtin_amdgcn_readfirstlane(mt);
     uint32_t g4 = 0;
-#if NGS_LEAN_G4
-    // the list's chunk base lives in LDS (S.g4, written once per query): values the part loop
-    // keeps in registers past 80 VGPRs were spilled to scratch, and a scratch reload's vmcnt(0)
-    // waited for every load in flight, the next part's included
-    if (nch) g4 = S.g4[lane];
-    (void)gbase;
-#else
-    g4 = (uint32_t)(gbase >> 2);
-#endif
+    if constexpr (G4) {
+        // the list's chunk base lives in LDS (S.g4, written once per query): values the part loop
+        // keeps in registers past 80 VGPRs were spilled to scratch, and a scratch reload's
+        // vmcnt(0) waited for every load in flight, the next part's included (the heavy list's
+        // launch, with part_ones beside the sketch path, is over the budget; the main one is not)
+        uint32_t lz = lane;  // opaque: the slot's address is made here, not kept (and spilled)
+        asm volatile("" : "+v"(lz));
+        if (nch) g4 = S.g4[lz];
+        (void)gbase;
+    } else {
+        g4 = (uint32_t)(gbase >> 2);
+    }
     {
         // the zero and its address made here, for the same reason
         uint32_t z, l = lane;
@@ -2295,14 +2303,17 @@ __device__ __forceinline__ void lean_query(WaveSmem<1, true>& S, const uint32_t 
     WSTAMP(0);
     const bool sketch = cmin >= kSketchMinCmin && cmin <= kSketchMax;
     const bool ones = ONES && cmin == 1;  // part_ones (the heavy list's launch only)
+    constexpr bool kG4 = NGS_LEAN_G4 || ONES;  // list chunk bases in LDS (lean_stage)
     if (p_total && cmin <= n && !sketch && !ones) { bail(); return; }  // exact counting: tier 1b
     uint32_t surv_n = 0, spilled = 0;
     // the LDS survivor list to this query's kEmitCap slots in HBM; false if they are full
     auto spill = [&]() -> bool {
         if (spilled + surv_n > P.ecap) return false;
-        uint32_t* et = P.est + (size_t)q * P.ecap + spilled;
-        uint8_t* ec = P.esc + (size_t)q * P.ecap + spilled;
-        for (uint32_t i = lane; i < surv_n; i += 64) {
+        uint32_t qs = q, l0 = lane;  // opaque: the slot pointers are made here, not kept (and spilled)
+        asm volatile("" : "+s"(qs), "+v"(l0));
+        uint32_t* et = P.est + (size_t)qs * P.ecap + spilled;
+        uint8_t* ec = P.esc + (size_t)qs * P.ecap + spilled;
+        for (uint32_t i = l0; i < surv_n; i += 64) {
             et[i] = S.surv_t[i];
             ec[i] = S.surv_c[i];
         }
@@ -2323,7 +2334,7 @@ __device__ __forceinline__ void lean_query(WaveSmem<1, true>& S, const uint32_t 
         gptr<uint4> post4 = (gptr<uint4>)reinterpret_cast<const uint4*>(X.post);
         asm volatile("" : "+s"(post4));
         const uint32_t a0 = (uint32_t)gbase & 3u;  // list start within its 16-byte chunk
-        if (NGS_LEAN_G4) S.g4[lane] = (uint32_t)(gbase >> 2);  // ... and its chunk (post holds < 2^34 entries)
+        if (kG4) S.g4[lane] = (uint32_t)(gbase >> 2);  // ... and its chunk (post holds < 2^34 entries)
         // entries [s, e) of this lane's list cover 16-byte chunks [(a0 + s) / 4, (a0 + e + 3) / 4)
         auto chunks = [a0](uint32_t s, uint32_t e) -> uint32_t { return e > s ? ((a0 + e + 3) >> 2) - ((a0 + s) >> 2) : 0u; };
         // end of the next bucket group: skip[row][min(K, bn + w)]; idle lanes load nothing
@@ -2430,7 +2441,7 @@ __device__ __forceinline__ void lean_query(WaveSmem<1, true>& S, const uint32_t 
             have_p = __builtin_amdgcn_readfirstlane(have_p ? 1u : 0u) != 0;
             // ---- part i+1: issue this wave's loads ----
             if (have_p) {
-                lean_stage(S, post4, gbase, a0, cur, len, nch, incl, tot, pv, p_vm);
+                lean_stage<kG4>(S, post4, gbase, a0, cur, len, nch, incl, tot, pv, p_vm);
                 p_mt = tot;
                 cur += len;
             }
@@ -2445,10 +2456,15 @@ __device__ __forceinline__ void lean_query(WaveSmem<1, true>& S, const uint32_t 
                     wave_sync();  // the list is read before it is refilled
                 }
                 uint32_t nc;
-                if constexpr (ONES)
-                    nc = ones ? part_ones(S, cv, c_vm, c_mt, X.n_short, X.n_terms, surv_n, P.est + (size_t)q * P.ecap,
-                                          P.esc + (size_t)q * P.ecap, spilled, P.ecap)
+                if constexpr (ONES) {
+                    // the query's slot pointers made here from an opaque copy of q (SALU, per part):
+                    // hoisted out of the loop they were two 64-bit VGPR pairs spilled to scratch
+                    uint32_t qs = q;
+                    asm volatile("" : "+s"(qs));
+                    nc = ones ? part_ones(S, cv, c_vm, c_mt, X.n_short, X.n_terms, surv_n, P.est + (size_t)qs * P.ecap,
+                                          P.esc + (size_t)qs * P.ecap, spilled, P.ecap)
                               : part_sketch(S, cv, c_vm, c_mt, cmin, X.n_short, X.n_terms, surv_n, P.dbg);
+                }
                 else
                     nc = part_sketch(S, cv, c_vm, c_mt, cmin, X.n_short, X.n_terms, surv_n, P.dbg);
                 WCOUNT(11, 1);
@@ -2616,9 +2632,10 @@ __global__ __launch_bounds__(64) void k_serve(DevIndex X, SearchParams P0, Serve
 // Tier 1a: the lean wave kernel over every query (qlist == nullptr), or over the heavy list.
 // DEFER: survivors spill to HBM for k_emit (the heavy launch always; the main one if kDeferEmit).
 // ONES: the heavy list's launch, which also takes cmin-1 queries (part_ones); the main launch
-// is compiled without that path. LISTED: the launch walks a query list (the heavy list); the
-// main launch (one workgroup per query) is compiled with the part loop once, not twice
-// (NGS_LEAN_ONE_COPY=0 restores both paths in every instantiation)
+// is compiled without that path. LISTED: the launch walks a query list (the heavy list), else
+// one workgroup per query (the main launch): either way the part loop is compiled once (with
+// both in one kernel the main launch carried 76 B of scratch spills and 434 lane reloads; the
+// same speed, profiles/r03_s5_ab_lean_one_copy.txt)
 template <bool DEFER, bool ONES = false, bool LISTED = true>
 __global__ __launch_bounds__(64, kLeanWavesPerSimd) void k_wave_lean(DevIndex X, SearchParams P,
                                                                     const uint8_t* __restrict__ qnorm,
@@ -2634,7 +2651,7 @@ __global__ __launch_bounds__(64, kLeanWavesPerSimd) void k_wave_lean(DevIndex X,
                                                                     const uint32_t* __restrict__ qlist,
                                                                     const uint32_t* __restrict__ qcount) {
     __shared__ WaveSmem<1, true> S;
-    if (!LISTED || !qlist) {
+    if constexpr (!LISTED) {
         lean_query<ONES>(S, blockIdx.x, X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats, fb, fbc);
         return;
     }
@@ -3115,7 +3132,7 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
             PHO.qhead = gcount + 9;
             // (esn[] was reset by k_prep)
             auto main_lean = [&]() {
-                hipLaunchKernelGGL((k_wave_lean<kDeferEmit, false, !NGS_LEAN_ONE_COPY>), dim3(P.n_queries), dim3(64), 0, s, X,
+                hipLaunchKernelGGL((k_wave_lean<kDeferEmit, false, false>), dim3(P.n_queries), dim3(64), 0, s, X,
                                    P, qnorm, off, qm,
                                    out_n, out_k, out_s, list2, count2, stats, fb, fbc, (const uint32_t*)nullptr,
                                    (const uint32_t*)nullptr);
