@@ -435,7 +435,9 @@ def main():
                    "corpus_gen_s": round(corpus_s, 2),
                    "paths": {"tier1a_finished": int(st.fast_queries), "heavy_listed": int(st.heavy_queries),
                              "full_listed": int(st.full_queries), "tier1b_handovers": int(st.handover_queries),
-                             "tier2": int(st.tier2_queries), "general": int(st.general_queries)},
+                             "tier2": int(st.tier2_queries), "general": int(st.general_queries),
+                             "slot_full": int(st.slot_full_queries)},
+                   "survivor_slots": int(st.survivor_slots),
                    "library": L.ngsVersion().decode()},
     }
     if rank == 0 and world == 1 and not args.no_dropin and not corpus.wide:

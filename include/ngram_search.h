@@ -197,6 +197,9 @@ typedef struct {
     uint64_t tier2_queries;    /* queries routed to the block-per-query tier-2 kernel */
     uint64_t heavy_queries;    /* listed by the prep kernel as heavy (cmin 2: lean kernel on a side stream) */
     uint64_t full_queries;     /* listed by the prep kernel for tier 1b from the start (cmin 1, short search) */
+    uint64_t slot_full_queries; /* handed to tier 1b because their survivor slots were full (the
+                                   context's slots grow for later calls) */
+    uint64_t survivor_slots;   /* survivor slots per query the call ran with */
 } ngs_stats;
 NGS_API int ngsSetTiming(uint32_t handle, int enable);
 /* The last HIP error code a call on this thread failed with (0: none); clear != 0 resets it.

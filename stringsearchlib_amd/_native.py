@@ -30,7 +30,8 @@ class NgsStats(C.Structure):
                 ("postings", C.c_uint64), ("lists", C.c_uint64), ("results", C.c_uint64), ("survivors", C.c_uint64),
                 ("fast_kernel_ms", C.c_double), ("prep_kernel_ms", C.c_double), ("general_ms", C.c_double),
                 ("handover_queries", C.c_uint64), ("tier2_queries", C.c_uint64),
-                ("heavy_queries", C.c_uint64), ("full_queries", C.c_uint64)]
+                ("heavy_queries", C.c_uint64), ("full_queries", C.c_uint64),
+                ("slot_full_queries", C.c_uint64), ("survivor_slots", C.c_uint64)]
 
 
 def build(jobs: int = 4) -> None:

@@ -207,6 +207,7 @@ struct Context {
     hipEvent_t ev[6] = {};
     size_t qcap = 0, bcap = 0, ncap = 0, ocap = 0;
     uint32_t ecap = kEmitCap;  // survivor slots per query in d_est / d_esc (ensure_queries, emit_cap)
+    uint32_t ecap_grow = 0;    // slots later calls ask for: raised when tier 1a ran out of them
     size_t ebcap = 0;          // ... for this many queries
     uint8_t* d_raw = nullptr;
     uint64_t* d_off = nullptr;
@@ -668,7 +669,31 @@ bool upload(Library& L, const std::vector<int>& devs) {
 // its slots is handed to tier 1b, and large libraries have them at any threshold: sizing the
 // cap by threshold (wide only at thr <= 1/8) handed 26,594 C4 and 7,871 C5 queries per batch
 // to tier 1b (C4 420 -> 452 ms, C5 20.3 -> 21.7 ms per batch, profiles/r03_s4_ab_ecap.txt).
-uint32_t emit_cap(size_t B) { return B <= kEmitWideBatch ? std::max(kEmitCap, kEmitCapWide) : kEmitCap; }
+uint32_t emit_cap_forced() {  // NGS_ECAP: fixed slots per query, no growth (experiments)
+    static const uint32_t forced = [] {
+        const char* e = std::getenv("NGS_ECAP");
+        return e ? std::max<uint32_t>(64, (uint32_t)std::strtoul(e, nullptr, 0)) : 0u;
+    }();
+    return forced;
+}
+
+uint32_t emit_cap(size_t B) {
+    if (const uint32_t forced = emit_cap_forced()) return forced;
+    static const uint32_t init = [] {  // NGS_ECAP_INIT: the slots a context starts with (tests)
+        const char* e = std::getenv("NGS_ECAP_INIT");
+        return e ? std::max<uint32_t>(64, (uint32_t)std::strtoul(e, nullptr, 0)) : 0u;
+    }();
+    if (init) return init;
+    return B <= kEmitWideBatch ? std::max(kEmitCap, kEmitCapWide) : kEmitCap;
+}
+
+// The most survivor slots per query a batch of B may grow to: powers of two up to kEmitCapMax,
+// within kEmitBudget bytes per context (5 bytes a slot).
+uint32_t emit_cap_max(size_t B) {
+    uint32_t cap = kEmitCap;
+    while (cap < kEmitCapMax && (uint64_t)std::max<size_t>(B, 1) * (cap * 2ull) * 5ull <= kEmitBudget) cap *= 2;
+    return cap;
+}
 
 bool ensure_queries(Context& c, size_t B, size_t bytes) {
     if (B > c.bcap) {
@@ -683,7 +708,8 @@ bool ensure_queries(Context& c, size_t B, size_t bytes) {
         c.bcap = nb;
     }
     // the survivor slots: (re)allocated when the batch or the cap this call needs outgrows them
-    const uint32_t want = emit_cap(B);
+    uint32_t want = emit_cap(B);
+    if (c.ecap_grow > want && !emit_cap_forced()) want = std::min(c.ecap_grow, std::max(want, emit_cap_max(B)));
     if (!c.d_est || B > c.ebcap || want > c.ecap) {
         for (void** p : {(void**)&c.d_est, (void**)&c.d_esc})
             if (*p) { hipFree(*p); *p = nullptr; }
@@ -908,6 +934,7 @@ int finish_search(Library& L, Replica& R, Context& c, uint32_t B, const SearchPa
         if (!HIP_CHECK(hipStreamSynchronize(s))) return -4;
     }
     DevStats ds{};
+    uint64_t slot_full = 0;
     for (uint32_t i = 0; i < kStatSlots; ++i) {
         const DevStats& x = hst[i];
         ds.postings += x.postings;
@@ -916,7 +943,11 @@ int finish_search(Library& L, Replica& R, Context& c, uint32_t B, const SearchPa
         ds.fast += x.fast;
         ds.survivors += x.survivors;
         ds.errors |= x.errors;
+        slot_full += x.slot_full;
     }
+    // queries that filled their survivor slots ran again in tier 1b: when that is more than 1/64
+    // of the batch, this context's later calls get twice the slots (bounded by emit_cap_max)
+    if (!small && slot_full * 64 > B && c.ecap < emit_cap_max(B)) c.ecap_grow = std::max(c.ecap_grow, c.ecap * 2);
     if (ds.errors) {
         std::fprintf(stderr, "ngram_search: fused kernel reported internal error 0x%x\n", ds.errors);
         return -5;
@@ -930,6 +961,8 @@ int finish_search(Library& L, Replica& R, Context& c, uint32_t B, const SearchPa
         st.handover_queries = counts3[2] + counts3[4] + counts3[5];
         st.heavy_queries = counts3[3];
         st.full_queries = counts3[5];
+        st.slot_full_queries = slot_full;
+        st.survivor_slots = P.ecap;
         st.postings = ds.postings;
         st.lists = ds.lists;
         st.results = ds.results;

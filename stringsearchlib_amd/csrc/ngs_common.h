@@ -203,6 +203,8 @@ constexpr uint32_t kEmitCap = NGS_EMIT_CAP;
 // batches up to kEmitWideBatch queries get kEmitCapWide slots per query (5 bytes each): a
 // threshold-0 query has thousands of one-hit survivors at C2 (part_ones)
 constexpr uint32_t kEmitCapWide = 4096;
+constexpr uint32_t kEmitCapMax = 32768;              // ... grown up to this many per query
+constexpr uint64_t kEmitBudget = 16ull << 30;         // ... within this many bytes per context
 constexpr size_t kEmitWideBatch = 262144;             // tier 1a survivors per query spilled to HBM for k_emit
 constexpr uint32_t kWaveMaxGrams = 63;          // counts <= 63: one lane per count value
 #ifndef NGS_SK2
@@ -328,7 +330,7 @@ struct alignas(64) DevStats {  // accumulated by the fused kernel (one atomic pe
     unsigned long long fast;
     unsigned long long survivors;  // scored terms that passed the threshold
     unsigned errors;  // bit 0 table overflow, 1 flush rounds, 2 part rounds: all "cannot happen"
-    unsigned pad;
+    unsigned slot_full;  // queries tier 1a handed over because their survivor slots (ecap) were full
 };
 
 }  // namespace ngs

@@ -2321,6 +2321,10 @@ __device__ __forceinline__ void lean_query(WaveSmem<1, true>& S, const uint32_t 
         surv_n = 0;
         return true;
     };
+    // counted for the host, which grows the slots of later calls (ensure_queries)
+    auto slot_full = [&]() {
+        if (lane == 0 && !(P.dbg & 32u)) atomicAdd(&stats[q & (kStatSlots - 1)].slot_full, 1u);
+    };
     if (p_total && cmin <= n) {
         // cmin 2: every colliding pair is a false candidate, so those parts are cut at half the size
         const uint32_t shrink = ones ? kOnesShrink : cmin == 2 ? kLeanShrink2 : 0u;
@@ -2452,7 +2456,7 @@ __device__ __forceinline__ void lean_query(WaveSmem<1, true>& S, const uint32_t 
             // ---- count part i while part i+1 is in flight ----
             if (have_c) {
                 if (surv_n + 64 > (uint32_t)kWaveSurv) {
-                    if (!spill()) { bail(); return; }
+                    if (!spill()) { slot_full(); bail(); return; }
                     wave_sync();  // the list is read before it is refilled
                 }
                 uint32_t nc;
@@ -2477,7 +2481,7 @@ __device__ __forceinline__ void lean_query(WaveSmem<1, true>& S, const uint32_t 
             if (!have_p) break;
         }
     }
-    if (!spill()) { bail(); return; }
+    if (!spill()) { slot_full(); bail(); return; }
     WSTAMP(6);
 #ifdef NGS_PHASE_STAMPS
     if (lane == 0)
