@@ -289,6 +289,10 @@ struct SearchParams {
 #define NGS_SLICES 4
 #endif
 constexpr uint32_t kSlices = NGS_SLICES;
+#ifndef NGS_T1B_GRID
+#define NGS_T1B_GRID 65536
+#endif
+constexpr uint32_t kTier1bGrid = NGS_T1B_GRID;  // cap on the persistent tier-1b grids (else one per wave slot)
 constexpr uint32_t kNoPart = 0xFFFFFFFFu;  // pcnt[q * nslices]: the query was answered unsliced
 
 // ---- low-latency score() (ngsServe, opt-in): a persistent one-wave server kernel polls a

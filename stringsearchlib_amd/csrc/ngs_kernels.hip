@@ -3128,9 +3128,9 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
             // per slot of the GPU (kWaveWavesPerSimd per SIMD), items from a counter in the
             // path-count line (zeroed per call with it)
             const uint32_t g1s = std::min<uint32_t>(P.n_queries * std::max<uint32_t>(P.nslices, 1u),
-                                                    persistent_slots(kWaveWavesPerSimd));
+                                                    std::min<uint32_t>(persistent_slots(kWaveWavesPerSimd), kTier1bGrid));
             const uint32_t gh = std::min<uint32_t>(P.n_queries, P.heavy_grid ? P.heavy_grid : 4096);
-            const uint32_t gfull = std::min<uint32_t>(P.n_queries, persistent_slots(kWaveWavesPerSimd));
+            const uint32_t gfull = std::min<uint32_t>(P.n_queries, std::min<uint32_t>(persistent_slots(kWaveWavesPerSimd), kTier1bGrid));
             SearchParams PM = P, PHO = P;  // the main and the heavy hand-over launches
             PM.qhead = gcount + 8;
             PHO.qhead = gcount + 9;
