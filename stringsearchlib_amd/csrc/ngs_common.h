@@ -155,6 +155,9 @@ constexpr bool kSketchLoose = NGS_SKETCH_LOOSE != 0;
 #ifndef NGS_LEAN_DEFER_SKIP
 #define NGS_LEAN_DEFER_SKIP 0  // 1: tier 1a issues the next skip-table read after the part's loads (1 % slower)
 #endif
+#ifndef NGS_LEAN_GROUPS
+#define NGS_LEAN_GROUPS 1  // tier 1a staging by fixed lane groups per list (lean_query_g) in the main launch; 0: packed (lean_stage)
+#endif
 constexpr uint32_t kListSlots = 64;             // slot lists per routing list in k_prep
 constexpr uint32_t kNoEmit = 0xFFFFFFFFu;       // esn[q]: query not finished by tier 1a
 constexpr uint32_t kEmitHeavy = 0x80000000u;    // esn[q] flag: finished by the heavy-list launch

@@ -2497,6 +2497,446 @@ __device__ __forceinline__ void lean_query(WaveSmem<1, true>& S, const uint32_t 
     }
 }
 
+// Tier 1a with lane groups (NGS_LEAN_GROUPS): each of the query's lists owns a fixed group of lanes
+// for the whole query, sized in proportion to its length (quota_j = 1 + (64 - ng) * len_j / P lanes).
+// Lane `slot` of list j's group loads chunks slot, slot + G, slot + 2G of that list's segment in
+// each part, so a chunk never has to find its list: no per-part prefix sum, list-start map or
+// segment table, no LDS round trips before a load. A part fits when no list has more than
+// 3 G chunks (its lanes' three register rounds). The part's entry bounds are applied only where a
+// cell reached cmin (the sketch counts the <= 3 neighbouring entries at each segment edge, never an
+// undercount): entry e of chunk k is in the segment iff 4k + e - head < len.
+
+// sketch count of a part staged by lane groups (3 <= cmin <= 15): part_sketch's one-wave loose path
+__device__ __forceinline__ uint32_t lean_sketch_g(WaveSmem<1, true>& S, const uint4 (&v)[kDmaRounds], uint32_t R,
+                                                  uint32_t k0, uint32_t G, uint32_t nch, uint32_t head, uint32_t len,
+                                                  uint32_t cmin, uint32_t n_short, uint32_t n_terms, uint32_t& surv_n) {
+    const uint32_t lane = lane_id();
+    R = __builtin_amdgcn_readfirstlane(R);
+    const uint32_t cm1 = __builtin_amdgcn_readfirstlane(cmin - 1u);
+    uint32_t seen = 0;
+#pragma unroll
+    for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) {
+        if (r < R && k0 + r * G < nch) {
+            const uint32_t t[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
+            uint32_t old[4];
+#pragma unroll
+            for (uint32_t e = 0; e < 4; ++e)
+                old[e] = atomicAdd(sketch_word<1, true>(S.table, t[e]), 1u << (sketch_sh4<1, true>(t[e]) & 31u));
+#pragma unroll
+            for (uint32_t e = 0; e < 4; ++e) seen = max(seen, __builtin_amdgcn_ubfe(old[e], sketch_sh4<1, true>(t[e]), 4u));
+        }
+    }
+    const bool ovf = seen == kSketchMax, hot = seen >= cm1;
+    wave_sync();
+    uint4* T4 = reinterpret_cast<uint4*>(S.table);
+    if (!__ballot(hot || ovf)) {  // no cell reached cmin: no candidates
+#pragma unroll
+        for (uint32_t i = 0; i < (uint32_t)kWaveSlots / 256; ++i) T4[lane + 64 * i] = make_uint4(0, 0, 0, 0);
+        wave_sync();
+        return 0;
+    }
+    const uint32_t ov = __ballot(ovf) ? 65u : 0u;  // a wrapped counter: exact counting (tier 1b)
+    uint32_t nw = 0;
+#pragma unroll
+    for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) {
+        if (r < R) {
+            const uint32_t t[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
+            uint32_t w[4];
+#pragma unroll
+            for (uint32_t e = 0; e < 4; ++e) w[e] = *sketch_word<1, true>(S.table, t[e]);
+#pragma unroll
+            for (uint32_t e = 0; e < 4; ++e) {
+                bool f = __builtin_amdgcn_ubfe(w[e], sketch_sh4<1, true>(t[e]), 4u) >= cmin;
+                if (__ballot(f)) {  // rare: the entry's segment bounds (and chunks not loaded) only here
+                    f = f && 4u * (k0 + r * G) + e - head < len;
+                    const unsigned long long b = __ballot(f);
+                    const uint32_t pos = nw + rank_below(b);
+                    if (f && pos < 64u) S.cbuf[pos] = t[e];
+                    nw += (uint32_t)__popcll(b);
+                }
+            }
+        }
+    }
+    const uint32_t nc = nw + ov;
+    wave_sync();
+#pragma unroll
+    for (uint32_t i = 0; i < (uint32_t)kWaveSlots / 256; ++i) T4[lane + 64 * i] = make_uint4(0, 0, 0, 0);
+    if (nc && nc <= 64) {
+        // lane l < nc holds candidate l; its term's exact count is the number of candidates with
+        // that term (every entry of a term lands in the same cell), owned by the first of them
+        uint32_t lc = lane;  // opaque: the slot address is made here, not kept across the part loop
+        asm volatile("" : "+v"(lc));
+        const uint32_t t = lc < nc ? S.cbuf[lc] : kStray;
+        uint32_t cnt = 0;
+        bool first = true;
+        for (uint32_t j = 0; j < nc; ++j) {
+            const uint32_t tj = __builtin_amdgcn_readlane(t, j);
+            const bool eq = t == tj;
+            cnt += eq;
+            first &= !(eq && j < lane);
+        }
+        surv_append(S, lane < nc && first && cnt >= cmin, min(n_short + t, n_terms - 1u), cnt, surv_n);
+    }
+    wave_sync();
+    return nc;
+}
+
+// part_ones (cmin 1) over a part staged by lane groups
+__device__ __forceinline__ uint32_t lean_ones_g(WaveSmem<1, true>& S, const uint4 (&v)[kDmaRounds], uint32_t R,
+                                                uint32_t k0, uint32_t G, uint32_t nch, uint32_t head, uint32_t len,
+                                                uint32_t n_short, uint32_t n_terms, uint32_t& surv_n,
+                                                uint32_t* __restrict__ et, uint8_t* __restrict__ ec, uint32_t& spilled,
+                                                uint32_t ecap) {
+    const uint32_t lane = lane_id();
+    R = __builtin_amdgcn_readfirstlane(R);
+    uint32_t seen = 0;
+#pragma unroll
+    for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) {
+        if (r < R && k0 + r * G < nch) {
+            const uint32_t t[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
+            uint32_t old[4];
+#pragma unroll
+            for (uint32_t e = 0; e < 4; ++e)
+                old[e] = atomicAdd(sketch_word<1, true>(S.table, t[e]), 1u << (sketch_sh4<1, true>(t[e]) & 31u));
+#pragma unroll
+            for (uint32_t e = 0; e < 4; ++e) seen = max(seen, __builtin_amdgcn_ubfe(old[e], sketch_sh4<1, true>(t[e]), 4u));
+        }
+    }
+    const bool ovf = __ballot(seen == kSketchMax) != 0;
+    wave_sync();
+    uint32_t nw = 0;
+    if (!ovf) {
+#pragma unroll
+        for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) {
+            if (r < R) {
+                const uint32_t t[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
+                uint32_t w[4];
+#pragma unroll
+                for (uint32_t e = 0; e < 4; ++e) w[e] = *sketch_word<1, true>(S.table, t[e]);
+#pragma unroll
+                for (uint32_t e = 0; e < 4; ++e) {
+                    const bool in = 4u * (k0 + r * G) + e - head < len;
+                    const uint32_t c = in ? __builtin_amdgcn_ubfe(w[e], sketch_sh4<1, true>(t[e]), 4u) : 0u;
+                    const bool one = c == 1, two = c >= 2;
+                    const unsigned long long b1 = __ballot(one);
+                    if (b1) {
+                        const uint32_t pos = spilled + rank_below(b1);
+                        if (one && pos < ecap) {
+                            et[pos] = min(n_short + t[e], n_terms - 1u);
+                            ec[pos] = 1;
+                        }
+                        spilled += (uint32_t)__popcll(b1);
+                    }
+                    const unsigned long long b2 = __ballot(two);
+                    if (b2) {
+                        const uint32_t pos = nw + rank_below(b2);
+                        if (two && pos < 64u) S.cbuf[pos] = t[e];
+                        nw += (uint32_t)__popcll(b2);
+                    }
+                }
+            }
+        }
+    }
+    wave_sync();
+    {
+        uint4* T4 = reinterpret_cast<uint4*>(S.table);
+#pragma unroll
+        for (uint32_t i = 0; i < (uint32_t)kWaveSlots / 256; ++i) T4[lane + 64 * i] = make_uint4(0, 0, 0, 0);
+    }
+    if (ovf || nw > 64 || spilled + surv_n > ecap) {
+        wave_sync();
+        return 65;
+    }
+    if (nw) {  // exact counts of the candidates (as part_sketch), every one of them a survivor
+        uint32_t lc = lane;
+        asm volatile("" : "+v"(lc));
+        const uint32_t t = lc < nw ? S.cbuf[lc] : kStray;
+        uint32_t cnt = 0;
+        bool first = true;
+        for (uint32_t j = 0; j < nw; ++j) {
+            const uint32_t tj = __builtin_amdgcn_readlane(t, j);
+            const bool eq = t == tj;
+            cnt += eq;
+            first &= !(eq && j < lane);
+        }
+        surv_append(S, lane < nw && first, min(n_short + t, n_terms - 1u), cnt, surv_n);
+    }
+    wave_sync();
+    return nw;
+}
+
+template <bool ONES>
+__device__ __forceinline__ void lean_query_g(WaveSmem<1, true>& S, const uint32_t q, const DevIndex& X,
+                                             const SearchParams& P, const uint8_t* __restrict__ qnorm,
+                                             const uint64_t* __restrict__ qoff, const uint32_t* __restrict__ qm,
+                                             uint32_t* __restrict__ out_n, uint32_t* __restrict__ out_k,
+                                             float* __restrict__ out_s, uint32_t* __restrict__ list2,
+                                             uint32_t* __restrict__ count2, DevStats* __restrict__ stats,
+                                             uint32_t* __restrict__ fb, uint32_t* __restrict__ fbc) {
+    const uint32_t lane = lane_id();
+    auto bail = [&]() {  // hand the query to tier 1b (nothing of it was written yet)
+        if (lane == 0) fb[atomicAdd(fbc, 1u)] = q;
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    };
+    const uint32_t m = qm[q];
+    const uint32_t L = P.limit;
+    if (m == kQueryWildcard) {  // nGramSearch.hpp:356-369, answer precomputed at index time
+        const uint32_t nk = min(L, X.n_keys);
+        const size_t ob = (size_t)q * P.out_stride;
+        for (uint32_t i = lane; i < nk; i += 64) {
+            out_k[ob + i] = X.wild_key[i];
+            out_s[ob + i] = X.wild_score[i];
+        }
+        if (lane == 0) out_n[q] = nk;
+        return;
+    }
+    if (m == 0) {  // nothing left after normalisation, nGramSearch.hpp:374-375
+        if (lane == 0) out_n[q] = 0;
+        return;
+    }
+    if (m <= X.full_scan_len || m - X.gsz + 1 > kWaveMaxGrams || L > kWaveMaxLimit) {
+        if (lane == 0) list2[atomicAdd(count2, 1u)] = q;  // tier 2 / library-wide path
+        return;
+    }
+    const uint32_t n = m - X.gsz + 1;  // grams of the query (hpp:29-36)
+    const uint32_t n_long = X.n_terms - X.n_short;
+    // lane c holds the fp32 score of c hits, (float)c / n (hpp:300); the smallest passing count
+    const float sc_long = lane <= n ? (float)lane / (float)n : 0.0f;
+    const unsigned long long pm = __ballot(lane <= n && lane > 0 && !(sc_long < P.thr));
+    const uint32_t cmin = pm ? (uint32_t)(__ffsll((long long)pm) - 1) : 1000u;
+    // heavy_class() lists these for launches of their own (same test, same cmin)
+    if (!P.lean_all && (cmin <= kHeavyCmin || (m < X.short_query_len && X.n_short))) return;
+    if (m < X.short_query_len && X.n_short) { bail(); return; }  // short search: tier 1b
+    const uint8_t* qg = qnorm + qoff[q];
+    for (uint32_t i = lane; i < m; i += 64) S.q[i] = char_at(qg, i, X.csize);
+    {
+        uint4* T4 = reinterpret_cast<uint4*>(S.table);
+#pragma unroll
+        for (uint32_t i = 0; i < (uint32_t)kWaveSlots / 256; ++i) T4[lane + 64 * i] = make_uint4(0, 0, 0, 0);
+    }
+    wave_sync();
+    // ---- searchLong (nGramSearch.hpp:278-301): the gram occurrences with postings, compacted to
+    // lanes 0..ng-1 (a gram repeated k times owns k lanes: counts with multiplicity) ----
+    uint64_t gbase = 0;
+    uint32_t glen = 0, grow = 0;
+    bool have = false;
+    if (lane < n) {
+        const uint32_t code = gram_at(X, [&](uint32_t i) { return S.q[i]; }, lane);
+        if (code != UINT32_MAX) {
+            gbase = X.gram_off[code];
+            glen = (uint32_t)(X.gram_off[code + 1] - gbase);
+            grow = X.gram_row[code];
+            have = glen != 0;
+        }
+    }
+    const unsigned long long hb = __ballot(have);
+    const uint32_t ng = __popcll(hb);
+    {
+        uint32_t src = 0;
+        unsigned long long rest = hb;
+        for (uint32_t k = 0; k <= lane && rest; ++k) {  // lane k takes the k-th set bit
+            src = __ffsll((long long)rest) - 1;
+            rest &= rest - 1;
+        }
+        const uint64_t b2 = __shfl(gbase, (int)src);
+        const uint32_t l2 = __shfl(glen, (int)src), r2 = __shfl(grow, (int)src);
+        gbase = lane < ng ? b2 : 0;
+        glen = lane < ng ? l2 : 0;
+        grow = lane < ng ? r2 : 0;
+    }
+    const uint64_t p_total = wave_sum((uint64_t)glen);
+    const bool sketch = cmin >= kSketchMinCmin && cmin <= kSketchMax;
+    const bool ones = ONES && cmin == 1;  // part_ones (the heavy list's launch only)
+    if (p_total && cmin <= n && !sketch && !ones) { bail(); return; }  // exact counting: tier 1b
+    uint32_t surv_n = 0, spilled = 0;
+    // the LDS survivor list to this query's kEmitCap slots in HBM; false if they are full
+    auto spill = [&]() -> bool {
+        if (spilled + surv_n > P.ecap) return false;
+        uint32_t qs = q, l0 = lane;  // opaque: the slot pointers are made here, not kept (and spilled)
+        asm volatile("" : "+s"(qs), "+v"(l0));
+        uint32_t* et = P.est + (size_t)qs * P.ecap + spilled;
+        uint8_t* ec = P.esc + (size_t)qs * P.ecap + spilled;
+        for (uint32_t i = l0; i < surv_n; i += 64) {
+            et[i] = S.surv_t[i];
+            ec[i] = S.surv_c[i];
+        }
+        spilled += surv_n;
+        surv_n = 0;
+        return true;
+    };
+    // counted for the host, which grows the slots of later calls (ensure_queries)
+    auto slot_full = [&]() {
+        if (lane == 0 && !(P.dbg & 32u)) atomicAdd(&stats[q & (kStatSlots - 1)].slot_full, 1u);
+    };
+    if (p_total && cmin <= n) {
+        // ---- lane groups: list j owns lanes [gend_j - gq_j, gend_j), gq_j = 1 + (64 - ng) len_j / P ----
+        const uint32_t quota = lane < ng ? 1u + (uint32_t)(((uint64_t)(64u - ng) * glen) / p_total) : 0u;
+        const uint32_t qincl = wave_incl_scan(quota);
+        uint32_t jl = 0;  // this lane's list: the lists whose groups end at or below it
+        for (uint32_t k = 0; k < ng; ++k) jl += lane >= (uint32_t)__builtin_amdgcn_readlane(qincl, k) ? 1u : 0u;
+        const bool has = jl < ng;
+        const int js = (int)(has ? jl : 0u);
+        const uint32_t G = has ? (uint32_t)__shfl(quota, js) : 1u;  // the group's size
+        const uint32_t k0 = lane - ((uint32_t)__shfl(qincl, js) - G);  // this lane's slot in it
+        const uint64_t lbase = __shfl(gbase, js);
+        const uint32_t lrow = (uint32_t)__shfl(grow, js);
+        // cmin 2: every colliding pair is a false candidate, so those parts are cut at half the size
+        const uint32_t shrink = ones ? kOnesShrink : cmin == 2 ? kLeanShrink2 : 0u;
+        // chunks a part may hold of this lane's list: its lanes' three rounds (cut as the sketch part is)
+        const uint32_t capc = has ? min(3u * G, max(2u, (3u * G) >> shrink)) : 0u;
+        const uint32_t K = X.n_buckets, span = X.bucket_span;
+        const uint32_t wmax = (uint32_t)max64(1, min64(K, kMaxPartSpan / max(span, 1u)));
+        const uint32_t w = (uint32_t)max64(1, min64(wmax, (uint64_t)K * (kSketchTarget >> shrink) / p_total));
+        const uint32_t skrow = lrow * (K + 1);
+        gptr<uint4> post4 = (gptr<uint4>)reinterpret_cast<const uint4*>(X.post);
+        asm volatile("" : "+s"(post4));
+        const uint32_t a0 = (uint32_t)lbase & 3u;      // list start within its 16-byte chunk
+        const uint32_t cb = (uint32_t)(lbase >> 2);    // ... and its chunk (post holds < 2^34 entries)
+        // entries [s, e) of this lane's list cover 16-byte chunks [(a0 + s) / 4, (a0 + e + 3) / 4)
+        auto chunks = [a0](uint32_t s, uint32_t e) -> uint32_t { return e > s ? ((a0 + e + 3) >> 2) - ((a0 + s) >> 2) : 0u; };
+        // end of the next bucket group: skip[row][min(K, bn + w)]; lanes without a list load nothing
+        auto next_end = [&](uint32_t bn) -> uint32_t { return X.skip[skrow + min(K, bn + w)]; };
+        // fill of the fullest list against its cap, in 1/256: sub-part steps aim at 3/4 of it
+        auto fill = [&](uint32_t nc) -> uint32_t {
+            const uint32_t f = has ? (nc * 256u + capc - 1u) / capc : 0u;
+            return max(1u, __builtin_amdgcn_readlane(wave_incl_max_scan(f), 63));
+        };
+        uint32_t cur = 0, bnext = 0;
+        uint32_t e_pre = has ? next_end(0) : 0u;
+        uint32_t in_sub = 0, sub_lo = 0, hi_lim = 0, sub_end = 0, sub_bnext = 0, step = 1;
+        // software pipeline in registers: part i+1's loads are in flight while part i is counted
+        uint4 pv[kDmaRounds];
+        uint32_t p_nch = 0, p_head = 0, p_len = 0, p_R = 0;
+        bool have_p = false;
+#pragma unroll
+        for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) pv[r] = make_uint4(0, 0, 0, 0);
+        unsigned* err = &stats->errors;
+        for (uint32_t guard = 0;;) {
+            uint4 cv[kDmaRounds];
+#pragma unroll
+            for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) cv[r] = pv[r];
+            const uint32_t c_nch = p_nch, c_head = p_head, c_len = p_len, c_R = p_R;
+            const bool have_c = have_p;
+            // ---- next part: per lane its list's segment [cur, cur + len) ----
+            uint32_t len = 0, nch = 0;
+            have_p = false;
+            in_sub = __builtin_amdgcn_readfirstlane(in_sub);
+            bnext = __builtin_amdgcn_readfirstlane(bnext);
+            bool fast = false;
+            if (!in_sub && bnext < K) {  // common case, straight-line: the next bucket group fits
+                const uint32_t e = has ? e_pre : cur;
+                nch = chunks(cur, e);
+                if (!__ballot(nch > capc) && __ballot(nch != 0)) {
+                    len = e - cur;
+                    bnext = min(K, bnext + w);
+                    if (has) e_pre = next_end(bnext);
+                    have_p = true;
+                    fast = true;
+                }
+            }
+            for (; !fast;) {
+                guard = __builtin_amdgcn_readfirstlane(guard);
+                bnext = __builtin_amdgcn_readfirstlane(bnext);
+                sub_lo = __builtin_amdgcn_readfirstlane(sub_lo);
+                step = __builtin_amdgcn_readfirstlane(step);
+                if (++guard > 8u * K + 4096u) {
+                    atomicOr(err, 4u);  // every lane (idempotent)
+                    break;
+                }
+                if (!in_sub) {
+                    if (bnext >= K) break;
+                    const uint32_t bhi = min(K, bnext + w), e = has ? e_pre : cur;
+                    nch = chunks(cur, e);
+                    if (!__ballot(nch > capc)) {
+                        len = e - cur;
+                        bnext = bhi;
+                        if (has) e_pre = next_end(bnext);
+                        if (__ballot(nch != 0)) { have_p = true; break; }
+                        continue;
+                    }
+                    in_sub = 1;  // the group is over a list's cap: term-id sub-ranges of it
+                    sub_lo = bnext * span;
+                    hi_lim = (uint32_t)min64((uint64_t)bhi * span, n_long);
+                    sub_end = e;
+                    sub_bnext = bhi;
+                    step = (uint32_t)max64(1, min64((uint64_t)(hi_lim - sub_lo) * 192u / fill(nch), kMaxPartSpan));
+                }
+                const uint32_t hi = (uint32_t)min64(hi_lim, (uint64_t)sub_lo + step);
+                // lower_bound(list, hi) per lane, as a ballot-controlled (uniform) loop
+                uint32_t a = cur, b = has ? sub_end : cur;
+                while (__ballot(a < b)) {
+                    const bool act = a < b;
+                    const uint32_t mid = (a + b) >> 1;
+                    uint32_t pvv = 0;
+                    if (act) pvv = X.post[lbase + mid];
+                    const bool below = pvv < hi;
+                    a = act && below ? mid + 1 : a;
+                    b = act && !below ? mid : b;
+                }
+                nch = has ? chunks(cur, a) : 0u;
+                if (__ballot(nch > capc) && hi - sub_lo > 1) {
+                    step = max(1u, (uint32_t)((uint64_t)(hi - sub_lo) * 192u / fill(nch)));
+                    continue;
+                }
+                len = has ? a - cur : 0u;
+                sub_lo = hi;
+                if (sub_lo >= hi_lim) {
+                    in_sub = 0;
+                    bnext = sub_bnext;
+                    if (has) e_pre = next_end(bnext);
+                }
+                if (__ballot(nch != 0)) { have_p = true; break; }
+                cur = a;
+            }
+            have_p = __builtin_amdgcn_readfirstlane(have_p ? 1u : 0u) != 0;
+            // ---- part i+1: issue this wave's loads (lane k0 of its group: chunks k0, k0 + G, k0 + 2G) ----
+            if (have_p) {
+                const uint32_t R = 1u + (__ballot(nch > G) ? 1u : 0u) + (__ballot(nch > 2u * G) ? 1u : 0u);
+                const uint32_t head = (a0 + cur) & 3u;
+                const uint32_t first = cb + ((a0 + cur) >> 2);
+#pragma unroll
+                for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) {
+                    const uint32_t k = k0 + r * G;
+                    if (r < R && k < nch) pv[r] = post4[first + k];  // lanes past their list's segment load nothing
+                }
+                p_nch = nch;
+                p_head = head;
+                p_len = len;
+                p_R = R;
+                cur += len;
+            }
+            // ---- count part i while part i+1 is in flight ----
+            if (have_c) {
+                if (surv_n + 64 > (uint32_t)kWaveSurv) {
+                    if (!spill()) { slot_full(); bail(); return; }
+                    wave_sync();  // the list is read before it is refilled
+                }
+                uint32_t nc;
+                if constexpr (ONES) {
+                    uint32_t qs = q;
+                    asm volatile("" : "+s"(qs));
+                    nc = ones ? lean_ones_g(S, cv, c_R, k0, G, c_nch, c_head, c_len, X.n_short, X.n_terms, surv_n,
+                                            P.est + (size_t)qs * P.ecap, P.esc + (size_t)qs * P.ecap, spilled, P.ecap)
+                              : lean_sketch_g(S, cv, c_R, k0, G, c_nch, c_head, c_len, cmin, X.n_short, X.n_terms, surv_n);
+                } else {
+                    nc = lean_sketch_g(S, cv, c_R, k0, G, c_nch, c_head, c_len, cmin, X.n_short, X.n_terms, surv_n);
+                }
+                if (nc > 64) { bail(); return; }  // wrapped counter or too many candidates: tier 1b
+            }
+            if (!have_p) break;
+        }
+    }
+    if (!spill()) { slot_full(); bail(); return; }
+    if (lane == 0) P.esn[q] = spilled | (P.lean_all ? kEmitHeavy : 0u);
+    if (lane == 0 && !(P.dbg & 32u)) {
+        DevStats* sl = stats + (q & (kStatSlots - 1));
+        atomicAdd(&sl->postings, (unsigned long long)p_total);
+        atomicAdd(&sl->lists, (unsigned long long)ng);
+        atomicAdd(&sl->fast, 1ull);
+        atomicAdd(&sl->survivors, (unsigned long long)spilled);
+    }
+}
+
 // Tier 1b / experiments: the full wave kernel, over every query (qlist == nullptr) or over the
 // queries tier 1a handed over (qlist[0 .. *qcount), grid-stride).
 template <int W>
@@ -2655,13 +3095,31 @@ __global__ __launch_bounds__(64, kLeanWavesPerSimd) void k_wave_lean(DevIndex X,
                                                                     const uint32_t* __restrict__ qlist,
                                                                     const uint32_t* __restrict__ qcount) {
     __shared__ WaveSmem<1, true> S;
+    // lane-group staging (lean_query_g) for the main launch; the heavy list's launch keeps the packed
+    // staging for its threshold-0 queries (part_ones: quarter-size parts of ~3 chunks per list, where a
+    // per-list cap splits most parts), NGS_LEAN_GROUPS 2: for all of them, 3: for its cmin >= 2 ones
+    auto one = [&](uint32_t q) {
+        if constexpr (NGS_LEAN_GROUPS == 0) {
+            lean_query<ONES>(S, q, X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats, fb, fbc);
+        } else if constexpr (!ONES || NGS_LEAN_GROUPS == 2) {
+            lean_query_g<ONES>(S, q, X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats, fb, fbc);
+        } else if constexpr (NGS_LEAN_GROUPS == 3) {
+            // cmin 1 iff (float)1 / n >= thr, the test lean_query makes (same fp32 division)
+            const uint32_t m = qm[q];
+            const bool c1 = m != kQueryWildcard && m >= X.gsz && !(1.0f / (float)(m - X.gsz + 1) < P.thr);
+            if (c1) lean_query<ONES>(S, q, X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats, fb, fbc);
+            else lean_query_g<ONES>(S, q, X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats, fb, fbc);
+        } else {
+            lean_query<ONES>(S, q, X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats, fb, fbc);
+        }
+    };
     if constexpr (!LISTED) {
-        lean_query<ONES>(S, blockIdx.x, X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats, fb, fbc);
+        one(blockIdx.x);
         return;
     }
     const uint32_t cnt = *qcount;  // the heavy list, grid-stride
     for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
-        lean_query<ONES>(S, qlist[i], X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats, fb, fbc);
+        one(qlist[i]);
         wave_sync();
     }
 }
