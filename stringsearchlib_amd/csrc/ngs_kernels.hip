@@ -2665,6 +2665,12 @@ __device__ __forceinline__ uint32_t lean_ones_g(WaveSmem<1, true>& S, const uint
     return nw;
 }
 
+// a staged part of lean_query_g: its chunks per lane's list, first entry in the first chunk, entries,
+// rounds (0: no part)
+struct PartGroups {
+    uint32_t nch, head, len, R;
+};
+
 template <bool ONES>
 __device__ __forceinline__ void lean_query_g(WaveSmem<1, true>& S, const uint32_t q, const DevIndex& X,
                                              const SearchParams& P, const uint8_t* __restrict__ qnorm,
@@ -2786,7 +2792,7 @@ __device__ __forceinline__ void lean_query_g(WaveSmem<1, true>& S, const uint32_
         const uint32_t capc = has ? min(3u * G, max(2u, (3u * G) >> shrink)) : 0u;
         const uint32_t K = X.n_buckets, span = X.bucket_span;
         const uint32_t wmax = (uint32_t)max64(1, min64(K, kMaxPartSpan / max(span, 1u)));
-        const uint32_t w = (uint32_t)max64(1, min64(wmax, (uint64_t)K * (kSketchTarget >> shrink) / p_total));
+        const uint32_t w = (uint32_t)max64(1, min64(wmax, (uint64_t)K * (kGroupTarget >> shrink) / p_total));
         const uint32_t skrow = lrow * (K + 1);
         gptr<uint4> post4 = (gptr<uint4>)reinterpret_cast<const uint4*>(X.post);
         asm volatile("" : "+s"(post4));
@@ -2803,26 +2809,17 @@ __device__ __forceinline__ void lean_query_g(WaveSmem<1, true>& S, const uint32_
         };
         uint32_t cur = 0, bnext = 0;
         uint32_t e_pre = has ? next_end(0) : 0u;
+        // the first skip-table read waited for here: the loop header then merges only the back
+        // edge's pending loads (with this one pending the wait there was vmcnt(0) on every part)
+        asm volatile("" ::"v"(e_pre));
         uint32_t in_sub = 0, sub_lo = 0, hi_lim = 0, sub_end = 0, sub_bnext = 0, step = 1;
-        // software pipeline in registers: part i+1's loads are in flight while part i is counted
-        uint4 pv[kDmaRounds];
-        uint32_t p_nch = 0, p_head = 0, p_len = 0, p_R = 0;
-        bool have_p = false;
-#pragma unroll
-        for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) pv[r] = make_uint4(0, 0, 0, 0);
         unsigned* err = &stats->errors;
-        for (uint32_t guard = 0;;) {
-            uint4 cv[kDmaRounds];
-#pragma unroll
-            for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) cv[r] = pv[r];
-            const uint32_t c_nch = p_nch, c_head = p_head, c_len = p_len, c_R = p_R;
-            const bool have_c = have_p;
-            // ---- next part: per lane its list's segment [cur, cur + len) ----
-            uint32_t len = 0, nch = 0;
-            have_p = false;
+        uint32_t guard = 0;
+        // ---- the next part: per lane its list's segment [cur, cur + len) of nch chunks ----
+        auto plan = [&](uint32_t& nch, uint32_t& len) -> bool {
+            bool have_p = false;
             in_sub = __builtin_amdgcn_readfirstlane(in_sub);
             bnext = __builtin_amdgcn_readfirstlane(bnext);
-            bool fast = false;
             if (!in_sub && bnext < K) {  // common case, straight-line: the next bucket group fits
                 const uint32_t e = has ? e_pre : cur;
                 nch = chunks(cur, e);
@@ -2830,11 +2827,10 @@ __device__ __forceinline__ void lean_query_g(WaveSmem<1, true>& S, const uint32_
                     len = e - cur;
                     bnext = min(K, bnext + w);
                     if (has) e_pre = next_end(bnext);
-                    have_p = true;
-                    fast = true;
+                    return true;
                 }
             }
-            for (; !fast;) {
+            for (;;) {
                 guard = __builtin_amdgcn_readfirstlane(guard);
                 bnext = __builtin_amdgcn_readfirstlane(bnext);
                 sub_lo = __builtin_amdgcn_readfirstlane(sub_lo);
@@ -2888,43 +2884,93 @@ __device__ __forceinline__ void lean_query_g(WaveSmem<1, true>& S, const uint32_
                 if (__ballot(nch != 0)) { have_p = true; break; }
                 cur = a;
             }
-            have_p = __builtin_amdgcn_readfirstlane(have_p ? 1u : 0u) != 0;
-            // ---- part i+1: issue this wave's loads (lane k0 of its group: chunks k0, k0 + G, k0 + 2G) ----
-            if (have_p) {
-                const uint32_t R = 1u + (__ballot(nch > G) ? 1u : 0u) + (__ballot(nch > 2u * G) ? 1u : 0u);
-                const uint32_t head = (a0 + cur) & 3u;
-                const uint32_t first = cb + ((a0 + cur) >> 2);
+            return __builtin_amdgcn_readfirstlane(have_p ? 1u : 0u) != 0;
+        };
+        // ---- a planned part's loads (lane k0 of its group: chunks k0, k0 + G, k0 + 2G) ----
+        auto stage = [&](uint4 (&v)[kDmaRounds], PartGroups& ps, uint32_t nch, uint32_t len) {
+            const uint32_t R = 1u + (__ballot(nch > G) ? 1u : 0u) + (__ballot(nch > 2u * G) ? 1u : 0u);
+            const uint32_t head = (a0 + cur) & 3u;
+            const uint32_t first = cb + ((a0 + cur) >> 2);
 #pragma unroll
-                for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) {
-                    const uint32_t k = k0 + r * G;
-                    if (r < R && k < nch) pv[r] = post4[first + k];  // lanes past their list's segment load nothing
-                }
-                p_nch = nch;
-                p_head = head;
-                p_len = len;
-                p_R = R;
-                cur += len;
-            }
-            // ---- count part i while part i+1 is in flight ----
-            if (have_c) {
-                if (surv_n + 64 > (uint32_t)kWaveSurv) {
-                    if (!spill()) { slot_full(); bail(); return; }
-                    wave_sync();  // the list is read before it is refilled
-                }
-                uint32_t nc;
-                if constexpr (ONES) {
-                    uint32_t qs = q;
-                    asm volatile("" : "+s"(qs));
-                    nc = ones ? lean_ones_g(S, cv, c_R, k0, G, c_nch, c_head, c_len, X.n_short, X.n_terms, surv_n,
-                                            P.est + (size_t)qs * P.ecap, P.esc + (size_t)qs * P.ecap, spilled, P.ecap)
-                              : lean_sketch_g(S, cv, c_R, k0, G, c_nch, c_head, c_len, cmin, X.n_short, X.n_terms, surv_n);
+            for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) {
+                const uint32_t k = k0 + r * G;
+                if constexpr (NGS_LEAN_LOAD3) {
+                    // every round loads, lanes past their segment the segment's first chunk again:
+                    // the part issues exactly three loads on every path, so the counting of the part
+                    // before can wait for its own loads alone (vmcnt(3))
+                    v[r] = post4[r < R && k < nch ? first + k : first];
                 } else {
-                    nc = lean_sketch_g(S, cv, c_R, k0, G, c_nch, c_head, c_len, cmin, X.n_short, X.n_terms, surv_n);
+                    if (r < R && k < nch) v[r] = post4[first + k];  // lanes past their list's segment load nothing
                 }
-                if (nc > 64) { bail(); return; }  // wrapped counter or too many candidates: tier 1b
             }
-            if (!have_p) break;
+            ps.nch = nch;
+            ps.head = head;
+            ps.len = len;
+            ps.R = R;
+            cur += len;
+        };
+        // ---- count a part; false: the query goes to tier 1b ----
+        auto count = [&](const uint4 (&v)[kDmaRounds], const PartGroups& ps) -> bool {
+            if (surv_n + 64 > (uint32_t)kWaveSurv) {
+                if (!spill()) { slot_full(); return false; }
+                wave_sync();  // the list is read before it is refilled
+            }
+            uint32_t nc;
+            if constexpr (ONES) {
+                uint32_t qs = q;
+                asm volatile("" : "+s"(qs));
+                nc = ones ? lean_ones_g(S, v, ps.R, k0, G, ps.nch, ps.head, ps.len, X.n_short, X.n_terms, surv_n,
+                                        P.est + (size_t)qs * P.ecap, P.esc + (size_t)qs * P.ecap, spilled, P.ecap)
+                          : lean_sketch_g(S, v, ps.R, k0, G, ps.nch, ps.head, ps.len, cmin, X.n_short, X.n_terms, surv_n);
+            } else {
+                nc = lean_sketch_g(S, v, ps.R, k0, G, ps.nch, ps.head, ps.len, cmin, X.n_short, X.n_terms, surv_n);
+            }
+            return nc <= 64;  // above: a wrapped counter or too many candidates
+        };
+#if NGS_LEAN_UNROLL2
+        // two register buffers that swap roles every part (the loop unrolled by two): no buffer copy
+        // at the back edge, whose wait for the next part's loads drained them every part
+        uint4 va[kDmaRounds], vb[kDmaRounds];
+        PartGroups sa{}, sb{};
+#pragma unroll
+        for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) va[r] = vb[r] = make_uint4(0, 0, 0, 0);
+        for (;;) {
+            {
+                uint32_t nch = 0, len = 0;
+                const bool hp = plan(nch, len);
+                if (hp) stage(va, sa, nch, len);
+                if (sb.R && !count(vb, sb)) { bail(); return; }
+                sa.R = hp ? sa.R : 0u;
+                if (!hp) break;
+            }
+            {
+                uint32_t nch = 0, len = 0;
+                const bool hp = plan(nch, len);
+                if (hp) stage(vb, sb, nch, len);
+                if (sa.R && !count(va, sa)) { bail(); return; }
+                sb.R = hp ? sb.R : 0u;
+                if (!hp) break;
+            }
         }
+#else
+        // software pipeline in registers: part i+1's loads are in flight while part i is counted
+        uint4 pv[kDmaRounds];
+        PartGroups ps{};
+#pragma unroll
+        for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) pv[r] = make_uint4(0, 0, 0, 0);
+        for (;;) {
+            uint4 cv[kDmaRounds];
+#pragma unroll
+            for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) cv[r] = pv[r];
+            const PartGroups cs = ps;
+            uint32_t nch = 0, len = 0;
+            const bool hp = plan(nch, len);
+            if (hp) stage(pv, ps, nch, len);
+            if (cs.R && !count(cv, cs)) { bail(); return; }  // count part i while part i+1 is in flight
+            ps.R = hp ? ps.R : 0u;
+            if (!hp) break;
+        }
+#endif
     }
     if (!spill()) { slot_full(); bail(); return; }
     if (lane == 0) P.esn[q] = spilled | (P.lean_all ? kEmitHeavy : 0u);
