@@ -9,8 +9,9 @@
  * against gram -> term posting lists kept as CSR in HBM, counted in a u4 count-sketch in LDS
  * (candidates resolved exactly; exact LDS hash counting where the sketch cannot decide),
  * weighted, merged per key and cut to `limit` by HIP kernels for gfx950. indexN interns the
- * strings and builds the CSR on the GPU (ngs_intern.hip, ngs_build.hip; gram dictionaries of
- * other gram sizes on the host) and keeps it resident. There is no CPU search fallback: if no
+ * strings and builds the CSR on the GPU (ngs_intern.hip, ngs_build.hip; for gram dictionaries of
+ * other gram sizes the GPU also finds the distinct gram keys and the host lays out only their
+ * lookup table) and keeps it resident. There is no CPU search fallback: if no
  * GPU is usable, indexN prints the HIP error and returns 0.
  *
  * Threading: one global reader/writer lock, as the reference (dllmain.cpp:22). indexN and
@@ -171,15 +172,22 @@ NGS_API int ngsSearchDeviceAsync(uint32_t handle, const uint8_t* dQueryBytes, co
                                  uint64_t* ticket);
 NGS_API int ngsSearchDeviceWait(uint32_t handle, uint64_t ticket);
 
-/* Low-latency score()/search() (opt-in; narrow indexes): with enable != 0 a persistent one-wave
- * server kernel answers single queries from a request block in pinned host memory, with no
- * kernel launch, copy or stream wait per call. It serves libraries small enough that one wave
- * searches a query (large libraries keep the sliced latency path) and limits up to 128; other
- * calls take the regular path. The kernel leaves after 200 ms without a request and is relaunched
- * on the next call; enable = 0 or dispose() stops it. Answers are the regular path's, bit for
- * bit. Returns 0, -1 (bad handle), -2 (unbuilt index), -3 (wide index), -4 (HIP error). Calls
- * through the server are serialised on the handle. */
+/* Low-latency score()/search() (narrow indexes): a persistent one-wave server kernel answers
+ * single queries from a request block in pinned host memory, with no kernel launch, copy or
+ * stream wait per call. It serves libraries small enough that one wave searches a query (fewer
+ * than 16 skip buckets; large libraries keep the sliced latency path) and limits up to 128; other
+ * calls take the regular path. It starts by itself on such a library after the 4th score()/
+ * search() call; ngsServe(h, 1) starts it at once, ngsServe(h, 0) stops it and turns the automatic
+ * start off. The kernel leaves after 200 ms without a request (or 10 s of life) and is relaunched
+ * on the next call; a batch call (scoreBatch/searchBatch of more than 16 queries, the device entry
+ * points) stops it first and keeps it stopped until the batch is done, so no batch kernel queues
+ * behind it; dispose() stops it. Answers are the regular path's, bit for bit. One request at a
+ * time per handle: a call that finds the server busy takes the regular path. Returns 0, -1 (bad
+ * handle), -2 (unbuilt index), -3 (wide index), -4 (HIP error). */
 NGS_API int ngsServe(uint32_t handle, int enable);
+/* The server of `handle`: 0 none, 1 set up but its kernel not running, 2 its kernel running; -1
+ * bad handle (tests). */
+NGS_API int ngsServeState(uint32_t handle);
 
 /* Per-call statistics of the last search on `handle` (enable timing first). */
 typedef struct {
@@ -200,11 +208,19 @@ typedef struct {
     uint64_t slot_full_queries; /* handed to tier 1b because their survivor slots were full (the
                                    context's slots grow for later calls) */
     uint64_t survivor_slots;   /* survivor slots per query the call ran with */
+    uint64_t survivor_slot_bytes; /* bytes of survivor slots the call's context held (rows x slots x
+                                     5; at most 16 GiB, and grown slots go back after 16 calls in a
+                                     row that fill none of them) */
 } ngs_stats;
 NGS_API int ngsSetTiming(uint32_t handle, int enable);
-/* The last HIP error code a call on this thread failed with (0: none); clear != 0 resets it.
- * The reference entry points answer 0 on failure, indistinguishable from "no results": a caller
- * that must tell them apart asks here afterwards. */
+/* The last failure of a call on this thread (0: none); clear != 0 resets it. A HIP error code, or
+ * NGS_ERR_INTERNAL (a kernel reported an internal error, the -5 of the device entry points) or
+ * NGS_ERR_QUERY_BUFFER (a batch outgrew the normalised-query buffer on its rerun). A batch split
+ * across replicas hands a replica thread's failure to the calling thread. The reference entry
+ * points answer 0 on failure, indistinguishable from "no results": a caller that must tell them
+ * apart asks here afterwards. */
+#define NGS_ERR_INTERNAL 0x10001
+#define NGS_ERR_QUERY_BUFFER 0x10002
 NGS_API int ngsLastError(int clear);
 NGS_API int ngsLastStats(uint32_t handle, ngs_stats* out);
 

@@ -31,7 +31,8 @@ class NgsStats(C.Structure):
                 ("fast_kernel_ms", C.c_double), ("prep_kernel_ms", C.c_double), ("general_ms", C.c_double),
                 ("handover_queries", C.c_uint64), ("tier2_queries", C.c_uint64),
                 ("heavy_queries", C.c_uint64), ("full_queries", C.c_uint64),
-                ("slot_full_queries", C.c_uint64), ("survivor_slots", C.c_uint64)]
+                ("slot_full_queries", C.c_uint64), ("survivor_slots", C.c_uint64),
+                ("survivor_slot_bytes", C.c_uint64)]
 
 
 def build(jobs: int = 4) -> None:
@@ -139,6 +140,9 @@ def lib():
     if hasattr(L, "ngsServe"):
         L.ngsServe.restype = C.c_int
         L.ngsServe.argtypes = [u32, C.c_int]
+    if hasattr(L, "ngsServeState"):
+        L.ngsServeState.restype = C.c_int
+        L.ngsServeState.argtypes = [u32]
     L.ngsSetTiming.restype = C.c_int
     L.ngsSetTiming.argtypes = [u32, C.c_int]
     if hasattr(L, "ngsLastError"):  # (experiment builds of older sources lack it)

@@ -44,10 +44,14 @@ constexpr size_t kSmallQ = size_t(64) << 10;         // ... and if their offsets
 constexpr size_t kSioStats = sizeof(DevStats) * (kStatSlots + 1);
 constexpr size_t kSioBytes = kSioStats + kSmallBlock + kSmallQ;
 constexpr int kRetryQcap = -6;                       // finish_search: rerun with the batch's byte count
+constexpr uint32_t kCalmCalls = 16;                  // grown survivor slots unused this many calls: halved
 
 // the last HIP failure on this thread (ngsLastError): the reference's entry points answer 0 on
 // failure, indistinguishable from "no results", so callers that care ask afterwards
 thread_local int t_last_error = 0;
+// failures that are not HIP errors (include/ngram_search.h: NGS_ERR_*)
+constexpr int kErrInternal = 0x10001;     // a kernel reported an internal error (finish_search -5)
+constexpr int kErrQueryBuffer = 0x10002;  // the batch outgrew the normalised-query buffer twice
 
 bool hip_ok(hipError_t e, const char* what) {
     if (e == hipSuccess) return true;
@@ -209,6 +213,8 @@ struct Context {
     uint32_t ecap = kEmitCap;  // survivor slots per query in d_est / d_esc (ensure_queries, emit_cap)
     uint32_t ecap_grow = 0;    // slots later calls ask for: raised when tier 1a ran out of them
     size_t ebcap = 0;          // ... for this many queries
+    uint32_t calm = 0;         // calls in a row with grown slots that no query filled
+    bool shrink = false;       // ... enough of them: the next call gives half the slots back
     uint8_t* d_raw = nullptr;
     uint64_t* d_off = nullptr;
     uint8_t* d_norm = nullptr;
@@ -365,6 +371,9 @@ struct Replica {
 // kServeIdleMs without a request or after kServeLifeMs, and is relaunched on demand.
 constexpr uint32_t kServeIdleMs = 200;
 constexpr uint32_t kServeLifeMs = 10000;
+// score()/search() start the server by themselves (no ngsServe call) from this many single-query
+// calls on a library the server can answer (fewer than 16 skip buckets, narrow strings)
+constexpr uint32_t kAutoServeAfter = 4;
 
 struct Server {
     int device = 0;
@@ -409,7 +418,12 @@ struct Server {
 struct Library {
     std::unique_ptr<Server> server;  // ngsServe (null: off)
     std::atomic<bool> serving{false};  // server != null, for the unlocked test in one_query
-    std::mutex server_mu;            // creating / dropping it
+    std::mutex server_mu;            // creating / dropping it, and one request at a time
+    std::atomic<int> serve_pref{0};  // 0: automatic (kAutoServeAfter), 1: ngsServe(h, 1), -1: ngsServe(h, 0)
+    std::atomic<uint32_t> single_calls{0};  // score()/search() calls so far (automatic start)
+    // batch calls in flight: the server kernel is stopped while any runs and not relaunched until
+    // they are done, so no batch kernel queues behind it on a shared hardware queue
+    std::atomic<int> batches{0};
     HostIndex host;
     int device = 0;                              // first replica's device (or the build device)
     std::vector<std::unique_ptr<Replica>> reps;  // empty until the index is on a GPU
@@ -650,12 +664,28 @@ bool upload(Library& L, const std::vector<int>& devs) {
     if (!upload_replica(L, *L.reps.front(), keys_unique, true)) return false;
     if (L.reps.size() > 1) {
         std::vector<char> rok(L.reps.size(), 0);
+        std::vector<int> rerr(L.reps.size(), 0);
         std::vector<std::thread> th;
         for (size_t i = 1; i < L.reps.size(); ++i)
-            th.emplace_back([&, i] { rok[i] = upload_replica(L, *L.reps[i], keys_unique, false); });
+            th.emplace_back([&, i] {
+                t_last_error = 0;
+                rok[i] = upload_replica(L, *L.reps[i], keys_unique, false);
+                rerr[i] = t_last_error;
+            });
         for (auto& t : th) t.join();
-        for (size_t i = 1; i < L.reps.size(); ++i)
-            if (!rok[i]) return false;
+        // a later replica whose device build failed is placed again on this thread, serially, with
+        // the host-built gram CSR (what the first replica falls back to) instead of failing indexN
+        for (size_t i = 1; i < L.reps.size(); ++i) {
+            if (rok[i]) continue;
+            if (rerr[i]) t_last_error = rerr[i];
+            const int dev = L.reps[i]->device;
+            L.reps[i] = std::make_unique<Replica>();
+            L.reps[i]->device = dev;
+            (void)hipSetDevice(dev);
+            (void)hipGetLastError();
+            if (!L.host.grams_built) build_grams_host(L.host);
+            if (!L.host.grams_built || !upload_replica(L, *L.reps[i], keys_unique, false)) return false;
+        }
     }
     L.device = devs.front();
     free_uploaded(L.host);
@@ -707,14 +737,22 @@ bool ensure_queries(Context& c, size_t B, size_t bytes) {
             return false;
         c.bcap = nb;
     }
-    // the survivor slots: (re)allocated when the batch or the cap this call needs outgrows them
+    // the survivor slots: (re)allocated when the batch or the cap this call needs outgrows them,
+    // or when a grown cap is given back (finish_search). The rows are this call's batch (or the
+    // rows held, if more and the cap is unchanged), and the cap is bounded by kEmitBudget at the
+    // rows actually allocated: a context that once ran a large batch must not grow a small
+    // batch's cap into rows x cap bytes past the budget.
     uint32_t want = emit_cap(B);
     if (c.ecap_grow > want && !emit_cap_forced()) want = std::min(c.ecap_grow, std::max(want, emit_cap_max(B)));
-    if (!c.d_est || B > c.ebcap || want > c.ecap) {
+    const bool give_back = c.shrink && c.d_est && want < c.ecap;
+    c.shrink = false;
+    if (!c.d_est || B > c.ebcap || want > c.ecap || give_back) {
+        const size_t nb = (want == c.ecap && c.d_est) ? std::max<size_t>({B, 1024, c.ebcap}) : std::max<size_t>(B, 1024);
+        if (!emit_cap_forced()) want = std::max(emit_cap(B), std::min(want, emit_cap_max(nb)));
         for (void** p : {(void**)&c.d_est, (void**)&c.d_esc})
             if (*p) { hipFree(*p); *p = nullptr; }
-        const size_t nb = std::max<size_t>({B, 1024, c.ebcap});
         c.ebcap = 0;
+        c.ecap = 0;
         if (!dev_alloc(&c.d_est, nb * want) || !dev_alloc(&c.d_esc, nb * want)) return false;
         c.ecap = want;
         c.ebcap = nb;
@@ -946,10 +984,21 @@ int finish_search(Library& L, Replica& R, Context& c, uint32_t B, const SearchPa
         slot_full += x.slot_full;
     }
     // queries that filled their survivor slots ran again in tier 1b: when that is more than 1/64
-    // of the batch, this context's later calls get twice the slots (bounded by emit_cap_max)
-    if (!small && slot_full * 64 > B && c.ecap < emit_cap_max(B)) c.ecap_grow = std::max(c.ecap_grow, c.ecap * 2);
+    // of the batch, this context's later calls get twice the slots (bounded by emit_cap_max);
+    // after kCalmCalls calls in a row that filled none of grown slots, half of them go back
+    if (!small) {
+        if (slot_full * 64 > B) {
+            c.calm = 0;
+            if (c.ecap < emit_cap_max(B)) c.ecap_grow = std::max(c.ecap_grow, c.ecap * 2);
+        } else if (slot_full == 0 && c.ecap > emit_cap(B) && ++c.calm >= kCalmCalls) {
+            c.calm = 0;
+            c.ecap_grow = c.ecap / 2 > emit_cap(B) ? c.ecap / 2 : 0u;
+            c.shrink = true;
+        }
+    }
     if (ds.errors) {
         std::fprintf(stderr, "ngram_search: fused kernel reported internal error 0x%x\n", ds.errors);
+        t_last_error = kErrInternal;
         return -5;
     }
     if (timing) {
@@ -963,6 +1012,7 @@ int finish_search(Library& L, Replica& R, Context& c, uint32_t B, const SearchPa
         st.full_queries = counts3[5];
         st.slot_full_queries = slot_full;
         st.survivor_slots = P.ecap;
+        st.survivor_slot_bytes = (uint64_t)c.ebcap * c.ecap * (sizeof(uint32_t) + sizeof(uint8_t));
         st.postings = ds.postings;
         st.lists = ds.lists;
         st.results = ds.results;
@@ -1092,7 +1142,9 @@ bool finish_host_chunk(Library& L, Replica& R, HostChunk& h, uint32_t Lm, std::v
     const uint32_t B = h.B, q0 = h.q0;
     const size_t stride = Lm;
     HostTimer ht;
-    if (finish_search(L, R, c, B, h.P, h.d_off, h.d_n, h.d_k, h.d_s, c.stream, h.small) != 0) return false;
+    const int frc = finish_search(L, R, c, B, h.P, h.d_off, h.d_n, h.d_k, h.d_s, c.stream, h.small);
+    if (frc == kRetryQcap) t_last_error = kErrQueryBuffer;  // cannot happen: the host path sizes the buffer
+    if (frc != 0) return false;
     ht.mark("wait for kernels");
     if (h.small) {
         const uint32_t* counts3 = reinterpret_cast<const uint32_t*>(c.h_sio) + kStatSlots * 16;
@@ -1241,14 +1293,19 @@ bool host_search(Library& L, const CharT* const* queries, uint32_t nq, float thr
     std::vector<std::vector<uint32_t>> pc(parts), pk(parts);
     std::vector<std::vector<float>> ps(parts);
     std::vector<char> pok(parts, 0);
+    std::vector<int> perr(parts, 0);  // each worker's ngsLastError, handed to the caller's thread
     std::vector<std::thread> th;
     for (uint32_t i = 0; i < parts; ++i) {
         const uint32_t q0 = i * per, n = std::min(per, nq - std::min(nq, q0));
         th.emplace_back([&, i, q0, n] {
+            t_last_error = 0;
             pok[i] = host_search_one(L, *L.reps[i], queries + q0, n, thr, Lm, pc[i], pk[i], ps[i]);
+            perr[i] = pok[i] ? 0 : (t_last_error ? t_last_error : kErrInternal);
         });
     }
     for (auto& t : th) t.join();
+    for (uint32_t i = 0; i < parts; ++i)
+        if (perr[i]) t_last_error = perr[i];
     counts.clear();
     keys.clear();
     scores.clear();
@@ -1329,7 +1386,10 @@ bool host_normalise(const uint32_t* valid, const char* q, uint8_t* out, uint32_t
 // the server routes to tier 2 or the general path, or a server that cannot be reached).
 bool serve_query(Library& L, const char* query, float thr, uint32_t limit, std::vector<uint32_t>& keys,
                  std::vector<float>& sc) {
-    std::lock_guard<std::mutex> g(L.server_mu);  // one request in flight; ngsServe(0) waits for it
+    // one request in flight (ngsServe(0) waits for it); a caller that finds the server busy with
+    // another thread's request takes the regular path instead of waiting
+    std::unique_lock<std::mutex> g(L.server_mu, std::try_to_lock);
+    if (!g.owns_lock() || L.batches.load(std::memory_order_acquire) > 0) return false;
     Server* sv = L.server.get();
     const uint32_t Lm = effective_limit(L, limit);
     Replica& R = *L.reps.front();
@@ -1378,6 +1438,48 @@ bool serve_query(Library& L, const char* query, float thr, uint32_t limit, std::
     return true;
 }
 
+// Starts the server for a library it can answer once kAutoServeAfter single-query calls came in
+// (unless ngsServe(h, 0) turned it off): score() at the reference's C1 latency with no opt-in.
+void maybe_auto_serve(Library& L) {
+    if (L.serve_pref.load(std::memory_order_relaxed) != 0 || L.reps.empty() || L.host.csize != 1) return;
+    if (L.reps.front()->dev.n_buckets / 8 > 1) return;  // a large library keeps the sliced latency path
+    if (L.single_calls.fetch_add(1, std::memory_order_relaxed) + 1 < kAutoServeAfter) return;
+    std::unique_lock<std::mutex> g(L.server_mu, std::try_to_lock);
+    if (!g.owns_lock() || L.server || L.serve_pref.load() != 0) return;
+    auto sv = std::make_unique<Server>();
+    if (!sv->init(L.reps.front()->device)) {
+        L.serve_pref.store(-1);  // no server on this device: do not try again
+        (void)hipGetLastError();
+        t_last_error = 0;
+        return;
+    }
+    L.server = std::move(sv);
+    L.serving.store(true, std::memory_order_release);
+}
+
+// batches of more than kSmallBatch queries count as batch traffic (smaller ones take the latency
+// path, like score())
+inline Library* batch_mark(Library* L, uint32_t nq) { return nq > kSmallBatch ? L : nullptr; }
+
+// Marks a batch call in flight for its lifetime: a running server kernel is stopped first (its
+// stream may share a hardware queue with the batch's streams) and is not relaunched meanwhile.
+struct BatchGuard {
+    Library* L;
+    explicit BatchGuard(Library* l) : L(l) {
+        if (!L) return;
+        L->batches.fetch_add(1, std::memory_order_acq_rel);
+        if (L->serving.load(std::memory_order_acquire)) {
+            std::lock_guard<std::mutex> g(L->server_mu);
+            if (L->server && !L->server->stopped()) L->server->stop();
+        }
+    }
+    ~BatchGuard() {
+        if (L) L->batches.fetch_sub(1, std::memory_order_acq_rel);
+    }
+    BatchGuard(const BatchGuard&) = delete;
+    BatchGuard& operator=(const BatchGuard&) = delete;
+};
+
 // A narrow call on a wide index (or the reverse) is answered like an unknown handle.
 template <typename CharT>
 uint32_t one_query(uint32_t handle, const CharT* query, CharT*** results, float** scores, float thr,
@@ -1387,6 +1489,7 @@ uint32_t one_query(uint32_t handle, const CharT* query, CharT*** results, float*
     if (!L || !L->host.indexed || !query || L->host.csize != sizeof(CharT)) return 0;  // dllmain.cpp:69, hpp:417-418
     std::vector<uint32_t> counts, keys;
     std::vector<float> sc;
+    if (sizeof(CharT) == 1 && !L->serving.load(std::memory_order_acquire)) maybe_auto_serve(*L);
     if (sizeof(CharT) == 1 && L->serving.load(std::memory_order_acquire) && serve_query(*L, reinterpret_cast<const char*>(query), thr, limit, keys, sc))
         return marshal(*L, keys, sc, results, scores);
     if (!host_search(*L, &query, 1, thr, limit, counts, keys, sc)) return 0;
@@ -1400,6 +1503,7 @@ uint32_t batch_query(uint32_t handle, const CharT* const* queries, uint32_t nq, 
     std::shared_lock<std::shared_mutex> lk(g_lock);
     Library* L = find_lib(handle);
     if (!L || !L->host.indexed || !queries || !counts || L->host.csize != sizeof(CharT)) return 0;
+    BatchGuard bg(batch_mark(L, nq));
     std::vector<uint32_t> cnt, keys;
     std::vector<float> sc;
     HostTimer ht;
@@ -1668,6 +1772,7 @@ NGS_API int ngsSearchDevice(uint32_t handle, const uint8_t* dQueryBytes, const u
     if (!Rp) return -3;  // no replica on the caller's device: its buffers and stream belong there
     Replica& R = *Rp;
     hipStream_t s = (hipStream_t)stream;
+    BatchGuard bg(L);
     if (Lm == 0) {
         return HIP_CHECK(hipMemsetAsync(dCounts, 0, sizeof(uint32_t) * nQueries, s)) &&
                        HIP_CHECK(hipStreamSynchronize(s))
@@ -1692,7 +1797,10 @@ NGS_API int ngsSearchDevice(uint32_t handle, const uint8_t* dQueryBytes, const u
         rc = read_bytes(qbytes) ? device_search(*L, R, *c, dQueryBytes, dQueryOffsets, nQueries, qbytes, threshold, Lm,
                                                 outStride, dCounts, dKeys, dScores, s)
                                 : -4;
-        if (rc == kRetryQcap) rc = -5;
+        if (rc == kRetryQcap) {
+            rc = -5;
+            t_last_error = kErrQueryBuffer;
+        }
     }
     R.give_back(std::move(c));
     return rc;
@@ -1716,6 +1824,8 @@ NGS_API int ngsSearchDeviceAsync(uint32_t handle, const uint8_t* dQueryBytes, co
     Replica* Rp = L->replica_at(cur);
     if (!Rp) return -3;
     hipStream_t s = (hipStream_t)stream;
+    BatchGuard bg(L);  // the server stops here; the pending call keeps it stopped until its Wait
+    L->batches.fetch_add(1, std::memory_order_acq_rel);
     Library::Pending pd;
     pd.R = Rp;
     pd.dq = dQueryBytes;
@@ -1731,17 +1841,22 @@ NGS_API int ngsSearchDeviceAsync(uint32_t handle, const uint8_t* dQueryBytes, co
         if (!HIP_CHECK(hipMemsetAsync(dCounts, 0, sizeof(uint32_t) * nQueries, s))) return -4;
     } else {
         pd.c = Rp->acquire();
-        if (!pd.c) return -4;
+        if (!pd.c) {
+            L->batches.fetch_sub(1, std::memory_order_acq_rel);
+            return -4;
+        }
         Context& c = *pd.c;
         uint64_t qbytes = 0;
         if (!c.qcap && !(HIP_CHECK(hipMemcpyAsync(&qbytes, dQueryOffsets + nQueries, sizeof(uint64_t),
                                                  hipMemcpyDeviceToHost, s)) &&
                          HIP_CHECK(hipStreamSynchronize(s)))) {
             Rp->give_back(std::move(pd.c));
+            L->batches.fetch_sub(1, std::memory_order_acq_rel);
             return -4;
         }
         if (!HIP_CHECK(hipEventRecord(c.in_ev, s)) || !HIP_CHECK(hipStreamWaitEvent(c.stream, c.in_ev, 0))) {
             Rp->give_back(std::move(pd.c));
+            L->batches.fetch_sub(1, std::memory_order_acq_rel);
             return -4;
         }
         pd.rc = queue_search(*L, *Rp, c, dQueryBytes, dQueryOffsets, nQueries, qbytes, threshold, Lm, outStride,
@@ -1768,6 +1883,10 @@ NGS_API int ngsSearchDeviceWait(uint32_t handle, uint64_t ticket) {
         pd = std::move(it->second);
         L->pending.erase(it);
     }
+    struct Done {  // the Async call's batch mark ends with its Wait
+        Library* L;
+        ~Done() { L->batches.fetch_sub(1, std::memory_order_acq_rel); }
+    } done{L};
     if (!pd.c) return 0;  // nothing was queued (limit 0 or no queries): the counts were cleared
     Replica& R = *pd.R;
     Context& c = *pd.c;
@@ -1783,7 +1902,10 @@ NGS_API int ngsSearchDeviceWait(uint32_t handle, uint64_t ticket) {
                  ? device_search(*L, R, c, pd.dq, pd.doff, pd.B, qbytes, pd.thr, pd.Lm, pd.stride, pd.dn, pd.dk,
                                  pd.ds, c.stream)
                  : -4;
-        if (rc == kRetryQcap) rc = -5;
+        if (rc == kRetryQcap) {
+            rc = -5;
+            t_last_error = kErrQueryBuffer;
+        }
     }
     R.give_back(std::move(pd.c));
     return rc;
@@ -1797,16 +1919,27 @@ NGS_API int ngsServe(uint32_t handle, int enable) {
     if (L->host.csize != 1) return -3;
     std::lock_guard<std::mutex> g(L->server_mu);
     if (!enable) {
+        L->serve_pref.store(-1);  // off, and no automatic start either
         L->serving.store(false, std::memory_order_release);
         L->server.reset();
         return 0;
     }
+    L->serve_pref.store(1);
     if (L->server) return 0;
     auto sv = std::make_unique<Server>();
     if (!sv->init(L->reps.front()->device)) return -4;
     L->server = std::move(sv);
     L->serving.store(true, std::memory_order_release);
     return 0;
+}
+
+NGS_API int ngsServeState(uint32_t handle) {
+    std::shared_lock<std::shared_mutex> lk(g_lock);
+    Library* L = find_lib(handle);
+    if (!L) return -1;
+    std::lock_guard<std::mutex> g(L->server_mu);
+    if (!L->server) return 0;
+    return L->server->stopped() ? 1 : 2;
 }
 
 NGS_API int ngsLastError(int clear) {

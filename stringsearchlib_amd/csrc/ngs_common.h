@@ -158,12 +158,6 @@ constexpr bool kSketchLoose = NGS_SKETCH_LOOSE != 0;
 #ifndef NGS_LEAN_GROUPS
 #define NGS_LEAN_GROUPS 1  // tier 1a staging by fixed lane groups per list (lean_query_g) in the main launch; 0: packed (lean_stage)
 #endif
-#ifndef NGS_LEAN_UNROLL2
-#define NGS_LEAN_UNROLL2 0  // lean_query_g's part loop unrolled by two over buffers that swap roles
-#endif
-#ifndef NGS_LEAN_LOAD3
-#define NGS_LEAN_LOAD3 0  // lean_query_g: every part issues its three loads (lanes past their segment reload its first chunk)
-#endif
 constexpr uint32_t kListSlots = 64;             // slot lists per routing list in k_prep
 constexpr uint32_t kNoEmit = 0xFFFFFFFFu;       // esn[q]: query not finished by tier 1a
 constexpr uint32_t kEmitHeavy = 0x80000000u;    // esn[q] flag: finished by the heavy-list launch

@@ -2894,14 +2894,7 @@ __device__ __forceinline__ void lean_query_g(WaveSmem<1, true>& S, const uint32_
 #pragma unroll
             for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) {
                 const uint32_t k = k0 + r * G;
-                if constexpr (NGS_LEAN_LOAD3) {
-                    // every round loads, lanes past their segment the segment's first chunk again:
-                    // the part issues exactly three loads on every path, so the counting of the part
-                    // before can wait for its own loads alone (vmcnt(3))
-                    v[r] = post4[r < R && k < nch ? first + k : first];
-                } else {
-                    if (r < R && k < nch) v[r] = post4[first + k];  // lanes past their list's segment load nothing
-                }
+                if (r < R && k < nch) v[r] = post4[first + k];  // lanes past their list's segment load nothing
             }
             ps.nch = nch;
             ps.head = head;
@@ -2927,32 +2920,6 @@ __device__ __forceinline__ void lean_query_g(WaveSmem<1, true>& S, const uint32_
             }
             return nc <= 64;  // above: a wrapped counter or too many candidates
         };
-#if NGS_LEAN_UNROLL2
-        // two register buffers that swap roles every part (the loop unrolled by two): no buffer copy
-        // at the back edge, whose wait for the next part's loads drained them every part
-        uint4 va[kDmaRounds], vb[kDmaRounds];
-        PartGroups sa{}, sb{};
-#pragma unroll
-        for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) va[r] = vb[r] = make_uint4(0, 0, 0, 0);
-        for (;;) {
-            {
-                uint32_t nch = 0, len = 0;
-                const bool hp = plan(nch, len);
-                if (hp) stage(va, sa, nch, len);
-                if (sb.R && !count(vb, sb)) { bail(); return; }
-                sa.R = hp ? sa.R : 0u;
-                if (!hp) break;
-            }
-            {
-                uint32_t nch = 0, len = 0;
-                const bool hp = plan(nch, len);
-                if (hp) stage(vb, sb, nch, len);
-                if (sa.R && !count(va, sa)) { bail(); return; }
-                sb.R = hp ? sb.R : 0u;
-                if (!hp) break;
-            }
-        }
-#else
         // software pipeline in registers: part i+1's loads are in flight while part i is counted
         uint4 pv[kDmaRounds];
         PartGroups ps{};
@@ -2970,7 +2937,6 @@ __device__ __forceinline__ void lean_query_g(WaveSmem<1, true>& S, const uint32_
             ps.R = hp ? ps.R : 0u;
             if (!hp) break;
         }
-#endif
     }
     if (!spill()) { slot_full(); bail(); return; }
     if (lane == 0) P.esn[q] = spilled | (P.lean_all ? kEmitHeavy : 0u);

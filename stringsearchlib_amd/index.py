@@ -20,10 +20,19 @@ def _b(s) -> bytes:
     return s if isinstance(s, bytes) else s.encode("latin-1")
 
 
+# ngsLastError's codes that are not HIP errors (include/ngram_search.h)
+NGS_ERR_INTERNAL = 0x10001
+NGS_ERR_QUERY_BUFFER = 0x10002
+
+
 def _check(what: str) -> None:
-    """Raise if the last call on this thread hit a HIP error (ngsLastError): the reference's
-    entry points answer 0 on failure, which would otherwise read as "no results"."""
+    """Raise if the last call on this thread failed (ngsLastError): the reference's entry points
+    answer 0 on failure, which would otherwise read as "no results"."""
     e = _native.lib().ngsLastError(1)
+    if e == NGS_ERR_INTERNAL:
+        raise RuntimeError(f"{what} failed: a kernel reported an internal error (see stderr)")
+    if e == NGS_ERR_QUERY_BUFFER:
+        raise RuntimeError(f"{what} failed: the batch outgrew the normalised-query buffer")
     if e:
         raise RuntimeError(f"{what} failed: HIP error {e} (see stderr)")
 
@@ -210,10 +219,15 @@ class StringIndex:
         return _native.lib().ngsGramSize(self.handle)
 
     def serve(self, enable: bool = True) -> None:
-        """ngsServe: single score()/search() calls through the persistent low-latency server."""
+        """ngsServe: single score()/search() calls through the persistent low-latency server (on a
+        small library it also starts by itself after the 4th call; serve(False) turns that off)."""
         rc = _native.lib().ngsServe(self.handle, int(enable))
         if rc:
             raise RuntimeError(f"ngsServe failed: {rc}")
+
+    def serve_state(self) -> int:
+        """ngsServeState: 0 no server, 1 set up but its kernel stopped, 2 its kernel running."""
+        return _native.lib().ngsServeState(self.handle)
 
     def set_timing(self, enable: bool = True) -> None:
         _native.lib().ngsSetTiming(self.handle, int(enable))

@@ -46,7 +46,36 @@ def main():
         for q, g, ref in zip(qs, got, refs):
             if len(g) != len(ref) or any(k1 != k2 or bits(s1) != bits(s2) for (k1, s1), (k2, s2) in zip(g, ref)):
                 fails.append(f"call {call} q={q!r}: {g[:3]} vs {ref[:3]}")
-    print(json.dumps({"fails": fails[:10], "slots": slots, "slot_full": full, "handovers": handovers}))
+    # a context that ran a large batch, then small batches whose slots grow, must stay
+    # within the 16 GiB slot budget (the rows are the batch's, not the large batch's); grown slots
+    # go back after 16 calls in a row that fill none of them
+    budget = 16 << 30
+    light = [b"ZZZZZZZZ"] * 262144  # no gram of the library: no survivors, fast
+    big = gi.score_batch(light, 0.3, 100)
+    if any(big):
+        fails.append("light batch returned results")
+    bytes_seen = [gi.last_stats()["survivor_slot_bytes"]]
+    for call in range(8):
+        got = gi.score_batch(qs, 0.3, 100)
+        st = gi.last_stats()
+        slots.append(st["survivor_slots"])
+        full.append(st["slot_full_queries"])
+        bytes_seen.append(st["survivor_slot_bytes"])
+        for q, g, ref in zip(qs, got, refs):
+            if len(g) != len(ref) or any(k1 != k2 or bits(s1) != bits(s2) for (k1, s1), (k2, s2) in zip(g, ref)):
+                fails.append(f"regrow call {call} q={q!r}: {g[:3]} vs {ref[:3]}")
+    calm_slots = []
+    for call in range(40):
+        gi.score_batch([b"ZZZZZZZZ"] * 48, 0.3, 100)
+        calm_slots.append(gi.last_stats()["survivor_slots"])
+    got = gi.score_batch(qs, 0.3, 100)  # still exact after the slots shrank
+    for q, g, ref in zip(qs, got, refs):
+        if len(g) != len(ref) or any(k1 != k2 or bits(s1) != bits(s2) for (k1, s1), (k2, s2) in zip(g, ref)):
+            fails.append(f"after shrink q={q!r}: {g[:3]} vs {ref[:3]}")
+    if max(bytes_seen) > budget:
+        fails.append(f"survivor slots past the budget: {bytes_seen}")
+    print(json.dumps({"fails": fails[:10], "slots": slots, "slot_full": full, "handovers": handovers,
+                      "bytes": bytes_seen, "calm_slots": calm_slots}))
 
 
 if __name__ == "__main__":

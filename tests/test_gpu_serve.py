@@ -27,7 +27,9 @@ def test_serve_matches_regular_path_c1_shape():
     gi = ssl.StringIndex(words, 1, None)
     oi = OracleIndex(words, 1, None)
     cases = [(0.0, 100), (0.3, 100), (0.5, 10), (0.3, 128), (0.3, 129), (0.3, 0)]
+    gi.serve(False)  # the regular path's answers (no automatic server start)
     want = {(q, t, l): gi.score(q, t, l) for q in qs for t, l in cases}
+    assert gi.serve_state() == 0
     gi.serve(True)
     for q in qs:
         for t, l in cases:
@@ -49,6 +51,7 @@ def test_serve_matches_regular_path_c1_shape():
 def test_serve_fixtures(fx):
     words, weights = fixture_words(fx), fixture_weights(fx)
     plain = ssl.StringIndex(words, fx["rowSize"], weights)
+    plain.serve(False)  # regular path only
     served = ssl.StringIndex(words, fx["rowSize"], weights)
     served.serve(True)
     for ph in fx["phases"]:
@@ -62,3 +65,42 @@ def test_serve_fixtures(fx):
             assert served.score(q, thr, c["limit"]) == plain.score(q, thr, c["limit"]), f"{fx['name']} q={q!r}"
     plain.dispose()
     served.dispose()
+
+
+def test_auto_serve_c1_default_path():
+    """score() on a small library starts the server by itself after its 4th call (no ngsServe),
+    answers exactly like the oracle through it, yields it to batch calls (a batch stops the kernel;
+    the next score() relaunches it), and dispose stops it (dllmain.cpp:82-90: the default path)."""
+    words, _, rng = ssl.synth.gen_corpus(1000, seed=7)
+    qs = ssl.synth.gen_queries(words, 1, 120, rng) + [words[3], words[4].lower(), b"", b"*", b"AB"]
+    gi = ssl.StringIndex(words, 1, None)
+    oi = OracleIndex(words, 1, None)
+    assert gi.serve_state() == 0
+    states = []
+    for i, q in enumerate(qs):
+        got = gi.score(q, 0.3, 100)
+        assert_exact(got, oi.score(q, 0.3, 100), f"auto-serve q={q!r}")
+        states.append(gi.serve_state())
+    assert states[:3] == [0, 0, 0], states[:6]  # the regular path for the first three calls
+    # then the server kernel answers (it may leave after 200 ms idle, e.g. beside a slow first
+    # general-path call, and is relaunched by the next call)
+    assert states[3] == 2 and states.count(2) >= len(states) - 8, states
+    assert_exact(gi.score(qs[1], 0.3, 100), oi.score(qs[1], 0.3, 100), "served")
+    assert gi.serve_state() == 2
+    # a batch call stops the kernel first (no batch kernel queues behind it)
+    got = gi.score_batch(qs[:64], 0.3, 100)
+    for q, g in zip(qs[:64], got):
+        assert_exact(g, oi.score(q, 0.3, 100), f"batch beside the server q={q!r}")
+    assert gi.serve_state() == 1
+    assert_exact(gi.score(qs[0], 0.3, 100), oi.score(qs[0], 0.3, 100), "relaunch")
+    assert gi.serve_state() == 2
+    h = gi.handle
+    gi.dispose()  # stops the kernel and drops the server with the index
+    assert ssl._native.lib().ngsServeState(h) == -1
+    # serve(False) turns the automatic start off for good
+    g2 = ssl.StringIndex(words, 1, None)
+    g2.serve(False)
+    for q in qs[:10]:
+        assert_exact(g2.score(q, 0.3, 100), oi.score(q, 0.3, 100), f"no server q={q!r}")
+    assert g2.serve_state() == 0
+    g2.dispose()
