@@ -253,20 +253,23 @@ class StepLoop:
         self.threshold, self.limit, self.stride = threshold, limit, stride
         self.depth, self.world, self.dev, self.stream = max(1, depth), world, dev, stream
         self.nbuf = self.depth + 1 if self.depth > 1 else (2 if world > 1 else 1)
-        self.gbs = [shard.GatherBuffer(B, stride, B, dev) for _ in range(self.nbuf)]
+        self.gbs = [shard.PackedGather(B, stride, B, dev) for _ in range(self.nbuf)]
         self.st = _native.NgsStats()
         self.pending = {}  # buffer index -> in-flight top-k gather (N > 1)
         self.inflight = collections.deque()  # (ticket, buffer index) of queued batches (depth > 1)
         self.nstep = 0
         self.ktimes = []
         self.gathered = []  # rank 0, N > 1: the PendingGathers of the timed steps (tests decode them)
+        self.gather_words = []  # int32 words each gather moved per rank (N > 1)
         self.keep_gathers = False
 
     def _finished(self, i):  # batch in buffer i is complete: statistics, then its gather (N > 1)
         self.L.ngsLastStats(self.h, C.byref(self.st))
         self.ktimes.append((self.st.fast_kernel_ms, self.st.prep_kernel_ms, self.st.general_ms))
-        if self.world > 1:  # no size exchange, no host read-back: fixed-size buffers
-            pg = shard.gather_to_root(self.gbs[i], async_op=True)  # overlaps the next batches
+        if self.world > 1:  # packed on the device, gathered up to the largest record count of the ranks
+            gb = self.gbs[i].pack(getattr(self.L, "ngsPackResults", None), self.stream)
+            pg = shard.gather_packed(gb, async_op=True)  # overlaps the next batches
+            self.gather_words.append(pg.words)
             self.pending[i] = pg
             if self.keep_gathers:
                 self.gathered.append(pg)
@@ -317,6 +320,7 @@ class StepLoop:
         self.drain()
         self.ktimes.clear()
         self.gathered.clear()
+        self.gather_words.clear()
         if self.world > 1:
             dist.barrier()
         self._sync()
@@ -335,16 +339,36 @@ class StepLoop:
         return elapsed, self.ktimes
 
 
-def pmc_traffic(cfg_name: str):
-    """HBM bytes per fused-kernel launch from a committed rocprofv3 PMC pass, if any."""
+def serialised_roofline(pmc, st, version):
+    """The dominant kernel alone: the main k_wave_lean launch's own algorithmic bytes (4 B per posting
+    and 16 B per list opened, of the queries it finished: this run's ngsLastStats) over its mean
+    duration with every dispatch serialised (the SQ counter pass in profiles/). With batches in
+    flight the launches overlap, so the step-level figure above is the conservative one; this is
+    the kernel-level one (None without a committed pass)."""
+    if not pmc or not pmc.get("main_kernel_serialised_ns"):
+        return None
+    ns = pmc["main_kernel_serialised_ns"]
+    b = 4 * st.main_postings + 16 * st.main_lists
+    return {"kernel": "main k_wave_lean launch (tier 1a over the batch)", "ms": round(ns / 1e6, 4),
+            "alg_bytes": int(b), "achieved": round(b / ns, 2), "frac": round(b / ns / HBM_PEAK_GBS, 4),
+            "source": pmc.get("sq_pass"), "profiled_library": pmc.get("library"),
+            "same_source": pmc.get("library") == version}
+
+
+def pmc_record(cfg_name: str):
+    """The committed rocprofv3 record of this config (tools/pmc_traffic.py): HBM bytes per call from
+    the FETCH_SIZE pass, the main k_wave_lean launch's duration under the serialised counter pass, and
+    the library stamp they were measured on; None if there is none."""
     p = os.path.join(ROOT, "profiles", f"pmc_{cfg_name}.json")
     if not os.path.exists(p):
         return None
     try:
         with open(p) as f:
-            return json.load(f).get("hbm_bytes_per_launch")
+            d = json.load(f)
     except (OSError, ValueError):
         return None
+    d["file"] = os.path.relpath(p, ROOT)
+    return d
 
 
 def main():
@@ -412,6 +436,8 @@ def main():
     # step instead (every kernel of a batch, per GPU), the conservative figure
     roof_ms = fast_ms if depth == 1 else step_ms
     achieved = alg_bytes / (roof_ms * 1e-3) / 1e9
+    pmc = pmc_record(args.config)
+    version = L.ngsVersion().decode()
     total_q = B * world * args.steps
     value = total_q / elapsed / 1e6
     out = {
@@ -422,14 +448,19 @@ def main():
                    "threshold": cfg["threshold"], "limit": cfg["limit"], "weights": cfg["weights"],
                    "parallelism": f"query-shard x{world}" + (" + RCCL gather of top-k" if world > 1 else "")},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(args.config),
+                     "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
+                     "traffic_source": ({"file": pmc["file"], "fetch_pass": pmc.get("source"),
+                                         "profiled_library": pmc.get("library"), "this_library": version,
+                                         "same_source": pmc.get("library") == version} if pmc else None),
                      "kernel": ("tier-1 phase: k_wave_lean over the batch + k_emit, beside it k_wave_lean + k_emit on the "
                                 "heavy list and k_wave on the full list (side streams), hand-over k_wave, k_fast (HIP "
                                 "events on the call stream)" if depth == 1 else
                                 f"whole step: every kernel of one batch (k_prep, the tier-1 phase, k_fast), batches "
                                 f"pipelined {depth} deep (ngsSearchDeviceAsync); per-GPU step time"),
                      "kernel_ms": round(roof_ms, 4), "alg_bytes_per_launch": alg_bytes,
-                     "postings_per_query": round(st.postings / max(1, st.fast_queries), 1)},
+                     "postings_per_query": round(st.postings / max(1, st.fast_queries), 1),
+                     "serialised": serialised_roofline(pmc, st, version)},
         "detail": {"phase_ms": round(fast_ms, 4), "depth": depth,
                    "prep_ms": round(sum(k[1] for k in ktimes) / len(ktimes), 4),
                    "general_ms": round(sum(k[2] for k in ktimes) / len(ktimes), 4),
@@ -443,6 +474,11 @@ def main():
                    "survivor_slots": int(st.survivor_slots),
                    "library": L.ngsVersion().decode()},
     }
+    if world > 1 and loop.gather_words:  # the packed gather's bytes per rank and step
+        out["detail"]["gather"] = {
+            "bytes_per_rank_step": round(4 * sum(loop.gather_words) / len(loop.gather_words)),
+            "fixed_layout_bytes": 4 * (1 + B * (1 + 2 * stride)),
+            "note": "packed [batch, total, counts, {key, score} records] up to the largest total of the ranks"}
     if rank == 0 and world == 1 and not args.no_dropin and not corpus.wide:
         out["detail"]["dropin"] = dropin_path(L, h, cfg, raw, offs)
         out["detail"]["dropin"].update(c1_latency(local))

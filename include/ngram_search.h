@@ -185,6 +185,14 @@ NGS_API int ngsSearchDeviceWait(uint32_t handle, uint64_t ticket);
  * time per handle: a call that finds the server busy takes the regular path. Returns 0, -1 (bad
  * handle), -2 (unbuilt index), -3 (wide index), -4 (HIP error). */
 NGS_API int ngsServe(uint32_t handle, int enable);
+/* Packs a device result block in ngsSearchDevice's layout (counts[n], query i's records at
+ * i * stride) on `stream`: dOffsets[n + 1] = exclusive prefix sum of the counts (dOffsets[n] = total
+ * records) and dRecords[2 * total] = {key id, fp32 score bits} per record in query order. Used by the
+ * multi-GPU gather (stringsearchlib_amd/shard.py) so that the bytes sent to rank 0 follow the
+ * results, not n x stride. Returns 0, -3 (bad argument), -4 (HIP error). */
+NGS_API int ngsPackResults(const uint32_t* dCounts, const uint32_t* dKeys, const float* dScores, uint32_t n,
+                           uint32_t stride, uint32_t* dOffsets, uint32_t* dRecords, void* stream);
+
 /* The server of `handle`: 0 none, 1 set up but its kernel not running, 2 its kernel running; -1
  * bad handle (tests). */
 NGS_API int ngsServeState(uint32_t handle);
@@ -211,6 +219,8 @@ typedef struct {
     uint64_t survivor_slot_bytes; /* bytes of survivor slots the call's context held (rows x slots x
                                      5; at most 16 GiB, and grown slots go back after 16 calls in a
                                      row that fill none of them) */
+    uint64_t main_postings;    /* postings and lists of the queries the main tier-1a launch finished */
+    uint64_t main_lists;
 } ngs_stats;
 NGS_API int ngsSetTiming(uint32_t handle, int enable);
 /* The last failure of a call on this thread (0: none); clear != 0 resets it. A HIP error code, or

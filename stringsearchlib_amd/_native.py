@@ -32,7 +32,7 @@ class NgsStats(C.Structure):
                 ("handover_queries", C.c_uint64), ("tier2_queries", C.c_uint64),
                 ("heavy_queries", C.c_uint64), ("full_queries", C.c_uint64),
                 ("slot_full_queries", C.c_uint64), ("survivor_slots", C.c_uint64),
-                ("survivor_slot_bytes", C.c_uint64)]
+                ("survivor_slot_bytes", C.c_uint64), ("main_postings", C.c_uint64), ("main_lists", C.c_uint64)]
 
 
 def build(jobs: int = 4) -> None:
@@ -140,6 +140,9 @@ def lib():
     if hasattr(L, "ngsServe"):
         L.ngsServe.restype = C.c_int
         L.ngsServe.argtypes = [u32, C.c_int]
+    if hasattr(L, "ngsPackResults"):
+        L.ngsPackResults.restype = C.c_int
+        L.ngsPackResults.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, u32, u32, C.c_void_p, C.c_void_p, C.c_void_p]
     if hasattr(L, "ngsServeState"):
         L.ngsServeState.restype = C.c_int
         L.ngsServeState.argtypes = [u32]

@@ -980,6 +980,8 @@ int finish_search(Library& L, Replica& R, Context& c, uint32_t B, const SearchPa
         ds.results += x.results;
         ds.fast += x.fast;
         ds.survivors += x.survivors;
+        ds.main_postings += x.main_postings;
+        ds.main_lists += x.main_lists;
         ds.errors |= x.errors;
         slot_full += x.slot_full;
     }
@@ -1017,6 +1019,8 @@ int finish_search(Library& L, Replica& R, Context& c, uint32_t B, const SearchPa
         st.lists = ds.lists;
         st.results = ds.results;
         st.survivors = ds.survivors;
+        st.main_postings = ds.main_postings;
+        st.main_lists = ds.main_lists;
         if (hipEventElapsedTime(&ms, c.ev[0], c.ev[1]) == hipSuccess) st.prep_kernel_ms = ms;
         if (hipEventElapsedTime(&ms, c.ev[2], c.ev[3]) == hipSuccess) st.fast_kernel_ms = ms;
         if (ngen && hipEventElapsedTime(&ms, c.ev[4], c.ev[5]) == hipSuccess) st.general_ms = ms;
@@ -1931,6 +1935,29 @@ NGS_API int ngsServe(uint32_t handle, int enable) {
     L->server = std::move(sv);
     L->serving.store(true, std::memory_order_release);
     return 0;
+}
+
+NGS_API int ngsPackResults(const uint32_t* dCounts, const uint32_t* dKeys, const float* dScores, uint32_t n,
+                           uint32_t stride, uint32_t* dOffsets, uint32_t* dRecords, void* stream) {
+    if (!dCounts || !dOffsets || (n && (!dKeys || !dScores || !dRecords || !stride))) return -3;
+    // the scan's scratch, one grow-only buffer per device (calls on one device serialise here)
+    static std::mutex mu;
+    static std::unordered_map<int, std::pair<void*, size_t>> temp;
+    int dev = 0;
+    if (!HIP_CHECK(hipGetDevice(&dev))) return -4;
+    std::lock_guard<std::mutex> g(mu);
+    auto& t = temp[dev];
+    const size_t need = pack_pairs_temp_bytes(n);
+    if (need > t.second) {
+        if (t.first) (void)hipFree(t.first);
+        t = {nullptr, 0};
+        if (!HIP_CHECK(hipMalloc(&t.first, std::max<size_t>(need, 1 << 16)))) return -4;
+        t.second = std::max<size_t>(need, 1 << 16);
+    }
+    return HIP_CHECK(launch_pack_pairs(dCounts, dKeys, dScores, n, stride, dOffsets, dRecords, t.first, t.second,
+                                       (hipStream_t)stream))
+               ? 0
+               : -4;
 }
 
 NGS_API int ngsServeState(uint32_t handle) {

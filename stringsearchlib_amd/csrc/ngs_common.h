@@ -342,6 +342,8 @@ struct alignas(64) DevStats {  // accumulated by the fused kernel (one atomic pe
     unsigned long long survivors;  // scored terms that passed the threshold
     unsigned errors;  // bit 0 table overflow, 1 flush rounds, 2 part rounds: all "cannot happen"
     unsigned slot_full;  // queries tier 1a handed over because their survivor slots (ecap) were full
+    unsigned long long main_postings;  // postings and lists of the queries the main tier-1a launch finished
+    unsigned long long main_lists;     // (its own algorithmic bytes, bench.py's serialised roofline)
 };
 
 }  // namespace ngs

@@ -45,6 +45,11 @@ size_t pack_temp_bytes(uint32_t B);
 hipError_t launch_pack(const uint32_t* n, const uint32_t* k, const float* s, uint32_t B, uint32_t stride,
                        uint32_t* pos, uint32_t* pk, float* ps, void* temp, size_t temp_bytes, hipStream_t st,
                        const uint64_t* koff = nullptr, uint64_t pbase = 0, uint32_t cs = 0, uint64_t* pp = nullptr);
+// ngsPackResults: counts[B] + records at i * stride -> pos[B + 1] (exclusive sum) and rec[2 * total]
+// = {key, score bits} pairs (the packed multi-GPU gather, stringsearchlib_amd/shard.py)
+size_t pack_pairs_temp_bytes(uint32_t B);
+hipError_t launch_pack_pairs(const uint32_t* n, const uint32_t* k, const float* s, uint32_t B, uint32_t stride,
+                             uint32_t* pos, uint32_t* rec, void* temp, size_t temp_bytes, hipStream_t st);
 
 // Wildcard answer (nGramSearch.hpp:356-369): keys sorted by (weight desc, rank asc).
 hipError_t build_wildcard(const float* d_w, uint32_t n_keys, uint32_t* d_keys, float* d_scores, hipStream_t s);

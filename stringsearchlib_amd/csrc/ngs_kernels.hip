@@ -2946,6 +2946,10 @@ __device__ __forceinline__ void lean_query_g(WaveSmem<1, true>& S, const uint32_
         atomicAdd(&sl->lists, (unsigned long long)ng);
         atomicAdd(&sl->fast, 1ull);
         atomicAdd(&sl->survivors, (unsigned long long)spilled);
+        if (!P.lean_all) {
+            atomicAdd(&sl->main_postings, (unsigned long long)p_total);
+            atomicAdd(&sl->main_lists, (unsigned long long)ng);
+        }
     }
 }
 
@@ -3748,6 +3752,35 @@ hipError_t launch_pack(const uint32_t* n, const uint32_t* k, const float* s, uin
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_pack, dim3((B + 3) / 4), dim3(256), 0, st, n, k, s, B, stride, pos, pk, ps, koff, pbase, cs,
                        pp);
+    return hipGetLastError();
+}
+
+// one wave per query, as k_pack: query q's count records to rec[2 pos[q] ..] as {key, score bits}
+__global__ __launch_bounds__(256) void k_pack_pairs(const uint32_t* __restrict__ n, const uint32_t* __restrict__ k,
+                                                    const float* __restrict__ s, uint32_t B, uint32_t stride,
+                                                    const uint32_t* __restrict__ pos, uint2* __restrict__ rec) {
+    const uint32_t q = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    if (q >= B) return;
+    const uint32_t c = min(n[q], stride), o = pos[q];
+    const size_t src = (size_t)q * stride;
+    for (uint32_t i = lane; i < c; i += 64) rec[o + i] = make_uint2(k[src + i], __float_as_uint(s[src + i]));
+}
+
+size_t pack_pairs_temp_bytes(uint32_t B) {
+    size_t bytes = 0;
+    hipcub::DeviceScan::InclusiveSum(nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                     (int)std::max<uint32_t>(B, 1));
+    return bytes;
+}
+
+// (the caller's counts hold B entries: an inclusive sum into pos + 1 behind pos[0] = 0)
+hipError_t launch_pack_pairs(const uint32_t* n, const uint32_t* k, const float* s, uint32_t B, uint32_t stride,
+                             uint32_t* pos, uint32_t* rec, void* temp, size_t temp_bytes, hipStream_t st) {
+    hipError_t e = hipMemsetAsync(pos, 0, sizeof(uint32_t), st);
+    if (e == hipSuccess && B) e = hipcub::DeviceScan::InclusiveSum(temp, temp_bytes, n, pos + 1, (int)B, st);
+    if (e != hipSuccess) return e;
+    if (B) hipLaunchKernelGGL(k_pack_pairs, dim3((B + 3) / 4), dim3(256), 0, st, n, k, s, B, stride, pos,
+                              reinterpret_cast<uint2*>(rec));
     return hipGetLastError();
 }
 

@@ -5,11 +5,13 @@ of the batch; the only collective is the gather of the top-k records to rank 0 (
 xGMI with the ``nccl`` backend; ``gloo`` in the CPU tests). Queries share no state, so
 nothing else crosses ranks.
 
-The gather moves one fixed-size buffer per rank, sized from numbers every rank knows
-(the padded per-rank batch and the output stride), so no collective or host read-back is
-needed to agree on sizes and the whole exchange stays asynchronous: ngsSearchDevice writes its
-counts / keys / scores straight into a GatherBuffer's views, the gather runs on RCCL's stream
-beside the next batch, and rank 0 compacts the records after it waits.
+bench.py's step loop gathers packed records (PackedGather): a finished batch's results are
+packed on the device (ngsPackResults: a prefix sum of the counts and one {key, score} pair per
+record), the ranks agree on the largest record count with one 8-byte all-reduce, and the gather
+moves [batch, total, counts, records] only up to that count, so the bytes on xGMI follow the
+results (about 20 per query at C3) instead of the output stride (100). The gather itself runs on
+RCCL's stream beside the next batch's kernels. GatherBuffer / gather_to_root are the fixed-size
+form (no size agreement: batch x stride records per rank), kept for callers that hold tensors.
 """
 from __future__ import annotations
 
@@ -119,4 +121,103 @@ def gather_to_root(counts, keys=None, scores=None, stride: int | None = None, gr
     bufs = [torch.empty_like(gb.buf) for _ in range(world)] if rank == 0 else None
     work = dist.gather(gb.buf, bufs, dst=0, group=group, async_op=True)
     pending = PendingGather(work, gb, bufs, rank)
+    return pending if async_op else pending.wait()
+
+
+def pack_torch(counts, keys, scores, n, stride, offsets, records):
+    """ngsPackResults over torch tensors (CPU tests; the GPU path calls the library): offsets[n + 1]
+    = exclusive prefix sum of counts, records[2 * total] = {key, score bits} in query order."""
+    c = counts[:n].to(torch.int64)
+    offsets[0] = 0
+    offsets[1:n + 1] = torch.cumsum(c, 0).to(offsets.dtype)
+    mask = torch.arange(stride, device=counts.device).unsqueeze(0) < c.view(n, 1)
+    k = keys[:n * stride].view(n, stride)[mask]
+    sb = scores[:n * stride].view(n, stride)[mask].view(torch.int32)
+    t = k.numel()
+    rec = records[:2 * t].view(t, 2)
+    rec[:, 0] = k
+    rec[:, 1] = sb
+
+
+class PackedGather:
+    """One batch's results and its packed gather buffer. ngsSearchDevice writes ``counts`` (a view
+    of the buffer), ``keys`` and ``scores`` (query i's records at i * stride); ``pack`` then fills the
+    buffer's [batch, total, counts[pad_b], records[2 * total]] on the device; ``gather_packed`` sends
+    its prefix up to the largest total over the ranks."""
+
+    def __init__(self, batch: int, stride: int, pad_b: int | None = None, device=None):
+        pad_b = batch if pad_b is None else pad_b
+        if batch > pad_b:
+            raise ValueError(f"batch {batch} > padded batch {pad_b}")
+        self.batch, self.stride, self.pad_b = batch, stride, pad_b
+        self.buf = torch.zeros(2 + pad_b + 2 * pad_b * stride, dtype=torch.int32, device=device)
+        self.buf[0] = batch
+        self.counts = self.buf[2:2 + batch]
+        self.records = self.buf[2 + pad_b:]
+        self.keys = torch.zeros(max(1, batch * stride), dtype=torch.int32, device=device)
+        self.scores = torch.zeros(max(1, batch * stride), dtype=torch.float32, device=device)
+        self.offsets = torch.zeros(batch + 1, dtype=torch.int32, device=device)
+
+    def pack(self, packer=None, stream=None):
+        """Packs the records on the device: ``packer`` is the library's ngsPackResults (on
+        ``stream``), or None for pack_torch. The total goes to buf[1]."""
+        if packer is None:
+            pack_torch(self.counts, self.keys, self.scores, self.batch, self.stride, self.offsets, self.records)
+        else:
+            rc = packer(self.counts.data_ptr(), self.keys.data_ptr(), self.scores.data_ptr(), self.batch,
+                        self.stride, self.offsets.data_ptr(), self.records.data_ptr(), stream)
+            if rc:
+                raise RuntimeError(f"ngsPackResults -> {rc}")
+        self.buf[1:2].copy_(self.offsets[self.batch:self.batch + 1])
+        return self
+
+    @staticmethod
+    def words(pad_b: int, total: int) -> int:
+        """int32 words of a packed buffer holding `total` records."""
+        return 2 + pad_b + 2 * total
+
+    @staticmethod
+    def decode(buf: torch.Tensor, pad_b: int):
+        """(counts, keys, scores) of a gathered packed buffer (its first words(pad_b, cap) words)."""
+        b, t = int(buf[0]), int(buf[1])
+        if not 0 <= b <= pad_b or buf.numel() < PackedGather.words(pad_b, t):
+            raise ValueError(f"gathered buffer of batch {b}, {t} records in {buf.numel()} words does not match "
+                             f"pad_b {pad_b}")
+        counts = buf[2:2 + b]
+        rec = buf[2 + pad_b:2 + pad_b + 2 * t].view(t, 2)
+        if int(counts.sum()) != t:
+            raise ValueError(f"gathered counts sum to {int(counts.sum())}, not the buffer's {t} records")
+        return counts, rec[:, 0].contiguous(), rec[:, 1].contiguous().view(torch.float32)
+
+
+class PendingPacked:
+    """An in-flight packed gather: ``complete()`` orders the current stream after it; ``wait()`` returns
+    the per-rank (counts, keys, scores) on rank 0 and None elsewhere."""
+
+    def __init__(self, work, pg: PackedGather, bufs, rank, words):
+        self.work, self.pg, self.bufs, self.rank, self.words = work, pg, bufs, rank, words
+
+    def complete(self):
+        self.work.wait()
+
+    def wait(self):
+        self.work.wait()
+        if self.rank != 0:
+            return None
+        return [PackedGather.decode(b, self.pg.pad_b) for b in self.bufs]
+
+
+def gather_packed(pg: PackedGather, group=None, async_op: bool = False):
+    """Gathers every rank's packed buffer (already packed) on rank 0: one 8-byte all-reduce agrees on
+    the largest record count (a host read of it), then one gather of the buffers' prefixes of that
+    size. Bytes per rank: 4 * (2 + pad_b + 2 * max total)."""
+    tot = pg.buf[1:2].to(torch.int64)
+    dist.all_reduce(tot, op=dist.ReduceOp.MAX, group=group)
+    words = PackedGather.words(pg.pad_b, int(tot.item()))
+    rank = dist.get_rank(group)
+    world = dist.get_world_size(group)
+    send = pg.buf[:words]
+    bufs = [torch.empty(words, dtype=torch.int32, device=pg.buf.device) for _ in range(world)] if rank == 0 else None
+    work = dist.gather(send, bufs, dst=0, group=group, async_op=True)
+    pending = PendingPacked(work, pg, bufs, rank, words)
     return pending if async_op else pending.wait()

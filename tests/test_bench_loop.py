@@ -112,6 +112,9 @@ def _worker(rank, world, port, depth, result_path):
         mx = e.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         assert float(mx) == elapsed
+        # the packed gather moves the records, not B x stride
+        assert len(loop.gather_words) == steps
+        assert all(w < 1 + B * (1 + 2 * LIMIT) for w in loop.gather_words), loop.gather_words
         if rank == 0:
             assert len(loop.gathered) == steps
             want = [tuple(map(list, oi.score_ids(q, THR, LIMIT))) for q in queries[:B * world]]

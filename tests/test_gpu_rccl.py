@@ -54,6 +54,16 @@ def test_rccl_gather_of_device_results_one_rank():
             assert got == w, f"q#{i}"
             o += n
         assert o == keys.numel()
+        # the packed form of bench.py's step loop: ngsPackResults on the device, then the gather
+        # of the buffer's prefix up to the largest record count
+        pg = shard.PackedGather(len(qs), stride, pad_b=len(qs) + 5, device=dev)
+        gi.search_device(raw.data_ptr(), off.data_ptr(), len(qs), 0.3, 16, stride, pg.counts.data_ptr(),
+                         pg.keys.data_ptr(), pg.scores.data_ptr(), stream)
+        pend = shard.gather_packed(pg.pack(ssl._native.lib().ngsPackResults, stream), async_op=True)
+        assert pend.words == 2 + len(qs) + 5 + 2 * o
+        (pc, pk, ps), = pend.wait()
+        assert torch.equal(pc, counts) and torch.equal(pk, keys) and torch.equal(ps.view(torch.int32),
+                                                                              scores.view(torch.int32))
         gi.dispose()
     finally:
         dist.destroy_process_group()

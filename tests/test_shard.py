@@ -68,6 +68,19 @@ def _worker(rank, world, port, result_path):
             assert all(torch.equal(a, b) for x, y in zip(got, got_async) for a, b in zip(x, y))
         else:
             assert got is None and got_async is None
+        # the packed form bench.py's step loop uses: records packed (pack_torch stands in for
+        # ngsPackResults), the ranks agree on the largest total, the gather moves only that prefix
+        pg = shard.PackedGather(hi - lo, stride, pad_b)
+        pg.counts.copy_(c)
+        pg.keys.copy_(k)
+        pg.scores.copy_(s)
+        pend = shard.gather_packed(pg.pack(), async_op=True)
+        assert pend.words < 1 + pad_b * (1 + 2 * stride)  # fewer words than the fixed layout
+        got_packed = pend.wait()
+        if rank == 0:
+            assert all(torch.equal(a, b) for x, y in zip(got, got_packed) for a, b in zip(x, y))
+        else:
+            assert got_packed is None
         if rank == 0:
             flat = []
             for counts, keys, scores in got:
