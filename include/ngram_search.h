@@ -239,7 +239,8 @@ NGS_API int ngsLastStats(uint32_t handle, ngs_stats* out);
  * out[0..7] = postings, lists, skip buckets, FNV-1a of gram_off, post, gram_row, skip, bucket span
  * (zeros for dictionary indexes: gram sizes other than narrow 3); out[8..15] = FNV-1a of term_off,
  * term_bytes, tk_off, tk, key_off, key_bytes, wildcard keys, wildcard scores; out[16] = shape flags
- * (1 keys unique, 2 one pair per term, 4 term ids in key-rank order). Returns min(n, 17),
+ * (1 keys unique, 2 one pair per term, 4 term ids in key-rank order, 8 rank lists: the threshold-0
+ * shortcut of indexes with one weight, DevIndex.rank_post). Returns min(n, 17),
  * -1 (bad handle), -4 (HIP error). */
 NGS_API int ngsIndexDigest(uint32_t handle, uint64_t* out, int n);
 /* The same digests of replica `replica` (0 .. ngsReplicaCount - 1): every replica of an index

@@ -435,6 +435,8 @@ struct Library {
     bool tk_identity = false;  // DevIndex.tk_identity / tk_monotone / w_max, computed once for every replica
     bool tk_monotone = false;
     float w_max = 0.0f;
+    bool rank_lists = false;   // DevIndex.rank_post: one weight (w_uniform), one pair per term, one term per key
+    uint32_t w_uniform = 0;
 
     // ngsSearchDeviceAsync calls in flight: their context stays out of the pool until
     // ngsSearchDeviceWait (the general path and the statistics need the host afterwards)
@@ -509,6 +511,7 @@ bool upload_replica(Library& L, Replica& R, bool keys_unique, bool first) {
     if (!ok) return false;
     pt.mark("replica: arrays to HBM");
     bool dev_built = false;
+    uint64_t n_post = H.post.size();
     if (!H.grams_built) {
         // the gram CSR and skip table from the terms now in HBM (ngs_build.hip); dictionary
         // indexes first find their distinct gram keys there and the host lays out the lookup table
@@ -540,6 +543,7 @@ bool upload_replica(Library& L, Replica& R, bool keys_unique, bool first) {
             post = dg.post;
             gram_row = dg.gram_row;
             skip = dg.skip;
+            n_post = dg.n_post;
             if (first) {
                 H.n_grams = dg.n_grams;
                 H.n_buckets = dg.n_buckets;
@@ -578,6 +582,20 @@ bool upload_replica(Library& L, Replica& R, bool keys_unique, bool first) {
     R.owned.push_back(wild_score);
     pt.mark("replica: gram CSR");
     if (!HIP_CHECK(build_wildcard(wild_w, H.n_keys, wild_key, wild_score, nullptr))) return false;
+    X.rank_post = nullptr;
+    X.w_uniform = L.w_uniform;
+    if (L.rank_lists) {
+        // the threshold-0 shortcut's rank lists (4 bytes per posting); an index that cannot have them
+        // (over 2^31 postings) searches without them
+        const uint32_t n_seg = H.gram_mode == 1 ? (uint32_t)H.gram_keys.size() : (uint32_t)kGramSpace;
+        uint32_t* rp = nullptr;
+        if (!dev_alloc(&rp, n_post + 4)) return false;
+        R.owned.push_back(rp);
+        const hipError_t e = build_rank_post(gram_off, n_seg, post, n_post, tk, H.n_short, H.n_keys, rp, nullptr);
+        if (e == hipSuccess) X.rank_post = rp;
+        else if (e != hipErrorNotSupported && !HIP_CHECK(e)) return false;
+        pt.mark("replica: rank lists");
+    }
     X.gram_off = gram_off;
     X.post = post;
     X.gram_row = gram_row;
@@ -653,6 +671,10 @@ bool upload(Library& L, const std::vector<int>& devs) {
         std::memcpy(&w, &kw.y, sizeof w);
         if (w > L.w_max) L.w_max = w;  // NaN weights score +0 (pair_enc) and never raise the bound
     }
+    // the threshold-0 shortcut (DevIndex.rank_post) needs one record shape per hit count: one weight
+    L.rank_lists = keys_unique && L.tk_identity && !H.tk.empty() && !std::getenv("NGS_NO_RANK_LISTS");
+    L.w_uniform = H.tk.empty() ? 0u : H.tk.front().y;
+    for (size_t i = 0; L.rank_lists && i < H.tk.size(); ++i) L.rank_lists = H.tk[i].y == L.w_uniform;
     pt.mark("upload: index shape checks");
     for (int d : devs) {
         L.reps.push_back(std::make_unique<Replica>());
@@ -2046,7 +2068,8 @@ NGS_API int ngsReplicaDigest(uint32_t handle, int replica, uint64_t* out, int n)
     for (int i = 0; i < 8; ++i)
         if (!digest(tptrs[i], tsizes[i], vals[8 + i])) return -4;
     // the shape flags the kernels branch on
-    const uint64_t flags = (X.keys_unique ? 1u : 0u) | (X.tk_identity ? 2u : 0u) | (X.tk_monotone ? 4u : 0u);
+    const uint64_t flags = (X.keys_unique ? 1u : 0u) | (X.tk_identity ? 2u : 0u) | (X.tk_monotone ? 4u : 0u) |
+                           (X.rank_post ? 8u : 0u);
     const int m = std::min(n, 17);
     for (int i = 0; i < m; ++i) out[i] = i < 16 ? vals[i] : flags;
     return m;

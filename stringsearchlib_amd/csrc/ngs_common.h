@@ -246,6 +246,12 @@ struct DevIndex {  // passed by value to kernels; all pointers are device pointe
     uint32_t ghash_bits;
     const uint64_t* ghash_key;  // dictionary mode: open addressing on packed code points, ~0 = empty
     const uint32_t* ghash_val;  // -> gram id (row of gram_off / gram_row)
+    // Rank lists (threshold 0, cmin 1): when every pair has one weight, every term one pair and every
+    // key one term, a one-hit term's record is (the one score of 1/n hits, its key rank), so the one-hit
+    // records of a query's top-L are the smallest key ranks of its lists. rank_post holds, per gram,
+    // the key ranks of its postings in ascending order (the offsets of post); null otherwise.
+    const uint32_t* rank_post;
+    uint32_t w_uniform;         // ... the weight's bits
 };
 
 constexpr uint64_t kGramEmpty = ~0ull;

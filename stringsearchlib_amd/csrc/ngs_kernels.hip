@@ -2259,7 +2259,9 @@ __device__ __forceinline__ void lean_query(WaveSmem<1, true>& S, const uint32_t 
     // lane c holds the fp32 score of c hits, (float)c / n (hpp:300); the smallest passing count
     const float sc_long = lane <= n ? (float)lane / (float)n : 0.0f;
     const unsigned long long pm = __ballot(lane <= n && lane > 0 && !(sc_long < P.thr));
-    const uint32_t cmin = pm ? (uint32_t)(__ffsll((long long)pm) - 1) : 1000u;
+    // threshold 0 with rank lists: the multi-hit terms only, k_emit adds the one-hit records
+    // (emit_rank_prefix)
+    const uint32_t cmin = pm ? (X.rank_post && (pm & 2ull) ? 2u : (uint32_t)(__ffsll((long long)pm) - 1)) : 1000u;
     // heavy_class() lists these for launches of their own (same test, same cmin)
     if (!P.lean_all && (cmin <= kHeavyCmin || (m < X.short_query_len && X.n_short))) return;
     if (m < X.short_query_len && X.n_short) { bail(); return; }  // short search: tier 1b
@@ -2709,7 +2711,9 @@ __device__ __forceinline__ void lean_query_g(WaveSmem<1, true>& S, const uint32_
     // lane c holds the fp32 score of c hits, (float)c / n (hpp:300); the smallest passing count
     const float sc_long = lane <= n ? (float)lane / (float)n : 0.0f;
     const unsigned long long pm = __ballot(lane <= n && lane > 0 && !(sc_long < P.thr));
-    const uint32_t cmin = pm ? (uint32_t)(__ffsll((long long)pm) - 1) : 1000u;
+    // threshold 0 with rank lists: the multi-hit terms only, k_emit adds the one-hit records
+    // (emit_rank_prefix)
+    const uint32_t cmin = pm ? (X.rank_post && (pm & 2ull) ? 2u : (uint32_t)(__ffsll((long long)pm) - 1)) : 1000u;
     // heavy_class() lists these for launches of their own (same test, same cmin)
     if (!P.lean_all && (cmin <= kHeavyCmin || (m < X.short_query_len && X.n_short))) return;
     if (m < X.short_query_len && X.n_short) { bail(); return; }  // short search: tier 1b
@@ -3147,7 +3151,76 @@ struct EmitSmem {
     uint64_t cand_own[kWaveCand];
     __device__ __forceinline__ uint64_t* cand() { return cand_own; }
     uint32_t q[kWaveMaxGrams + 8];
+    uint32_t kset[2 * kWaveMaxLimit];  // emit_rank_prefix: the keys of the multi-hit top-L
 };
+
+// The one-hit records of a threshold-0 query's top-L (DevIndex.rank_post; tier 1a counted the query
+// at cmin 2 and its multi-hit records are in the buffer). With one weight, one pair per term and one
+// term per key, every one-hit term's record is (enc1 = the score of 1 hit of n, its key rank), and a
+// multi-hit record is never worse than that score. A one-hit term in the top-L has all the terms
+// before it in its list (smaller key ranks: each a one-hit record that ties and wins on the rank, or a
+// multi-hit one at least as good) in the top-L too, so it is among its list's first L entries. Those
+// are merged into the buffer (calcScore's records, nGramSearch.hpp:318-336), each list until its
+// records pass tau (ascending ranks: the rest are worse). An entry whose term is multi-hit is a
+// duplicate of its real record: dropped when that record is among the multi-hit top-L (kset), and
+// worse than tau otherwise.
+template <bool RADIX>
+__device__ void emit_rank_prefix(EmitSmem& S, const DevIndex& X, const SearchParams& P, uint32_t n, uint32_t L,
+                                 float sc_long, uint32_t& cand_n, uint64_t& tau) {
+    const uint32_t lane = lane_id();
+    wave_flush<RADIX>(S, cand_n, tau, L, true);  // the multi-hit top-L (<= L records)
+    constexpr uint32_t kSet = 2 * kWaveMaxLimit, kEmpty = 0xFFFFFFFFu;
+    auto slot = [](uint32_t k) -> uint32_t { return (k * 0x9E3779B1u) >> (32 - 8); };
+    static_assert(kSet == 256, "8-bit set slots");
+    for (uint32_t i = lane; i < kSet; i += 64) S.kset[i] = kEmpty;
+    wave_sync();
+    if (lane < cand_n) {
+        const uint32_t k = (uint32_t)S.cand()[lane], k2 = lane + 64 < cand_n ? (uint32_t)S.cand()[lane + 64] : kEmpty;
+        for (uint32_t h = slot(k);; h = (h + 1) & (kSet - 1))
+            if (atomicCAS(&S.kset[h], kEmpty, k) == kEmpty) break;
+        if (k2 != kEmpty)
+            for (uint32_t h = slot(k2);; h = (h + 1) & (kSet - 1))
+                if (atomicCAS(&S.kset[h], kEmpty, k2) == kEmpty) break;
+    }
+    wave_sync();
+    // this lane's gram occurrence: its list (a repeated gram's list twice: its terms are multi-hit)
+    uint64_t gbase = 0;
+    uint32_t glen = 0;
+    if (lane < n) {
+        const uint32_t code = gram_at(X, [&](uint32_t i) { return S.q[i]; }, lane);
+        if (code != UINT32_MAX) {
+            gbase = X.gram_off[code];
+            glen = (uint32_t)min64(X.gram_off[code + 1] - gbase, (uint64_t)L);
+        }
+    }
+    const float sc = __uint_as_float(X.w_uniform) * __shfl(sc_long, 1);  // pair_enc of one hit
+    const uint32_t enc1 = sc > 0.0f ? __float_as_uint(sc) + 1u : 1u;
+    const uint64_t hi = (uint64_t)(~enc1) << 32;
+    for (uint32_t j = 0; j < n; ++j) {
+        const uint32_t len = __builtin_amdgcn_readlane(glen, (int)j);
+        const uint64_t b = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(gbase >> 32), (int)j) << 32) |
+                           __builtin_amdgcn_readlane((uint32_t)gbase, (int)j);
+        for (uint32_t o = 0; o < len; o += 64) {
+            const uint32_t i = o + lane;
+            const uint64_t rec = i < len ? hi | X.rank_post[b + i] : kNoCand;
+            if (!__ballot(rec < tau)) break;  // ascending: the rest of the list is worse too
+            bool want = rec < tau;
+            if (want) {
+                const uint32_t k = (uint32_t)rec;
+                for (uint32_t h = slot(k);; h = (h + 1) & (kSet - 1)) {
+                    const uint32_t v = S.kset[h];
+                    if (v == k) { want = false; break; }
+                    if (v == kEmpty) break;
+                }
+            }
+            if (cand_n + 64 > (uint32_t)kWaveCand) wave_trim<RADIX>(S, cand_n, tau, L, true);
+            want = want && rec < tau;
+            const unsigned long long bw = __ballot(want);
+            if (want) S.cand()[cand_n + rank_below(bw)] = rec;
+            cand_n += __popcll(bw);
+        }
+    }
+}
 
 // one wave per workgroup: four-wave workgroups wait for four free slots on one CU beside tier 1a
 // (the heavy list's k_emit measured 1.8 ms against 0.32 ms)
@@ -3275,6 +3348,16 @@ __device__ __forceinline__ void emit_query(EmitSmem& S, const uint32_t q, const 
         }
         t = t_next;
         code = code_next;
+    }
+    // threshold 0 with rank lists: tier 1a counted this query at cmin 2 (its multi-hit terms, above);
+    // its one-hit records come from the first L key ranks of each of its lists
+    if (X.rank_post && !(__shfl(sc_long, 1) < P.thr)) {
+        if (!have_q) {
+            const uint8_t* qg = qnorm + qoff[q];
+            for (uint32_t k = lane; k < m; k += 64) S.q[k] = char_at(qg, k, X.csize);
+            wave_sync();
+        }
+        emit_rank_prefix<RADIX>(S, X, P, n, L, sc_long, cand_n, tau);
     }
     wave_flush<RADIX>(S, cand_n, tau, L, X.keys_unique != 0);
     const size_t ob = (size_t)q * P.out_stride;
@@ -3465,7 +3548,40 @@ __global__ void k_wild_split(const uint64_t* __restrict__ rec, const float* __re
     scores[i] = w[k];
 }
 
+__global__ void k_rank_fill(const uint32_t* __restrict__ post, const uint2* __restrict__ tk, uint32_t n_short,
+                            uint64_t n, uint32_t* __restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = tk[n_short + post[i]].x;
+}
+
 }  // namespace
+
+hipError_t build_rank_post(const uint64_t* gram_off, uint32_t n_seg, const uint32_t* post, uint64_t n_post,
+                           const uint2* tk, uint32_t n_short, uint32_t n_keys, uint32_t* out, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(out + n_post, 0, 4 * sizeof(uint32_t), s);  // the 16-byte pad
+    if (e != hipSuccess || !n_post) return e;
+    if (n_post > 0x7FFFFFFFull) return hipErrorNotSupported;  // hipcub's int item count
+    uint32_t* a = nullptr;
+    void* temp = nullptr;
+    size_t bytes = 0;
+    const int bits = n_keys > 1 ? 32 - __builtin_clz(n_keys - 1) : 1;
+    e = hipcub::DeviceSegmentedRadixSort::SortKeys(nullptr, bytes, a, out, (int)n_post, (int)n_seg, gram_off,
+                                                    gram_off + 1, 0, bits, s);
+    if (e == hipSuccess) e = hipMalloc(&a, sizeof(uint32_t) * n_post);
+    if (e == hipSuccess) e = hipMalloc(&temp, std::max<size_t>(bytes, 1));
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_rank_fill, dim3((uint32_t)((n_post + 255) / 256)), dim3(256), 0, s, post, tk, n_short,
+                           n_post, a);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess)
+        e = hipcub::DeviceSegmentedRadixSort::SortKeys(temp, bytes, a, out, (int)n_post, (int)n_seg, gram_off,
+                                                        gram_off + 1, 0, bits, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    hipFree(a);
+    hipFree(temp);
+    return e;
+}
 
 hipError_t build_wildcard(const float* d_w, uint32_t n_keys, uint32_t* d_keys, float* d_scores, hipStream_t s) {
     if (!n_keys) return hipSuccess;

@@ -94,3 +94,54 @@ def test_cmin1_ones_and_short_routing(alphabet, rows, lo, hi, qlen):
             else:
                 assert st["full_queries"] == len(qs), st
     gi.dispose()
+
+
+def _digest_flags(gi):
+    import ctypes as C
+    from stringsearchlib_amd import _native
+    out = (C.c_uint64 * 17)()
+    assert _native.lib().ngsIndexDigest(gi.handle, out, 17) == 17
+    return out[16]
+
+
+@pytest.mark.parametrize("weight", [None, 0.5, 0.0, -2.0, 1e-45])
+@pytest.mark.parametrize("alphabet,rows,lo,hi,qlen", [
+    (b"ABCDEFGHIJKLMNOPQRSTUVWXYZ", 60000, 8, 24, 12),  # C2's shape: thousands of one-hit terms
+    (b"ABC", 20000, 6, 20, 10),                          # repeated grams in every query and key
+])
+def test_cmin1_rank_lists(alphabet, rows, lo, hi, qlen, weight):
+    """Threshold 0 on an index with one weight (NULL weights: 1.0), one pair per term and one term
+    per key: tier 1a counts only the multi-hit terms (cmin 2) and k_emit takes the one-hit records
+    from the first `limit` key ranks of each list (DevIndex.rank_post, emit_rank_prefix). Exact vs the
+    oracle and vs the same index without rank lists (NGS_NO_RANK_LISTS, part_ones), for weights that
+    make every count tie (0, negative, a subnormal that underflows) as well as ordinary ones."""
+    import os
+    rng = random.Random(rows + qlen + len(alphabet))
+    words = list(dict.fromkeys(_words(rng, alphabet, rows, lo, hi)))  # one term per key
+    wts = None if weight is None else [weight] * len(words)
+    gi = ssl.StringIndex(words, 1, wts)
+    os.environ["NGS_NO_RANK_LISTS"] = "1"
+    try:
+        gp = ssl.StringIndex(words, 1, wts)
+    finally:
+        del os.environ["NGS_NO_RANK_LISTS"]
+    assert _digest_flags(gi) & 8 and not _digest_flags(gp) & 8
+    gi.set_timing(True)
+    gp.set_timing(True)
+    oi = OracleIndex(words, 1, wts)
+    qs = _queries(rng, words, 48, qlen) + [b"ABCABCABCABC", b"AAAAAAAAAAAA", b"ZZZZZZZZZZZZ"]
+    for limit in (100, 10, 1, 128):
+        got = gi.score_batch(qs, 0.0, limit)
+        st = gi.last_stats()
+        plain = gp.score_batch(qs, 0.0, limit)
+        stp = gp.last_stats()
+        for q, g, p in zip(qs, got, plain):
+            ref = oi.score(q, 0.0, limit)
+            assert len(g) == len(ref), f"q={q!r} limit={limit}: {len(g)} vs {len(ref)}"
+            for i, ((k1, s1), (k2, s2)) in enumerate(zip(g, ref)):
+                assert k1 == k2 and bits(s1) == bits(s2), f"q={q!r} limit={limit} #{i}: {k1!r}|{s1} vs {k2!r}|{s2}"
+            assert g == p, f"q={q!r} limit={limit}: rank lists differ from part_ones"
+        if len(alphabet) > 3:  # the multi-hit terms only reach the survivor slots
+            assert st["survivors"] * 4 < stp["survivors"], (st, stp)
+    gi.dispose()
+    gp.dispose()
