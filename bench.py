@@ -41,7 +41,8 @@ CONFIGS = {
                workload="C3: 10M-row ASCII corpus, gSize=3, rowSize=1, per-row float weights, "
                         "batch=65536/GPU, threshold=0.3, limit=100"),
     # BASELINE.json configs[1]
-    "c2": dict(rows=1_000_000, batch=4096, threshold=0.0, limit=100, weights=False,
+    # (three batches in flight: a 4,096-query batch is a few waves per CU)
+    "c2": dict(rows=1_000_000, batch=4096, threshold=0.0, limit=100, weights=False, depth=3,
                workload="C2: 1M-row ASCII corpus, gSize=3, weight=NULL, batch=4096/GPU, threshold=0, limit=100"),
     # BASELINE.json configs[3] (our indexW/gSize extension, parity unpinned). With gSize 2 over the
     # 37-symbol alphabet a list holds ~440k postings and a 12-character query reads ~4.7M (19 MB),
@@ -381,8 +382,9 @@ def main():
     ap.add_argument("--batch", type=int, default=None, help="override per-GPU batch (debug only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-dropin", action="store_true", help="skip the scoreBatch / score() latency lines")
-    ap.add_argument("--depth", type=int, default=2,
-                    help="batches in flight (ngsSearchDeviceAsync); 1 = one blocking ngsSearchDevice per step")
+    ap.add_argument("--depth", type=int, default=None,
+                    help="batches in flight (ngsSearchDeviceAsync; default 2, C2 3); 1 = one blocking "
+                         "ngsSearchDevice per step")
     args = ap.parse_args()
     cfg = dict(CONFIGS[args.config])
     if args.rows:
@@ -420,7 +422,7 @@ def main():
         d_raw = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(dev)
         d_off = torch.tensor(offs, dtype=torch.int64, device=dev)
     stride = min(cfg["limit"], n_keys)
-    depth = max(1, args.depth)
+    depth = max(1, args.depth if args.depth is not None else cfg.get("depth", 2))
     L.ngsSetTiming(h, 1)
     loop = StepLoop(L, h, d_raw, d_off, B, cfg["threshold"], cfg["limit"], stride, depth, world, dev,
                     torch.cuda.current_stream(dev).cuda_stream)

@@ -272,8 +272,8 @@ struct Context {
         for (hipEvent_t e : {fork, join, join2, prep_ev, lists_ev, in_ev})
             if (e) hipEventDestroy(e);
         if (stream) hipStreamDestroy(stream);
-        if (side) hipStreamDestroy(side);
-        if (side2 && side2 != side) hipStreamDestroy(side2);
+        if (side && side != stream) hipStreamDestroy(side);
+        if (side2 && side2 != side && side2 != stream) hipStreamDestroy(side2);
     }
 };
 
@@ -334,8 +334,8 @@ struct Replica {
         }
         auto c = std::make_unique<Context>();
         c->device = device;
+        // (the side streams are made by the first call whose batch needs them, queue_search)
         if (!HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) ||
-            !HIP_CHECK(make_side_stream(&c->side)) || !HIP_CHECK(make_second_side(c->side, &c->side2)) ||
             !HIP_CHECK(hipEventCreateWithFlags(&c->fork, hipEventDisableTiming)) ||
             !HIP_CHECK(hipEventCreateWithFlags(&c->join, hipEventDisableTiming)) ||
             !HIP_CHECK(hipEventCreateWithFlags(&c->join2, hipEventDisableTiming)) ||
@@ -942,18 +942,36 @@ int queue_search(Library& L, Replica& R, Context& c, const uint8_t* d_raw, const
     P.prec = c.d_prec;
     P.pcnt = c.d_pcnt;
     const bool timing = L.timing.load();
+    // A small batch is a few waves per CU of long per-query chains (C2: 4,096 queries, every one on
+    // the heavy list), so throughput comes from batches in flight, not from the main and side streams
+    // of one call overlapping: its side work goes on the call's own stream, in order, and a context
+    // that only ever runs such batches never makes its side streams. Three pipelined calls then hold
+    // three hardware queues (HIP maps streams to its four queues round-robin as they are made) instead
+    // of six streams sharing four (C2 28.6 -> 34.8 Mq/s at three in flight; NGS_ONE_STREAM_BATCH sets
+    // the size, 0 turns it off)
+    static const uint32_t one_stream_batch = [] {
+        const char* e = std::getenv("NGS_ONE_STREAM_BATCH");
+        return e ? (uint32_t)std::strtoul(e, nullptr, 0) : kOneStreamBatch;
+    }();
+    hipStream_t side = s, side2 = s;
+    if (B > one_stream_batch) {
+        if (!c.side && !HIP_CHECK(make_side_stream(&c.side))) return -4;
+        if (!c.side2 && !HIP_CHECK(make_second_side(c.side, &c.side2))) return -4;
+        side = c.side;
+        side2 = c.side2;
+    }
     // statistics, path counts and list counters
     if (!small && !HIP_CHECK(hipMemsetAsync(c.d_stats, 0, sizeof(DevStats) * (kStatSlots + 1 + 2 * kListSlots), s)))
         return -4;
     if (timing) HIP_CHECK(hipEventRecord(c.ev[0], s));
     if (!HIP_CHECK(launch_prep(d_raw, d_off, B, P, c.d_norm, c.d_qm, R.dev.csize, R.dev, c.d_heavy, gc + 3, c.d_full,
-                               gc + 5, c.d_lslots, c.d_lctr, s, c.side, c.prep_ev, c.lists_ev)))
+                               gc + 5, c.d_lslots, c.d_lctr, s, side, c.prep_ev, c.lists_ev)))
         return -4;
     if (timing) HIP_CHECK(hipEventRecord(c.ev[1], s));
     if (timing) HIP_CHECK(hipEventRecord(c.ev[2], s));
     if (!HIP_CHECK(launch_fast(R.dev, P, c.d_norm, d_off, c.d_qm, d_n, d_k, d_s, c.d_list2, gc + 1, c.d_fb, gc + 2,
-                               c.d_fb2, gc + 4, c.d_heavy, gc + 3, c.d_full, gc + 5, c.d_glist, gc, sd, s, c.side,
-                               c.side2, c.fork, c.join, c.join2, c.lists_ev)))
+                               c.d_fb2, gc + 4, c.d_heavy, gc + 3, c.d_full, gc + 5, c.d_glist, gc, sd, s, side,
+                               side2, c.fork, c.join, c.join2, c.lists_ev)))
         return -4;
     if (timing) HIP_CHECK(hipEventRecord(c.ev[3], s));
     // the statistics and the path counts in one read-back (the general path adds no statistics)

@@ -175,6 +175,10 @@ constexpr bool kHeavyLean = NGS_HEAVY_LEAN != 0;
 #define NGS_LEAN_SHRINK2 1
 #endif
 constexpr uint32_t kLeanShrink2 = NGS_LEAN_SHRINK2;  // tier 1a cmin-2 sketch parts: cap and target >> this
+#ifndef NGS_RANK_SHRINK
+#define NGS_RANK_SHRINK NGS_LEAN_SHRINK2
+#endif
+constexpr uint32_t kRankShrink = NGS_RANK_SHRINK;    // ... of threshold-0 queries on rank lists
 #ifndef NGS_LEAN_ONES
 #define NGS_LEAN_ONES 1
 #endif
@@ -184,6 +188,7 @@ constexpr bool kLeanOnes = NGS_LEAN_ONES != 0;
 #define NGS_ONES_SHRINK 2
 #endif
 constexpr uint32_t kOnesShrink = NGS_ONES_SHRINK;  // ... in parts of a quarter of the sketch cap
+constexpr uint32_t kOneStreamBatch = 16384;     // batches up to this size run on one stream per call
 constexpr uint32_t kHeavyWaves = 1;             // ... on this many waves per query
 constexpr uint32_t kHeavyGrid = 4096;           // ... by this many workgroups (grid-stride)
 constexpr bool kSidePriority = false;           // ... on a highest-priority stream
@@ -207,6 +212,9 @@ constexpr int kWaveSurv = 128;                  // survivor list (term, count) b
 #define NGS_EMIT_CAP 1024
 #endif
 constexpr uint32_t kEmitCap = NGS_EMIT_CAP;
+// threshold-0 queries on rank lists (DevIndex.rank_post): tier 1a leaves the query's lists for k_emit
+// in the last slots of its survivor slots, per list lane the posting offset (2 x u32) and the length
+constexpr uint32_t kRankInfo = 3 * 64;
 // batches up to kEmitWideBatch queries get kEmitCapWide slots per query (5 bytes each): a
 // threshold-0 query has thousands of one-hit survivors at C2 (part_ones)
 constexpr uint32_t kEmitCapWide = 4096;

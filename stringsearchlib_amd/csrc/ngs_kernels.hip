@@ -2261,7 +2261,8 @@ __device__ __forceinline__ void lean_query(WaveSmem<1, true>& S, const uint32_t 
     const unsigned long long pm = __ballot(lane <= n && lane > 0 && !(sc_long < P.thr));
     // threshold 0 with rank lists: the multi-hit terms only, k_emit adds the one-hit records
     // (emit_rank_prefix)
-    const uint32_t cmin = pm ? (X.rank_post && (pm & 2ull) ? 2u : (uint32_t)(__ffsll((long long)pm) - 1)) : 1000u;
+    const bool rank = X.rank_post && (pm & 2ull);
+    const uint32_t cmin = pm ? (rank ? 2u : (uint32_t)(__ffsll((long long)pm) - 1)) : 1000u;
     // heavy_class() lists these for launches of their own (same test, same cmin)
     if (!P.lean_all && (cmin <= kHeavyCmin || (m < X.short_query_len && X.n_short))) return;
     if (m < X.short_query_len && X.n_short) { bail(); return; }  // short search: tier 1b
@@ -2308,9 +2309,17 @@ __device__ __forceinline__ void lean_query(WaveSmem<1, true>& S, const uint32_t 
     constexpr bool kG4 = NGS_LEAN_G4 || ONES;  // list chunk bases in LDS (lean_stage)
     if (p_total && cmin <= n && !sketch && !ones) { bail(); return; }  // exact counting: tier 1b
     uint32_t surv_n = 0, spilled = 0;
+    // rank lists: the query's lists for k_emit (emit_rank_prefix) in its last kRankInfo slots
+    const uint32_t ecap_q = P.ecap - (rank ? kRankInfo : 0u);
+    if (rank) {
+        uint32_t* ri = P.est + (size_t)q * P.ecap + ecap_q;
+        ri[lane] = (uint32_t)gbase;
+        ri[64 + lane] = (uint32_t)(gbase >> 32);
+        ri[128 + lane] = min(glen, L);
+    }
     // the LDS survivor list to this query's kEmitCap slots in HBM; false if they are full
     auto spill = [&]() -> bool {
-        if (spilled + surv_n > P.ecap) return false;
+        if (spilled + surv_n > ecap_q) return false;
         uint32_t qs = q, l0 = lane;  // opaque: the slot pointers are made here, not kept (and spilled)
         asm volatile("" : "+s"(qs), "+v"(l0));
         uint32_t* et = P.est + (size_t)qs * P.ecap + spilled;
@@ -2328,8 +2337,18 @@ __device__ __forceinline__ void lean_query(WaveSmem<1, true>& S, const uint32_t 
         if (lane == 0 && !(P.dbg & 32u)) atomicAdd(&stats[q & (kStatSlots - 1)].slot_full, 1u);
     };
     if (p_total && cmin <= n) {
-        // cmin 2: every colliding pair is a false candidate, so those parts are cut at half the size
-        const uint32_t shrink = ones ? kOnesShrink : cmin == 2 ? kLeanShrink2 : 0u;
+        // cmin 2: every colliding pair is a false candidate, so those parts are cut at half the size;
+        // a gram the query repeats makes every term of its list a candidate, so a list held by mu
+        // lanes cuts them further (the part's candidates stay within the 64 a part resolves)
+        uint32_t shrink = ones ? kOnesShrink : cmin == 2 ? (rank ? kRankShrink : kLeanShrink2) : 0u;
+        if (cmin == 2) {
+            uint32_t mu = 0;
+            for (uint32_t k = 0; k < ng; ++k)
+                mu += gbase == (((uint64_t)__builtin_amdgcn_readlane((uint32_t)(gbase >> 32), (int)k) << 32) |
+                                __builtin_amdgcn_readlane((uint32_t)gbase, (int)k)) ? 1u : 0u;
+            const unsigned long long dup = __ballot(lane < ng && mu >= 2), dup3 = __ballot(lane < ng && mu >= 3);
+            shrink += (dup ? 1u : 0u) + (dup3 ? 1u : 0u);
+        }
         const uint32_t kChunks = (uint32_t)kWaveChunks >> shrink;  // part cap in 16-byte chunks
         const uint32_t K = X.n_buckets, span = X.bucket_span;
         const uint32_t wmax = (uint32_t)max64(1, min64(K, kMaxPartSpan / max(span, 1u)));
@@ -2713,7 +2732,8 @@ __device__ __forceinline__ void lean_query_g(WaveSmem<1, true>& S, const uint32_
     const unsigned long long pm = __ballot(lane <= n && lane > 0 && !(sc_long < P.thr));
     // threshold 0 with rank lists: the multi-hit terms only, k_emit adds the one-hit records
     // (emit_rank_prefix)
-    const uint32_t cmin = pm ? (X.rank_post && (pm & 2ull) ? 2u : (uint32_t)(__ffsll((long long)pm) - 1)) : 1000u;
+    const bool rank = X.rank_post && (pm & 2ull);
+    const uint32_t cmin = pm ? (rank ? 2u : (uint32_t)(__ffsll((long long)pm) - 1)) : 1000u;
     // heavy_class() lists these for launches of their own (same test, same cmin)
     if (!P.lean_all && (cmin <= kHeavyCmin || (m < X.short_query_len && X.n_short))) return;
     if (m < X.short_query_len && X.n_short) { bail(); return; }  // short search: tier 1b
@@ -2759,9 +2779,17 @@ __device__ __forceinline__ void lean_query_g(WaveSmem<1, true>& S, const uint32_
     const bool ones = ONES && cmin == 1;  // part_ones (the heavy list's launch only)
     if (p_total && cmin <= n && !sketch && !ones) { bail(); return; }  // exact counting: tier 1b
     uint32_t surv_n = 0, spilled = 0;
+    // rank lists: the query's lists for k_emit (emit_rank_prefix) in its last kRankInfo slots
+    const uint32_t ecap_q = P.ecap - (rank ? kRankInfo : 0u);
+    if (rank) {
+        uint32_t* ri = P.est + (size_t)q * P.ecap + ecap_q;
+        ri[lane] = (uint32_t)gbase;
+        ri[64 + lane] = (uint32_t)(gbase >> 32);
+        ri[128 + lane] = min(glen, L);
+    }
     // the LDS survivor list to this query's kEmitCap slots in HBM; false if they are full
     auto spill = [&]() -> bool {
-        if (spilled + surv_n > P.ecap) return false;
+        if (spilled + surv_n > ecap_q) return false;
         uint32_t qs = q, l0 = lane;  // opaque: the slot pointers are made here, not kept (and spilled)
         asm volatile("" : "+s"(qs), "+v"(l0));
         uint32_t* et = P.est + (size_t)qs * P.ecap + spilled;
@@ -3152,6 +3180,7 @@ struct EmitSmem {
     __device__ __forceinline__ uint64_t* cand() { return cand_own; }
     uint32_t q[kWaveMaxGrams + 8];
     uint32_t kset[2 * kWaveMaxLimit];  // emit_rank_prefix: the keys of the multi-hit top-L
+    uint32_t rstage[8 * 64];            // ... and the ranks of the lists in flight (kRankLoads)
 };
 
 // The one-hit records of a threshold-0 query's top-L (DevIndex.rank_post; tier 1a counted the query
@@ -3164,60 +3193,90 @@ struct EmitSmem {
 // records pass tau (ascending ranks: the rest are worse). An entry whose term is multi-hit is a
 // duplicate of its real record: dropped when that record is among the multi-hit top-L (kset), and
 // worse than tau otherwise.
-template <bool RADIX>
-__device__ void emit_rank_prefix(EmitSmem& S, const DevIndex& X, const SearchParams& P, uint32_t n, uint32_t L,
-                                 float sc_long, uint32_t& cand_n, uint64_t& tau) {
+constexpr int kRankLoads = 8;  // lists whose next 64 ranks are in flight at once
+
+// loads of offsets o .. o + 63 of up to kRankLoads lists of `todo` (lowest first, removed from it);
+// returns the lists taken
+__device__ __forceinline__ unsigned long long rank_issue(const DevIndex& X, uint64_t gbase, uint32_t glen,
+                                                         unsigned long long& todo, uint32_t o,
+                                                         uint32_t (&r)[kRankLoads]) {
     const uint32_t lane = lane_id();
-    wave_flush<RADIX>(S, cand_n, tau, L, true);  // the multi-hit top-L (<= L records)
-    constexpr uint32_t kSet = 2 * kWaveMaxLimit, kEmpty = 0xFFFFFFFFu;
-    auto slot = [](uint32_t k) -> uint32_t { return (k * 0x9E3779B1u) >> (32 - 8); };
-    static_assert(kSet == 256, "8-bit set slots");
-    for (uint32_t i = lane; i < kSet; i += 64) S.kset[i] = kEmpty;
-    wave_sync();
-    if (lane < cand_n) {
-        const uint32_t k = (uint32_t)S.cand()[lane], k2 = lane + 64 < cand_n ? (uint32_t)S.cand()[lane + 64] : kEmpty;
-        for (uint32_t h = slot(k);; h = (h + 1) & (kSet - 1))
-            if (atomicCAS(&S.kset[h], kEmpty, k) == kEmpty) break;
-        if (k2 != kEmpty)
-            for (uint32_t h = slot(k2);; h = (h + 1) & (kSet - 1))
-                if (atomicCAS(&S.kset[h], kEmpty, k2) == kEmpty) break;
-    }
-    wave_sync();
-    // this lane's gram occurrence: its list (a repeated gram's list twice: its terms are multi-hit)
-    uint64_t gbase = 0;
-    uint32_t glen = 0;
-    if (lane < n) {
-        const uint32_t code = gram_at(X, [&](uint32_t i) { return S.q[i]; }, lane);
-        if (code != UINT32_MAX) {
-            gbase = X.gram_off[code];
-            glen = (uint32_t)min64(X.gram_off[code + 1] - gbase, (uint64_t)L);
+    unsigned long long taken = 0;
+#pragma unroll
+    for (int u = 0; u < kRankLoads; ++u) {
+        r[u] = 0;
+        if (todo) {
+            const uint32_t j = (uint32_t)__ffsll((long long)todo) - 1u;
+            todo &= todo - 1;
+            taken |= 1ull << j;
+            const uint32_t len = __builtin_amdgcn_readlane(glen, (int)j);
+            const uint64_t b = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(gbase >> 32), (int)j) << 32) |
+                               __builtin_amdgcn_readlane((uint32_t)gbase, (int)j);
+            if (o + lane < len) r[u] = X.rank_post[b + o + lane];
         }
     }
-    const float sc = __uint_as_float(X.w_uniform) * __shfl(sc_long, 1);  // pair_enc of one hit
-    const uint32_t enc1 = sc > 0.0f ? __float_as_uint(sc) + 1u : 1u;
+    return taken;
+}
+
+template <bool RADIX>
+__device__ __forceinline__ void emit_rank_prefix(EmitSmem& S, const DevIndex& X, uint32_t L, uint32_t enc1,
+                                                 uint64_t gbase, uint32_t glen, uint32_t& cand_n, uint64_t& tau) {
+    const uint32_t lane = lane_id();
+    if (cand_n > L) wave_trim<RADIX>(S, cand_n, tau, L, true);  // the multi-hit top-L, unsorted
+    constexpr uint32_t kSet = 2 * kWaveMaxLimit, kEmpty = 0xFFFFFFFFu;
+    static_assert(kSet == 256, "8-bit set slots");
+    static_assert(sizeof(S.rstage) == sizeof(uint32_t) * 64 * kRankLoads, "staging for kRankLoads lists");
+    auto slot = [](uint32_t k) -> uint32_t { return (k * 0x9E3779B1u) >> (32 - 8); };
+    auto insert = [&](uint32_t k) {
+        for (uint32_t h = slot(k);; h = (h + 1) & (kSet - 1))
+            if (atomicCAS(&S.kset[h], kEmpty, k) == kEmpty) break;
+    };
+    for (uint32_t i = lane; i < kSet; i += 64) S.kset[i] = kEmpty;
+    wave_sync();
+    if (lane < cand_n) insert((uint32_t)S.cand()[lane]);
+    if (lane + 64 < cand_n) insert((uint32_t)S.cand()[lane + 64]);
+    wave_sync();
     const uint64_t hi = (uint64_t)(~enc1) << 32;
-    for (uint32_t j = 0; j < n; ++j) {
-        const uint32_t len = __builtin_amdgcn_readlane(glen, (int)j);
-        const uint64_t b = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(gbase >> 32), (int)j) << 32) |
-                           __builtin_amdgcn_readlane((uint32_t)gbase, (int)j);
-        for (uint32_t o = 0; o < len; o += 64) {
-            const uint32_t i = o + lane;
-            const uint64_t rec = i < len ? hi | X.rank_post[b + i] : kNoCand;
-            if (!__ballot(rec < tau)) break;  // ascending: the rest of the list is worse too
-            bool want = rec < tau;
-            if (want) {
-                const uint32_t k = (uint32_t)rec;
-                for (uint32_t h = slot(k);; h = (h + 1) & (kSet - 1)) {
-                    const uint32_t v = S.kset[h];
-                    if (v == k) { want = false; break; }
-                    if (v == kEmpty) break;
-                }
+    unsigned long long alive = __ballot(glen != 0);
+    for (uint32_t o = 0; o < L && alive; o += 64) {
+        unsigned long long todo = alive & __ballot(glen > o);
+        while (todo) {
+            // offsets o .. o + 63 of up to kRankLoads lists in flight at once, staged in LDS (no
+            // registers live across the buffer trims below)
+            unsigned long long taken;
+            {
+                uint32_t r[kRankLoads];
+                taken = rank_issue(X, gbase, glen, todo, o, r);
+#pragma unroll
+                for (int u = 0; u < kRankLoads; ++u) S.rstage[64 * u + lane] = r[u];
+                wave_sync();
             }
-            if (cand_n + 64 > (uint32_t)kWaveCand) wave_trim<RADIX>(S, cand_n, tau, L, true);
-            want = want && rec < tau;
-            const unsigned long long bw = __ballot(want);
-            if (want) S.cand()[cand_n + rank_below(bw)] = rec;
-            cand_n += __popcll(bw);
+#pragma unroll 1
+            for (uint32_t u = 0; taken; ++u) {
+                const uint32_t j = (uint32_t)__ffsll((long long)taken) - 1u;
+                taken &= taken - 1;
+                const uint32_t len = __builtin_amdgcn_readlane(glen, (int)j);
+                const uint64_t rec = o + lane < len ? hi | S.rstage[64 * u + lane] : kNoCand;
+                if (!__ballot(rec < tau)) {  // ascending: the rest of the list is worse too
+                    alive &= ~(1ull << j);
+                    continue;
+                }
+                bool want = rec < tau;
+                if (want) {
+                    const uint32_t k = (uint32_t)rec;
+                    for (uint32_t h = slot(k);; h = (h + 1) & (kSet - 1)) {
+                        const uint32_t v = S.kset[h];
+                        if (v == k) { want = false; break; }
+                        if (v == kEmpty) break;
+                    }
+                }
+                if (cand_n + 64 > (uint32_t)kWaveCand) wave_trim<RADIX>(S, cand_n, tau, L, true);
+                want = want && rec < tau;
+                const unsigned long long bw = __ballot(want);
+                if (want) S.cand()[cand_n + rank_below(bw)] = rec;
+                cand_n += __popcll(bw);
+            }
+            wave_sync();  // the staging is read before the next lists' ranks overwrite it
         }
     }
 }
@@ -3240,6 +3299,14 @@ __device__ __forceinline__ void emit_query(EmitSmem& S, const uint32_t q, const 
     uint32_t t = et[lane], code = ec[lane];
     uint32_t sn = P.esn[q];
     const uint32_t m = qm[q];
+    // rank lists: the query's lists as tier 1a left them (emit_rank_prefix), in the same round trip
+    uint64_t gbase = 0;
+    uint32_t glen = 0;
+    if (RADIX && X.rank_post) {
+        const uint32_t* ri = et + (P.ecap - kRankInfo);
+        gbase = ((uint64_t)ri[64 + lane] << 32) | ri[lane];
+        glen = ri[128 + lane];
+    }
     if (sn == kNoEmit) return;  // tier 1a did not finish this query
     // the main launch leaves the heavy launch's queries to the heavy list's k_emit
     if (!heavy_launch && (sn & kEmitHeavy)) return;
@@ -3251,6 +3318,9 @@ __device__ __forceinline__ void emit_query(EmitSmem& S, const uint32_t q, const 
     uint64_t tau = kNoCand;
     // the query's characters only for an exact-match test (a survivor scoring > 0.999), rare
     bool have_q = false;
+    // threshold 0 with rank lists (emit_rank_prefix; cmin-1 queries are on the heavy list, whose
+    // launch is the RADIX one)
+    const bool rank_mode = RADIX && X.rank_post && !(__shfl(sc_long, 1) < P.thr);
     // one pair per term (DevIndex.tk_identity): a software pipeline over the batches of 64: while
     // batch b is scored, the pairs of batches b + 1 .. b + D and the survivors of batches up to
     // b + 2D + 1 are in flight (a threshold-0 query has thousands of survivors, and a batch is
@@ -3351,13 +3421,9 @@ __device__ __forceinline__ void emit_query(EmitSmem& S, const uint32_t q, const 
     }
     // threshold 0 with rank lists: tier 1a counted this query at cmin 2 (its multi-hit terms, above);
     // its one-hit records come from the first L key ranks of each of its lists
-    if (X.rank_post && !(__shfl(sc_long, 1) < P.thr)) {
-        if (!have_q) {
-            const uint8_t* qg = qnorm + qoff[q];
-            for (uint32_t k = lane; k < m; k += 64) S.q[k] = char_at(qg, k, X.csize);
-            wave_sync();
-        }
-        emit_rank_prefix<RADIX>(S, X, P, n, L, sc_long, cand_n, tau);
+    if (rank_mode) {
+        const float sc1 = __uint_as_float(X.w_uniform) * __shfl(sc_long, 1);  // pair_enc of one hit
+        emit_rank_prefix<RADIX>(S, X, L, sc1 > 0.0f ? __float_as_uint(sc1) + 1u : 1u, gbase, glen, cand_n, tau);
     }
     wave_flush<RADIX>(S, cand_n, tau, L, X.keys_unique != 0);
     const size_t ob = (size_t)q * P.out_stride;
