@@ -209,6 +209,7 @@ struct Context {
     hipEvent_t prep_ev = nullptr, lists_ev = nullptr;  // k_prep done (s), heavy / full lists merged (side)
     hipEvent_t in_ev = nullptr;   // ngsSearchDeviceAsync: the caller's stream up to the call
     hipEvent_t ev[6] = {};
+    hipEvent_t piece_ev[kBackPieces] = {};  // finish_host_chunk: the read-back's pieces landed
     size_t qcap = 0, bcap = 0, ncap = 0, ocap = 0;
     uint32_t ecap = kEmitCap;  // survivor slots per query in d_est / d_esc (ensure_queries, emit_cap)
     uint32_t ecap_grow = 0;    // slots later calls ask for: raised when tier 1a ran out of them
@@ -270,6 +271,8 @@ struct Context {
         for (hipEvent_t e : ev)
             if (e) hipEventDestroy(e);
         for (hipEvent_t e : {fork, join, join2, prep_ev, lists_ev, in_ev})
+            if (e) hipEventDestroy(e);
+        for (hipEvent_t e : piece_ev)
             if (e) hipEventDestroy(e);
         if (stream) hipStreamDestroy(stream);
         if (side && side != stream) hipStreamDestroy(side);
@@ -345,6 +348,8 @@ struct Replica {
             return nullptr;
         for (hipEvent_t& e : c->ev)
             if (!HIP_CHECK(hipEventCreate(&e))) return nullptr;
+        for (hipEvent_t& e : c->piece_ev)
+            if (!HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming))) return nullptr;
         if (!dev_alloc(&c->d_group, 64) || !dev_alloc(&c->d_stats, kStatSlots + 1 + 2 * kListSlots) ||
             !dev_alloc(&c->d_sio, kSioBytes) ||
             !HIP_CHECK(hipMemsetAsync(c->d_sio, 0, kSioStats, c->stream)) ||
@@ -866,7 +871,7 @@ bool ensure_general(const Replica& R, Context& c, hipStream_t s) {
 // lists, no side streams; the latency path of score() and small batches).
 int queue_search(Library& L, Replica& R, Context& c, const uint8_t* d_raw, const uint64_t* d_off, uint32_t B,
                  uint64_t qbytes, float thr, uint32_t limit, uint32_t stride, uint32_t* d_n, uint32_t* d_k,
-                 float* d_s, hipStream_t s, SearchParams& P, bool small) {
+                 float* d_s, hipStream_t s, SearchParams& P, bool small, bool defer_heavy = false) {
     // small: the statistics go to the latency block (zeroed by k_prep, read back by the caller
     // together with the results)
     DevStats* sd = small ? reinterpret_cast<DevStats*>(c.d_sio) : c.d_stats;
@@ -971,7 +976,7 @@ int queue_search(Library& L, Replica& R, Context& c, const uint8_t* d_raw, const
     if (timing) HIP_CHECK(hipEventRecord(c.ev[2], s));
     if (!HIP_CHECK(launch_fast(R.dev, P, c.d_norm, d_off, c.d_qm, d_n, d_k, d_s, c.d_list2, gc + 1, c.d_fb, gc + 2,
                                c.d_fb2, gc + 4, c.d_heavy, gc + 3, c.d_full, gc + 5, c.d_glist, gc, sd, s, side,
-                               side2, c.fork, c.join, c.join2, c.lists_ev)))
+                               side2, c.fork, c.join, c.join2, c.lists_ev, defer_heavy)))
         return -4;
     if (timing) HIP_CHECK(hipEventRecord(c.ev[3], s));
     // the statistics and the path counts in one read-back (the general path adds no statistics)
@@ -1125,7 +1130,7 @@ bool queue_host_chunk(Library& L, Replica& R, Context& c, const CharT* const* qu
     if (!c.h_off.grow(sizeof(uint64_t) * (B + 1))) return false;
     uint64_t* ho = c.h_off.as<uint64_t>();
     ho[0] = 0;
-    parallel_ranges(B, 16384, [&](size_t a, size_t e) {
+    parallel_ranges(B, 8192, [&](size_t a, size_t e) {
         for (size_t i = a; i < e; ++i) ho[i + 1] = queries[q0 + i] ? str_len(queries[q0 + i]) * cs : 0;
     });
     for (uint32_t i = 0; i < B; ++i) ho[i + 1] += ho[i];
@@ -1153,7 +1158,7 @@ bool queue_host_chunk(Library& L, Replica& R, Context& c, const CharT* const* qu
     } else {
         if (!c.h_raw.grow(std::max<uint64_t>(qbytes, 1))) return false;
         uint8_t* hr = c.h_raw.as<uint8_t>();
-        parallel_ranges(B, 16384, [&](size_t a, size_t e) {
+        parallel_ranges(B, 8192, [&](size_t a, size_t e) {
             for (size_t i = a; i < e; ++i)
                 if (queries[q0 + i]) std::memcpy(hr + ho[i], queries[q0 + i], ho[i + 1] - ho[i]);
         });
@@ -1177,7 +1182,8 @@ bool queue_host_chunk(Library& L, Replica& R, Context& c, const CharT* const* qu
 
 // Completes a queued chunk: waits, runs the general path, reads back exactly the results
 // (packed on the device for large chunks), fills the chunk's counts and hands its records to
-// `emit(recs, scores, n, last)`: recs are u32 key ranks, or in pointer mode (h.pcs) u64 result
+// `emit(recs, scores, n, last, chunk_total)` (in pieces of the chunk's chunk_total records, in order):
+// recs are u32 key ranks, or in pointer mode (h.pcs) u64 result
 // pointers.
 template <class Emit>
 bool finish_host_chunk(Library& L, Replica& R, HostChunk& h, uint32_t Lm, std::vector<uint32_t>& counts, bool last,
@@ -1212,9 +1218,9 @@ bool finish_host_chunk(Library& L, Replica& R, HostChunk& h, uint32_t Lm, std::v
             const uint64_t* koff = L.host.key_off.data();
             std::vector<uint64_t> ptr(k.size());
             for (size_t i = 0; i < k.size(); ++i) ptr[i] = h.pbase + koff[k[i]] * h.pcs;
-            emit(static_cast<const void*>(ptr.data()), sc.data(), (uint32_t)k.size(), last);
+            emit(static_cast<const void*>(ptr.data()), sc.data(), (uint32_t)k.size(), last, (uint32_t)k.size());
         } else {
-            emit(static_cast<const void*>(k.data()), sc.data(), (uint32_t)k.size(), last);
+            emit(static_cast<const void*>(k.data()), sc.data(), (uint32_t)k.size(), last, (uint32_t)k.size());
         }
         return true;
     }
@@ -1231,17 +1237,34 @@ bool finish_host_chunk(Library& L, Replica& R, HostChunk& h, uint32_t Lm, std::v
     ht.mark("pack + offsets back");
     const uint32_t total = c.h_res.as<uint32_t>()[B];
     for (uint32_t i = 0; i < B; ++i) counts[q0 + i] = c.h_res.as<uint32_t>()[i + 1] - c.h_res.as<uint32_t>()[i];
-    const size_t rb = (h.pcs ? sizeof(uint64_t) : sizeof(uint32_t)) * (size_t)total;  // record bytes
-    if (!c.h_res.grow(rb + sizeof(float) * (size_t)total) ||
-        !HIP_CHECK(hipMemcpyAsync(c.h_res.p, c.d_pk, rb, hipMemcpyDeviceToHost, c.stream)) ||
-        !HIP_CHECK(hipMemcpyAsync(c.h_res.as<uint8_t>() + rb, c.d_ps, sizeof(float) * total, hipMemcpyDeviceToHost,
-                                  c.stream)) ||
-        !HIP_CHECK(hipStreamSynchronize(c.stream)))
-        return false;
-    ht.mark("records back");
-    // straight from the pinned buffer
-    emit(static_cast<const void*>(c.h_res.p), reinterpret_cast<const float*>(c.h_res.as<uint8_t>() + rb), total, last);
-    ht.mark("emit");
+    const size_t esz = h.pcs ? sizeof(uint64_t) : sizeof(uint32_t);
+    const size_t rb = esz * (size_t)total;  // record bytes
+    if (!c.h_res.grow(rb + sizeof(float) * (size_t)total)) return false;
+    // the records come back in pieces, each marshalled (straight from the pinned buffer) while the
+    // next ones are still on the link: the copy and the host's copy into the caller's arrays overlap
+    const uint32_t pieces = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(kBackPieces, total / kBackPieceMin));
+    const uint32_t per = (total + pieces - 1) / pieces;
+    uint8_t* hr = c.h_res.as<uint8_t>();
+    for (uint32_t i = 0; i < pieces; ++i) {
+        const size_t a = (size_t)i * per, n = std::min<size_t>(per, total - std::min<size_t>(total, a));
+        hipStream_t sp = c.stream;  // (pieces alternating over two streams measured slower: 0.47-0.62 ms)
+        if (n && !(HIP_CHECK(hipMemcpyAsync(hr + a * esz, reinterpret_cast<const uint8_t*>(c.d_pk) + a * esz, n * esz,
+                                            hipMemcpyDeviceToHost, sp)) &&
+                   HIP_CHECK(hipMemcpyAsync(hr + rb + a * sizeof(float), c.d_ps + a, n * sizeof(float),
+                                            hipMemcpyDeviceToHost, sp))))
+            return false;
+        if (!HIP_CHECK(hipEventRecord(c.piece_ev[i], sp))) return false;
+    }
+    for (uint32_t i = 0; i < pieces; ++i) {
+        const size_t a = (size_t)i * per, n = std::min<size_t>(per, total - std::min<size_t>(total, a));
+        if (!HIP_CHECK(hipEventSynchronize(c.piece_ev[i]))) {
+            (void)hipStreamSynchronize(c.stream);  // nothing may still write the buffer
+            return false;
+        }
+        emit(static_cast<const void*>(hr + a * esz), reinterpret_cast<const float*>(hr + rb) + a, (uint32_t)n, last,
+             total);
+    }
+    ht.mark("records back + emit");
     return true;
 }
 
@@ -1306,7 +1329,7 @@ bool host_search_one(Library& L, Replica& R, const CharT* const* queries, uint32
     keys.clear();
     scores.clear();
     return host_search_chunks(L, R, queries, nq, thr, Lm, counts, [&](const void* recs, const float* sc, uint32_t n,
-                                                                       bool) {
+                                                                       bool, uint32_t) {
         const uint32_t* k = static_cast<const uint32_t*>(recs);
         keys.insert(keys.end(), k, k + n);
         scores.insert(scores.end(), sc, sc + n);
@@ -1565,9 +1588,10 @@ uint32_t batch_query(uint32_t handle, const CharT* const* queries, uint32_t nq, 
         const uint64_t pbase = (uint64_t)(uintptr_t)L->host.key_bytes.data();
         static_assert(sizeof(CharT*) == sizeof(uint64_t), "result pointers are 64-bit");
         const bool ok = host_search_chunks(*L, *L->reps.front(), queries, nq, thr, Lm, cnt,
-                                           [&](const void* recs, const float* sc, uint32_t n, bool last) {
+                                           [&](const void* recs, const float* sc, uint32_t n, bool last,
+                                               uint32_t chunk_total) {
             if (!res) {
-                cap = (off == 0 && last) ? std::max<size_t>(n, 1) : (size_t)nq * Lm;
+                cap = (off == 0 && last) ? std::max<size_t>(chunk_total, 1) : (size_t)nq * Lm;
                 res = new CharT*[cap];
                 out_s = scores ? new float[cap] : nullptr;
             }
@@ -1903,8 +1927,20 @@ NGS_API int ngsSearchDeviceAsync(uint32_t handle, const uint8_t* dQueryBytes, co
             L->batches.fetch_sub(1, std::memory_order_acq_rel);
             return -4;
         }
+        // NGS_DEFER_HEAVY (experiment): 1 = the heavy chain waits for the main launch (launch_fast),
+        // -1 = when another batch is in flight. Measured on C3 at depth 2 in one box: 35.5-35.7 Mq/s
+        // either way against 36.5-36.6 with the chains side by side (the default, 0)
+        static const int defer_mode = [] {
+            const char* e = std::getenv("NGS_DEFER_HEAVY");
+            return e ? std::atoi(e) : 0;
+        }();
+        bool defer = defer_mode == 1;
+        if (defer_mode < 0) {
+            std::lock_guard<std::mutex> g(L->pend_mu);
+            defer = !L->pending.empty();
+        }
         pd.rc = queue_search(*L, *Rp, c, dQueryBytes, dQueryOffsets, nQueries, qbytes, threshold, Lm, outStride,
-                             dCounts, dKeys, dScores, c.stream, pd.P, false);
+                             dCounts, dKeys, dScores, c.stream, pd.P, false, defer);
     }
     std::lock_guard<std::mutex> g(L->pend_mu);
     *ticket = L->next_ticket++;

@@ -188,6 +188,8 @@ constexpr bool kLeanOnes = NGS_LEAN_ONES != 0;
 #define NGS_ONES_SHRINK 2
 #endif
 constexpr uint32_t kOnesShrink = NGS_ONES_SHRINK;  // ... in parts of a quarter of the sketch cap
+constexpr uint32_t kBackPieces = 4;              // host batches: records read back in up to this many pieces
+constexpr uint32_t kBackPieceMin = 131072;        // ... of at least this many records
 constexpr uint32_t kOneStreamBatch = 16384;     // batches up to this size run on one stream per call
 constexpr uint32_t kHeavyWaves = 1;             // ... on this many waves per query
 constexpr uint32_t kHeavyGrid = 4096;           // ... by this many workgroups (grid-stride)

@@ -3692,20 +3692,24 @@ int phase_stats(unsigned long long* out, int n, bool reset) {
 
 // The heavy and full lists from k_prep's slot lists: per list, a scan of the 64 slot counts,
 // then the slots' entries copied behind each other (slot order: the lists' order does not matter).
-__global__ __launch_bounds__(256) void k_lists(const uint32_t* __restrict__ slots, const uint32_t* __restrict__ ctr,
-                                               uint32_t cap, uint32_t* __restrict__ heavy, uint32_t* __restrict__ hcount,
-                                               uint32_t* __restrict__ full, uint32_t* __restrict__ fcount) {
-    __shared__ uint32_t base[2 * kListSlots + 2];
-    const uint32_t t = threadIdx.x, lane = t & 63u;
-    if (t < 128) {  // wave 0: heavy slots, wave 1: full slots
-        const uint32_t L = t >> 6, c = ctr[16 * (L * kListSlots + lane)];
+// One wave: it runs beside the main tier-1a launch, whose one-wave workgroups refill every wave slot
+// as they free up, so a larger workgroup (four free slots on one CU at once) waited ~1.2 ms for
+// room at C3 and held back the heavy list's launch behind it.
+__global__ __launch_bounds__(64) void k_lists(const uint32_t* __restrict__ slots, const uint32_t* __restrict__ ctr,
+                                              uint32_t cap, uint32_t* __restrict__ heavy, uint32_t* __restrict__ hcount,
+                                              uint32_t* __restrict__ full, uint32_t* __restrict__ fcount) {
+    __shared__ uint32_t base[2 * (kListSlots + 1)];
+    const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll
+    for (uint32_t L = 0; L < 2; ++L) {  // 0: heavy slots, 1: full slots
+        const uint32_t c = ctr[16 * (L * kListSlots + lane)];
         const uint32_t incl = wave_incl_scan(c);
         base[L * (kListSlots + 1) + lane + 1] = incl;
         if (lane == 0) base[L * (kListSlots + 1)] = 0;
         if (lane == 63) *(L ? fcount : hcount) = incl;
     }
     __syncthreads();
-    for (uint32_t sl = t >> 6; sl < 2 * kListSlots; sl += 4) {
+    for (uint32_t sl = 0; sl < 2 * kListSlots; ++sl) {
         const uint32_t L = sl / kListSlots, k = sl % kListSlots;
         const uint32_t b0 = base[L * (kListSlots + 1) + k], n = base[L * (kListSlots + 1) + k + 1] - b0;
         const uint32_t* src = slots + (size_t)sl * cap;
@@ -3759,7 +3763,7 @@ hipError_t launch_prep(const uint8_t* raw, const uint64_t* off, uint32_t B, cons
         hipError_t e;
         if ((e = hipEventRecord(prep_ev, s)) != hipSuccess || (e = hipStreamWaitEvent(side, prep_ev, 0)) != hipSuccess)
             return e;
-        hipLaunchKernelGGL(k_lists, dim3(1), dim3(256), 0, side, slots, ctr, cap, heavy, hcount, full, fcount);
+        hipLaunchKernelGGL(k_lists, dim3(1), dim3(64), 0, side, slots, ctr, cap, heavy, hcount, full, fcount);
         dbg_check(side, "k_lists");
         if ((e = hipEventRecord(lists_ev, side)) != hipSuccess) return e;
     }
@@ -3772,7 +3776,7 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
                        const uint32_t* heavy, const uint32_t* hcount, const uint32_t* full,
                        const uint32_t* fcount, uint32_t* glist, uint32_t* gcount, DevStats* stats, hipStream_t s,
                        hipStream_t side, hipStream_t side2, hipEvent_t fork, hipEvent_t join, hipEvent_t join2,
-                       hipEvent_t lists_ev) {
+                       hipEvent_t lists_ev, bool defer_heavy) {
     if (!P.n_queries) return hipSuccess;
     hipError_t e = hipSuccess;
     switch (P.waves) {  // waves per query (SearchParams.waves, NGS_WAVES; 0 = tier 1a + 1b)
@@ -3804,6 +3808,12 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
             // then the heavy list's chain on side, which is already ordered after k_prep with k_lists
             // queued on it (launch_prep): queued second, so that it starts soon after k_lists (the
             // host queues ~15 operations per call; at C2 this launch carries every query)
+            // defer_heavy: the heavy list's chain starts when the main launch has finished (a batch
+            // queued behind another one in flight: its main launch then has the GPU to itself, and the
+            // heavy chain runs beside the next batch's)
+            if (defer_heavy && kMainFirst && side != s &&
+                ((e = hipEventRecord(fork, s)) != hipSuccess || (e = hipStreamWaitEvent(side, fork, 0)) != hipSuccess))
+                return e;
             if (kHeavyLean) {
                 SearchParams PH = P;
                 PH.lean_all = 1;
@@ -3824,7 +3834,6 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
             }
             if ((e = hipEventRecord(join, side)) != hipSuccess) return e;
             // side2 waits for the lists
-            (void)fork;
             if ((e = hipStreamWaitEvent(side2, lists_ev, 0)) != hipSuccess) return e;
             if (P.heavy_waves == 4) {
                 hipLaunchKernelGGL(k_wave<4>, dim3(gh), dim3(256), 0, side2, X, P, qnorm, off, qm, out_n, out_k,
