@@ -191,6 +191,14 @@ constexpr uint32_t kOnesShrink = NGS_ONES_SHRINK;  // ... in parts of a quarter 
 constexpr uint32_t kBackPieces = 4;              // host batches: records read back in up to this many pieces
 constexpr uint32_t kBackPieceMin = 131072;        // ... of at least this many records
 constexpr uint32_t kOneStreamBatch = 16384;     // batches up to this size run on one stream per call
+#ifndef NGS_HEAVY_FUSE
+#define NGS_HEAVY_FUSE 0  // measured slower: C2 18.1-18.7 against 32.9-34.9 Mq/s, C3 30.7-32.1 against 34.6-35.5 (one box)
+#endif
+constexpr bool kHeavyFuse = NGS_HEAVY_FUSE != 0;  // the heavy list's lean launch and k_emit as one kernel (k_heavy)
+#ifndef NGS_HEAVY_FUSE_WPS
+#define NGS_HEAVY_FUSE_WPS 5
+#endif
+constexpr int kHeavyFuseWavesPerSimd = NGS_HEAVY_FUSE_WPS;  // ... its occupancy target (the emit needs ~97 VGPRs)
 constexpr uint32_t kHeavyWaves = 1;             // ... on this many waves per query
 constexpr uint32_t kHeavyGrid = 4096;           // ... by this many workgroups (grid-stride)
 constexpr bool kSidePriority = false;           // ... on a highest-priority stream

@@ -3464,6 +3464,44 @@ __global__ __launch_bounds__(64 * kEmitWaves) void k_emit(DevIndex X, SearchPara
     }
 }
 
+// The heavy list's launch with its k_emit fused (kHeavyFuse): each wave scores its query's survivors
+// (emit_query) right after counting them (lean_query), over the same LDS (the sketch table is dead by
+// then), so a query's calcScore and top-L overlap the other queries' counting instead of waiting for
+// the whole launch, and one launch and its drain leave the heavy chain (C2: every query).
+union HeavySmem {
+    WaveSmem<1, true> w;
+    EmitSmem e;
+};
+
+template <bool ONES>
+__global__ __launch_bounds__(64, kHeavyFuseWavesPerSimd) void k_heavy(DevIndex X, SearchParams P,
+                                                                     const uint8_t* __restrict__ qnorm,
+                                                                     const uint64_t* __restrict__ qoff,
+                                                                     const uint32_t* __restrict__ qm,
+                                                                     uint32_t* __restrict__ out_n,
+                                                                     uint32_t* __restrict__ out_k,
+                                                                     float* __restrict__ out_s,
+                                                                     uint32_t* __restrict__ list2,
+                                                                     uint32_t* __restrict__ count2,
+                                                                     DevStats* __restrict__ stats,
+                                                                     uint32_t* __restrict__ fb, uint32_t* __restrict__ fbc,
+                                                                     const uint32_t* __restrict__ qlist,
+                                                                     const uint32_t* __restrict__ qcount) {
+    __shared__ HeavySmem U;
+    const uint32_t cnt = *qcount;  // the heavy list, grid-stride
+    for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
+        const uint32_t q = qlist[i];
+        if constexpr (NGS_LEAN_GROUPS == 2)
+            lean_query_g<ONES>(U.w, q, X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats, fb, fbc);
+        else
+            lean_query<ONES>(U.w, q, X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats, fb, fbc);
+        wave_sync();
+        __threadfence();  // the survivor slots and the count written above are read back below
+        emit_query<true, NGS_EMIT_DEPTH>(U.e, q, true, X, P, qnorm, qoff, qm, out_n, out_k, out_s, stats);
+        wave_sync();
+    }
+}
+
 // Joins the slices of sliced tier 1b (SearchParams.prec / pcnt): per query of the list, the
 // slices' top-L records through the running top-L (key-max dedup, tau pruning), then results.
 __global__ __launch_bounds__(64) void k_merge(DevIndex X, SearchParams P, const uint32_t* __restrict__ qlist,
@@ -3817,12 +3855,18 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
             if (kHeavyLean) {
                 SearchParams PH = P;
                 PH.lean_all = 1;
-                hipLaunchKernelGGL((k_wave_lean<true, kLeanOnes>), dim3(gh), dim3(64), 0, side, X, PH, qnorm, off, qm, out_n,
-                                   out_k, out_s, list2, count2, stats, fb2, fbc2, heavy, hcount);
-                dbg_check(side, "k_wave_lean (heavy list)");
-                hipLaunchKernelGGL(k_emit<true>, dim3((gh + kEmitWaves - 1) / kEmitWaves), dim3(64 * kEmitWaves), 0, side,
-                                   X, PH, qnorm, off, qm, out_n, out_k, out_s, stats, heavy, hcount);
-                dbg_check(side, "k_emit (heavy list)");
+                if (kHeavyFuse) {
+                    hipLaunchKernelGGL((k_heavy<kLeanOnes>), dim3(gh), dim3(64), 0, side, X, PH, qnorm, off, qm, out_n,
+                                       out_k, out_s, list2, count2, stats, fb2, fbc2, heavy, hcount);
+                    dbg_check(side, "k_heavy (heavy list)");
+                } else {
+                    hipLaunchKernelGGL((k_wave_lean<true, kLeanOnes>), dim3(gh), dim3(64), 0, side, X, PH, qnorm, off, qm,
+                                       out_n, out_k, out_s, list2, count2, stats, fb2, fbc2, heavy, hcount);
+                    dbg_check(side, "k_wave_lean (heavy list)");
+                    hipLaunchKernelGGL(k_emit<true>, dim3((gh + kEmitWaves - 1) / kEmitWaves), dim3(64 * kEmitWaves), 0,
+                                       side, X, PH, qnorm, off, qm, out_n, out_k, out_s, stats, heavy, hcount);
+                    dbg_check(side, "k_emit (heavy list)");
+                }
                 hipLaunchKernelGGL(k_wave<1>, dim3(g1s), dim3(64), 0, side, X, PHO, qnorm, off, qm, out_n, out_k,
                                    out_s, list2, count2, stats, (const uint32_t*)fb2, (const uint32_t*)fbc2);
                 dbg_check(side, "k_wave<1> (heavy hand-overs)");
