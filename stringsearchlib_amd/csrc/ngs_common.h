@@ -109,6 +109,10 @@ constexpr int kWaveWavesPerSimd = NGS_WPS;      // occupancy target of tier 1b: 
 #define NGS_LEAN_WPS 6
 #endif
 constexpr int kLeanWavesPerSimd = NGS_LEAN_WPS; // tier 1a: 6 -> <= 80 VGPRs (LDS 6 KB: 24 waves per CU)
+#ifndef NGS_HEAVY_LEAN_WPS
+#define NGS_HEAVY_LEAN_WPS NGS_LEAN_WPS
+#endif
+constexpr int kHeavyLeanWavesPerSimd = NGS_HEAVY_LEAN_WPS;  // ... the heavy list's launch (packed staging)
 #ifndef NGS_LEAN_CAND_IN_TABLE
 #define NGS_LEAN_CAND_IN_TABLE 1
 #endif
@@ -184,6 +188,9 @@ constexpr uint32_t kRankShrink = NGS_RANK_SHRINK;    // ... of threshold-0 queri
 #endif
 // tier 1a also takes cmin-1 queries (threshold 0) on the heavy list: part_ones
 constexpr bool kLeanOnes = NGS_LEAN_ONES != 0;
+#ifndef NGS_HEAVY_ONES_ALWAYS
+#define NGS_HEAVY_ONES_ALWAYS 0  // experiment: the heavy launch compiled with part_ones at every threshold
+#endif
 #ifndef NGS_ONES_SHRINK
 #define NGS_ONES_SHRINK 2
 #endif

@@ -3128,8 +3128,8 @@ __global__ __launch_bounds__(64) void k_serve(DevIndex X, SearchParams P0, Serve
 // one workgroup per query (the main launch): either way the part loop is compiled once (with
 // both in one kernel the main launch carried 76 B of scratch spills and 434 lane reloads; the
 // same speed, profiles/r03_s5_ab_lean_one_copy.txt)
-template <bool DEFER, bool ONES = false, bool LISTED = true>
-__global__ __launch_bounds__(64, kLeanWavesPerSimd) void k_wave_lean(DevIndex X, SearchParams P,
+template <bool DEFER, bool ONES = false, bool LISTED = true, bool PACKED = false>
+__global__ __launch_bounds__(64, PACKED ? kHeavyLeanWavesPerSimd : kLeanWavesPerSimd) void k_wave_lean(DevIndex X, SearchParams P,
                                                                     const uint8_t* __restrict__ qnorm,
                                                                     const uint64_t* __restrict__ qoff,
                                                                     const uint32_t* __restrict__ qm,
@@ -3147,7 +3147,7 @@ __global__ __launch_bounds__(64, kLeanWavesPerSimd) void k_wave_lean(DevIndex X,
     // staging for its threshold-0 queries (part_ones: quarter-size parts of ~3 chunks per list, where a
     // per-list cap splits most parts), NGS_LEAN_GROUPS 2: for all of them, 3: for its cmin >= 2 ones
     auto one = [&](uint32_t q) {
-        if constexpr (NGS_LEAN_GROUPS == 0) {
+        if constexpr (NGS_LEAN_GROUPS == 0 || (PACKED && NGS_LEAN_GROUPS != 2)) {
             lean_query<ONES>(S, q, X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats, fb, fbc);
         } else if constexpr (!ONES || NGS_LEAN_GROUPS == 2) {
             lean_query_g<ONES>(S, q, X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats, fb, fbc);
@@ -3860,8 +3860,17 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
                                        out_k, out_s, list2, count2, stats, fb2, fbc2, heavy, hcount);
                     dbg_check(side, "k_heavy (heavy list)");
                 } else {
-                    hipLaunchKernelGGL((k_wave_lean<true, kLeanOnes>), dim3(gh), dim3(64), 0, side, X, PH, qnorm, off, qm,
-                                       out_n, out_k, out_s, list2, count2, stats, fb2, fbc2, heavy, hcount);
+                    // part_ones is compiled in only where a lean query can have cmin 1: without rank lists,
+                    // at a threshold the shortest lean query (n_min grams) passes with one hit
+                    const uint32_t n_min = (X.n_short ? X.short_query_len : X.full_scan_len + 1) - X.gsz + 1;
+                    const bool ones = kLeanOnes && (NGS_HEAVY_ONES_ALWAYS || (!X.rank_post && !(1.0f / (float)n_min < P.thr)));
+                    if (ones)
+                        hipLaunchKernelGGL((k_wave_lean<true, kLeanOnes, true, true>), dim3(gh), dim3(64), 0, side, X, PH,
+                                           qnorm, off, qm, out_n, out_k, out_s, list2, count2, stats, fb2, fbc2, heavy,
+                                           hcount);
+                    else
+                        hipLaunchKernelGGL((k_wave_lean<true, false, true, true>), dim3(gh), dim3(64), 0, side, X, PH, qnorm,
+                                           off, qm, out_n, out_k, out_s, list2, count2, stats, fb2, fbc2, heavy, hcount);
                     dbg_check(side, "k_wave_lean (heavy list)");
                     hipLaunchKernelGGL(k_emit<true>, dim3((gh + kEmitWaves - 1) / kEmitWaves), dim3(64 * kEmitWaves), 0,
                                        side, X, PH, qnorm, off, qm, out_n, out_k, out_s, stats, heavy, hcount);

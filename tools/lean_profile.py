@@ -1,6 +1,6 @@
 """Phase breakdown of the tier-1a lean kernel (diagnostic build: make -C stringsearchlib_amd/csrc prof,
 then NGS_LIB=prof). Cycles (s_memtime) per query and phase, summed over the queries' waves, plus
-part statistics."""
+part statistics. usage: NGS_LIB=prof python tools/lean_profile.py [rows] [batch] [thr] [qlen]"""
 import ctypes as C
 import os
 import sys
@@ -18,11 +18,14 @@ def main():
     rows = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
     B = int(sys.argv[2]) if len(sys.argv) > 2 else 65536
     thr = float(sys.argv[3]) if len(sys.argv) > 3 else 0.3
+    qlen = int(sys.argv[4]) if len(sys.argv) > 4 else 0  # > 0: queries cut to this many bytes (8: C3's heavy ones)
     corpus = bench.Corpus(rows)
     h = bench.build_index(corpus, True, 0)
     L = _native.lib()
     raw, offs = corpus.queries(B)
     qs = [raw[offs[i]:offs[i + 1]] for i in range(B)]
+    if qlen:
+        qs = [q[:qlen] for q in qs]
     arr = (C.c_char_p * B)(*qs)
     counts = (C.c_uint32 * B)()
     out = (C.c_uint64 * 32)()
