@@ -150,6 +150,9 @@ constexpr bool kSketchLoose = NGS_SKETCH_LOOSE != 0;
 #ifndef NGS_EMIT_DEPTH
 #define NGS_EMIT_DEPTH 1  // batches of survivor pairs in flight in the heavy list's k_emit
 #endif
+#ifndef NGS_SORT64
+#define NGS_SORT64 1  // final flushes of <= 64 distinct records sorted in registers (wave_sort64)
+#endif
 #ifndef NGS_RADIX_SELECT
 #define NGS_RADIX_SELECT 1  // top-L buffer refills by radix select (wave_select); 0: bitonic sort
 #endif

@@ -1056,6 +1056,29 @@ __device__ void wave_select(SM& S, uint32_t& cand_n, uint64_t& tau, uint32_t L) 
     tau = kth;
 }
 
+// A buffer of n <= 64 distinct records sorted in registers, one record per lane: a bitonic network
+// over lane shuffles (log2 P2 (log2 P2 + 1) / 2 stages for P2 = next_pow2(n)), no LDS round trip
+// and barrier per stage as in the LDS sort below. The final flush of most queries (C3: ~35
+// survivors, 20 results) is this one.
+template <class SM>
+__device__ __forceinline__ void wave_sort64(SM& S, uint32_t n) {
+    const uint32_t lane = lane_id();
+    const uint32_t P2 = next_pow2(max(n, 2u));
+    uint64_t r = lane < n ? S.cand()[lane] : kNoCand;
+    for (uint32_t k = 2; k <= P2; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)r, (int)j);
+            const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(r >> 32), (int)j);
+            const uint64_t p = ((uint64_t)hi << 32) | lo;
+            const bool keep_min = ((lane & k) == 0) == ((lane & j) == 0);
+            r = keep_min ? min64(r, p) : max64(r, p);
+        }
+    }
+    wave_sync();  // every lane has read the buffer
+    if (lane < P2) S.cand()[lane] = r;
+    wave_sync();
+}
+
 // Wave-local running top-L over the candidate buffer (same algorithm as flush()), sorted.
 // unique: no two records share a key (DevIndex.keys_unique): only the second pass runs, after a
 // radix select has cut a buffer of more than L records to its L smallest (wave_select).
@@ -1065,6 +1088,13 @@ template <bool RADIX = false, class SM>
 __device__ void wave_flush(SM& S, uint32_t& cand_n, uint64_t& tau, uint32_t L, bool unique = false) {
     const uint32_t lane = lane_id();
     if (RADIX && NGS_RADIX_SELECT && unique && cand_n > L && L) wave_select(S, cand_n, tau, L);
+    if (NGS_SORT64 && unique && cand_n <= 64) {  // distinct records: sorted in registers
+        const uint32_t n = cand_n;
+        wave_sort64(S, n);
+        cand_n = min(n, L);
+        tau = n >= L && L ? S.cand()[L - 1] : kNoCand;
+        return;
+    }
     const uint32_t n = min(cand_n, (uint32_t)kWaveCand);
     const uint32_t P2 = next_pow2(max(n, 2u));
     for (uint32_t i = lane; i < P2; i += 64) {
