@@ -5,7 +5,7 @@
 set -o pipefail
 VARS=$1; shift
 mkdir -p gpurun_out/ab
-for pass in 1 2; do
+for pass in $(seq 1 ${AB_PASSES:-2}); do
   for v in $VARS; do
     [ "$v" = main ] && lib="" || lib=$v
     NGS_LIB=$lib timeout -k 10 240 python3 bench.py --no-cpu-baseline --steps 100 --warmup 5 "$@" > gpurun_out/ab/$v.$pass.json 2> gpurun_out/ab/$v.$pass.err || { echo "$v failed"; tail -3 gpurun_out/ab/$v.$pass.err; exit 1; }
