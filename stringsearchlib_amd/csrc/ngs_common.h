@@ -110,7 +110,7 @@ constexpr int kWaveWavesPerSimd = NGS_WPS;      // occupancy target of tier 1b: 
 #endif
 constexpr int kLeanWavesPerSimd = NGS_LEAN_WPS; // tier 1a: 6 -> <= 80 VGPRs (LDS 6 KB: 24 waves per CU)
 #ifndef NGS_HEAVY_LEAN_WPS
-#define NGS_HEAVY_LEAN_WPS 5  // 95 VGPRs, no scratch (6: 80 VGPRs and 56 B of scratch in the part loop)
+#define NGS_HEAVY_LEAN_WPS NGS_LEAN_WPS  // (5: 95 VGPRs and no scratch, measured no faster: profiles/r04_s2_ab_heavy_wps_sort64.txt)
 #endif
 constexpr int kHeavyLeanWavesPerSimd = NGS_HEAVY_LEAN_WPS;  // ... the heavy list's launch (packed staging)
 #ifndef NGS_LEAN_CAND_IN_TABLE
