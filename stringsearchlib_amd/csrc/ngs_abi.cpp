@@ -947,8 +947,9 @@ int queue_search(Library& L, Replica& R, Context& c, const uint8_t* d_raw, const
     P.prec = c.d_prec;
     P.pcnt = c.d_pcnt;
     const bool timing = L.timing.load();
-    // A small batch is a few waves per CU of long per-query chains (C2: 4,096 queries, every one on
-    // the heavy list), so throughput comes from batches in flight, not from the main and side streams
+    // A small batch whose queries are all on the heavy list (C2: 4,096 queries at threshold 0) is a
+    // few waves per CU of long per-query chains, so throughput comes from batches in flight, not from
+    // the main and side streams
     // of one call overlapping: its side work goes on the call's own stream, in order, and a context
     // that only ever runs such batches never makes its side streams. Three pipelined calls then hold
     // three hardware queues (HIP maps streams to its four queues round-robin as they are made) instead
@@ -958,8 +959,12 @@ int queue_search(Library& L, Replica& R, Context& c, const uint8_t* d_raw, const
         const char* e = std::getenv("NGS_ONE_STREAM_BATCH");
         return e ? (uint32_t)std::strtoul(e, nullptr, 0) : kOneStreamBatch;
     }();
+    // (only where every lean query is on the heavy list, cmin <= kHeavyCmin for any gram count up to
+    // kWaveMaxGrams, as at threshold 0: with a mix, the heavy chain on its own stream overlaps the
+    // main launch, and in order after it a call of 8,192 C3-like queries took 0.23 ms longer)
+    const bool all_heavy = !((float)kHeavyCmin / (float)kWaveMaxGrams < thr);
     hipStream_t side = s, side2 = s;
-    if (B > one_stream_batch) {
+    if (B > one_stream_batch || !all_heavy) {
         if (!c.side && !HIP_CHECK(make_side_stream(&c.side))) return -4;
         if (!c.side2 && !HIP_CHECK(make_second_side(c.side, &c.side2))) return -4;
         side = c.side;
