@@ -981,7 +981,7 @@ int queue_search(Library& L, Replica& R, Context& c, const uint8_t* d_raw, const
     if (timing) HIP_CHECK(hipEventRecord(c.ev[2], s));
     if (!HIP_CHECK(launch_fast(R.dev, P, c.d_norm, d_off, c.d_qm, d_n, d_k, d_s, c.d_list2, gc + 1, c.d_fb, gc + 2,
                                c.d_fb2, gc + 4, c.d_heavy, gc + 3, c.d_full, gc + 5, c.d_glist, gc, sd, s, side,
-                               side2, c.fork, c.join, c.join2, c.lists_ev, defer_heavy)))
+                               side2, c.fork, c.join, c.join2, c.lists_ev, defer_heavy, all_heavy && !NGS_NO_SKIP_EMPTY)))
         return -4;
     if (timing) HIP_CHECK(hipEventRecord(c.ev[3], s));
     // the statistics and the path counts in one read-back (the general path adds no statistics)

@@ -3844,7 +3844,7 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
                        const uint32_t* heavy, const uint32_t* hcount, const uint32_t* full,
                        const uint32_t* fcount, uint32_t* glist, uint32_t* gcount, DevStats* stats, hipStream_t s,
                        hipStream_t side, hipStream_t side2, hipEvent_t fork, hipEvent_t join, hipEvent_t join2,
-                       hipEvent_t lists_ev, bool defer_heavy) {
+                       hipEvent_t lists_ev, bool defer_heavy, bool all_heavy) {
     if (!P.n_queries) return hipSuccess;
     hipError_t e = hipSuccess;
     switch (P.waves) {  // waves per query (SearchParams.waves, NGS_WAVES; 0 = tier 1a + 1b)
@@ -3938,17 +3938,22 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
             }
             if ((e = hipEventRecord(join2, side2)) != hipSuccess) return e;
             if (!kMainFirst) main_lean();
-            if (kDeferEmit) {
+            // all_heavy (every lean query on the heavy list, e.g. threshold 0): the main launch finishes
+            // no query and hands none over (it returns before either for a heavy or full one), so its
+            // k_emit and hand-over launches would find nothing
+            if (kDeferEmit && !all_heavy) {
                 hipLaunchKernelGGL(k_emit<false>, dim3((P.n_queries + kEmitWaves - 1) / kEmitWaves), dim3(64 * kEmitWaves), 0,
                                    s, X, P, qnorm, off, qm, out_n, out_k, out_s, stats, (const uint32_t*)nullptr,
                                    (const uint32_t*)nullptr);
                 dbg_check(s, "k_emit");
             }
             // tier 1b over the queries tier 1a handed over
-            hipLaunchKernelGGL(k_wave<1>, dim3(g1s), dim3(64), 0, s, X, PM, qnorm, off, qm, out_n, out_k, out_s,
-                               list2, count2, stats, (const uint32_t*)fb, (const uint32_t*)fbc);
-            dbg_check(s, "k_wave<1> (hand-overs)");
-            if (P.nslices > 1) {
+            if (!all_heavy) {
+                hipLaunchKernelGGL(k_wave<1>, dim3(g1s), dim3(64), 0, s, X, PM, qnorm, off, qm, out_n, out_k, out_s,
+                                   list2, count2, stats, (const uint32_t*)fb, (const uint32_t*)fbc);
+                dbg_check(s, "k_wave<1> (hand-overs)");
+            }
+            if (P.nslices > 1 && !all_heavy) {
                 hipLaunchKernelGGL(k_merge, dim3(g1b), dim3(64), 0, s, X, P, (const uint32_t*)fb, (const uint32_t*)fbc,
                                    out_n, out_k, out_s, stats);
                 dbg_check(s, "k_merge (hand-overs)");
