@@ -201,7 +201,7 @@ constexpr uint32_t kOnesShrink = NGS_ONES_SHRINK;  // ... in parts of a quarter 
 constexpr uint32_t kBackPieces = 4;              // host batches: records read back in up to this many pieces
 constexpr uint32_t kBackPieceMin = 131072;        // ... of at least this many records
 #ifndef NGS_NO_SKIP_EMPTY
-#define NGS_NO_SKIP_EMPTY 1  // 1: launch the main k_emit and hand-over tier 1b even when all queries are heavy
+#define NGS_NO_SKIP_EMPTY 0  // 1: launch the main k_emit and hand-over tier 1b even when all queries are heavy
 #endif
 constexpr uint32_t kOneStreamBatch = 16384;     // batches up to this size run on one stream per call
 #ifndef NGS_HEAVY_FUSE
