@@ -17,7 +17,16 @@
  * iteration order (documented in DESIGN.md §Parity):
  *   - ties in (score, key length) are broken by the key's first appearance in the input;
  *   - wildcard ("" / "*", hpp:356-369): a key takes the largest weight of its pairs;
- *   - exact-match promotion (hpp:328-335) wins over any later pair of the same key.
+ *   - exact-match promotion (hpp:328-335) sets the key's score to 100, an ordinary score in
+ *     ScoreComparer (h:262-269): a key with w*s > 100 ranks above a promoted key, and one at
+ *     exactly 100 ties with it on the score and is ordered by length. calcScore runs over the
+ *     short scores, then the long ones (hpp:393-394), each in unordered_map order, and a
+ *     promotion overwrites what the key had so far while a later pair max-merges over it. The
+ *     order inside one group is unspecified; this restatement takes a group's promoting pairs
+ *     FIRST: a key's score is max(100, w*s of its other long pairs) when a long pair promotes
+ *     it (its short pairs came before and are overwritten), else the max over all its pairs
+ *     with a promoting pair counting 100. This agrees with the reference whenever its answer
+ *     does not depend on the iteration order; ngo_search_amb reports the queries where it does.
  */
 #define _GNU_SOURCE
 #include "ngs_oracle.h"
@@ -28,7 +37,6 @@
 #include <string.h>
 
 #define GRAM_SPACE (1u << 21)
-#define PROMOTED 0xFFFFFFFFu
 #define SHORT_TERM_LEN 6 /* hpp:82 */
 #define SHORT_QUERY_LEN 9 /* hpp:381 */
 
@@ -57,6 +65,8 @@ static void* xrealloc(void* p, size_t n) {
 
 static uint32_t f2u(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
 static float u2f(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
+/* score encoding: enc = bits(max(w*s, +0)) + 1 (0 = key absent); a promoted key is the score 100 */
+#define ENC100 (0x42C80000u + 1u)
 
 /* ------------------------------------------------------------------ interning ---------- */
 typedef struct {
@@ -116,6 +126,7 @@ struct ngo_index {
     uint32_t n_terms, n_short;
     uint64_t* term_off; uint8_t* term_bytes; /* normalised term strings */
     uint32_t* tk_off; uint32_t* tk_key; float* tk_w; /* wordMap/wordWeight (h:290,293) */
+    uint32_t* kt_off; uint32_t* kt_term;             /* key -> its terms (the pairs, transposed) */
     /* keys ordered by (raw trimmed length, first appearance): the tie refinement */
     uint32_t n_keys;
     uint64_t* key_off; uint8_t* key_bytes;
@@ -268,6 +279,17 @@ ngo_index* ngo_build(char* const* words, uint64_t size, uint16_t rowSize, const 
         }
         free(fill);
     }
+    /* key -> terms: which pairs a promotable key has (emit_term's short-group rule) */
+    ix->kt_off = xcalloc((size_t)keys.n + 1, 4);
+    ix->kt_term = xmalloc((size_t)nuniq * 4 + 4);
+    for (uint32_t p = 0; p < nuniq; ++p) ix->kt_off[krank[pairs[p].key] + 1]++;
+    for (uint32_t k = 0; k < keys.n; ++k) ix->kt_off[k + 1] += ix->kt_off[k];
+    {
+        uint32_t* fill = xmalloc((size_t)keys.n * 4 + 4);
+        memcpy(fill, ix->kt_off, (size_t)keys.n * 4);
+        for (uint32_t p = 0; p < nuniq; ++p) ix->kt_term[fill[krank[pairs[p].key]]++] = tmap[pairs[p].term];
+        free(fill);
+    }
 
     /* wildcard answer (hpp:356-369): every key with a weight of one of its pairs */
     ix->wild_w = xmalloc((size_t)keys.n * 4);
@@ -324,6 +346,7 @@ ngo_index* ngo_build(char* const* words, uint64_t size, uint16_t rowSize, const 
 void ngo_free(ngo_index* ix) {
     if (!ix) return;
     free(ix->term_off); free(ix->term_bytes); free(ix->tk_off); free(ix->tk_key); free(ix->tk_w);
+    free(ix->kt_off); free(ix->kt_term);
     free(ix->key_off); free(ix->key_bytes); free(ix->wild_w); free(ix->wild_order);
     free(ix->gram_off); free(ix->post); free(ix);
 }
@@ -347,6 +370,9 @@ void ngo_set_valid(ngo_index* ix, const char* chars, int n) {
 typedef struct {
     uint32_t* cnt; uint32_t* touched; /* long-term counters + touched list */
     uint32_t* kenc; uint32_t* ktouch; uint32_t nkt;
+    /* per key, for ngo_search_amb: bit 0 a long pair promotes, bit 1 a short pair promotes;
+     * the best non-promoting long / short encodings */
+    uint8_t* kfl; uint32_t* knl; uint32_t* kns;
     uint64_t* sortbuf;
     uint8_t* q; size_t qcap;
 } workspace;
@@ -357,9 +383,12 @@ static void ws_init(workspace* w, const ngo_index* ix) {
     w->cnt = xcalloc(nl + 1, 4); w->touched = xmalloc(((size_t)nl + 1) * 4);
     w->kenc = xcalloc((size_t)ix->n_keys + 1, 4); w->ktouch = xmalloc(((size_t)ix->n_keys + 1) * 4);
     w->sortbuf = xmalloc(((size_t)ix->n_keys + 1) * 8);
+    w->kfl = xcalloc((size_t)ix->n_keys + 1, 1);
+    w->knl = xcalloc((size_t)ix->n_keys + 1, 4); w->kns = xcalloc((size_t)ix->n_keys + 1, 4);
 }
 static void ws_free(workspace* w) {
     free(w->cnt); free(w->touched); free(w->kenc); free(w->ktouch); free(w->sortbuf); free(w->q);
+    free(w->kfl); free(w->knl); free(w->kns);
 }
 
 /* libStr = escapeBlank(stringLib[key]); trim; libStr == query  (hpp:330-334; no toUpper) */
@@ -374,18 +403,48 @@ static int key_matches_query(const ngo_index* ix, uint32_t k, const uint8_t* q, 
     return 1;
 }
 
-/* calcScore (hpp:310-341) for one scored term: threshold, weight, max-merge, promotion */
+/* Does key k have a long term that every gram of the query hits (searchLong scores it
+ * count/n = 1 > 0.999, hpp:300,328) and that passes the threshold? Then calcScore's long pass
+ * promotes k (hpp:335) after every short pair of k (hpp:393-394). */
+static int key_promoted_long(const ngo_index* ix, uint32_t k, const uint8_t* q, uint32_t m, float thr) {
+    if (m < 3 || 1.0f < thr) return 0;                             /* hpp:281, :315 */
+    for (uint32_t p = ix->kt_off[k]; p < ix->kt_off[k + 1]; ++p) {
+        uint32_t t = ix->kt_term[p];
+        if (t < ix->n_short) continue;
+        const uint8_t* s = ix->term_bytes + ix->term_off[t];
+        uint32_t L = (uint32_t)(ix->term_off[t + 1] - ix->term_off[t]), all = 1;
+        for (uint32_t i = 0; all && i + 2 < m; ++i) {
+            if ((q[i] | q[i + 1] | q[i + 2]) & 0x80) { all = 0; break; } /* never counted (search_ws) */
+            uint32_t hit = 0;
+            for (uint32_t j = 0; !hit && j + 2 < L; ++j)
+                hit = s[j] == q[i] && s[j + 1] == q[i + 1] && s[j + 2] == q[i + 2];
+            all = hit;
+        }
+        if (all) return 1;
+    }
+    return 0;
+}
+
+/* calcScore (hpp:310-341) for one scored term: threshold, weight, max-merge, promotion.
+ * grp: 1 = a short score (searchShort), 0 = a long one (searchLong). */
 static void emit_term(const ngo_index* ix, workspace* w, uint32_t t, float s, float thr,
-                      const uint8_t* q, uint32_t m) {
+                      const uint8_t* q, uint32_t m, int grp) {
     if (s < thr) return;                                           /* hpp:315 */
     int exact_possible = (double)s > 0.999;                        /* hpp:328 */
     for (uint32_t p = ix->tk_off[t]; p < ix->tk_off[t + 1]; ++p) {
         uint32_t k = ix->tk_key[p];
         float sc = ix->tk_w[p] * s;                                /* hpp:326 */
         uint32_t enc = sc > 0.0f ? f2u(sc) + 1u : 1u;              /* max(w*s, 0.0f) */
-        if (exact_possible && key_matches_query(ix, k, q, m)) enc = PROMOTED; /* hpp:335 */
+        int promo = exact_possible && key_matches_query(ix, k, q, m);
+        if (promo) enc = ENC100;                                   /* hpp:335: score = 100 */
+        /* a short pair above 100 of a key that the long pass promotes later is overwritten */
+        if (grp && !promo && enc > ENC100 && key_matches_query(ix, k, q, m) && key_promoted_long(ix, k, q, m, thr))
+            continue;
         if (!w->kenc[k]) w->ktouch[w->nkt++] = k;
         if (enc > w->kenc[k]) w->kenc[k] = enc;
+        if (promo) w->kfl[k] |= grp ? 2 : 1;
+        else if (grp) { if (enc > w->kns[k]) w->kns[k] = enc; }
+        else if (enc > w->knl[k]) w->knl[k] = enc;
     }
 }
 
@@ -415,7 +474,8 @@ static int cmp_u64(const void* a, const void* b) {
 }
 
 static uint32_t search_ws(const ngo_index* ix, workspace* w, const char* query, float thr, uint32_t limit,
-                          uint32_t* out_keys, float* out_scores, uint32_t cap) {
+                          uint32_t* out_keys, float* out_scores, uint32_t cap, int* amb) {
+    if (amb) *amb = 0;
     if (!ix->indexed) return 0;                                    /* hpp:417-418 */
     if (limit == 0) limit = 2147483647u;                           /* hpp:420-421 */
     if (cap < limit) limit = cap;
@@ -439,7 +499,7 @@ static uint32_t search_ws(const ngo_index* ix, workspace* w, const char* query, 
         for (uint32_t t = 0; t < end; ++t) {
             const uint8_t* s = ix->term_bytes + ix->term_off[t];
             uint32_t L = (uint32_t)(ix->term_off[t + 1] - ix->term_off[t]);
-            emit_term(ix, w, t, (float)string_match(q, m, s, L) / (float)m, thr, q, m); /* hpp:244 */
+            emit_term(ix, w, t, (float)string_match(q, m, s, L) / (float)m, thr, q, m, 1); /* hpp:244 */
         }
     }
     if (m >= 3) {                                                  /* hpp:281 searchLong */
@@ -454,7 +514,7 @@ static uint32_t search_ws(const ngo_index* ix, workspace* w, const char* query, 
         }
         for (uint32_t i = 0; i < nt; ++i) {
             uint32_t t = w->touched[i];
-            emit_term(ix, w, ix->n_short + t, (float)w->cnt[t] / (float)ng, thr, q, m); /* hpp:300 */
+            emit_term(ix, w, ix->n_short + t, (float)w->cnt[t] / (float)ng, thr, q, m, 0); /* hpp:300 */
             w->cnt[t] = 0;
         }
     }
@@ -463,14 +523,20 @@ static uint32_t search_ws(const ngo_index* ix, workspace* w, const char* query, 
     for (uint32_t i = 0; i < w->nkt; ++i) {
         uint32_t k = w->ktouch[i];
         w->sortbuf[i] = ((uint64_t)(~w->kenc[k]) << 32) | k;
-        w->kenc[k] = 0;
+        /* the reference's score of k depends on unordered_map order: a long promotion with a
+         * long pair above 100 beside it, or (no long promotion) a short promotion with a short
+         * pair above both 100 and every long pair */
+        if (amb && ((w->kfl[k] & 1) ? w->knl[k] > ENC100
+                                     : (w->kfl[k] & 2) && w->kns[k] > ENC100 && w->kns[k] > w->knl[k]))
+            *amb = 1;
+        w->kenc[k] = 0; w->kfl[k] = 0; w->knl[k] = 0; w->kns[k] = 0;
     }
     qsort(w->sortbuf, w->nkt, 8, cmp_u64);
     uint32_t n = w->nkt < limit ? w->nkt : limit;                  /* hpp:425 */
     for (uint32_t i = 0; i < n; ++i) {
         uint32_t enc = ~(uint32_t)(w->sortbuf[i] >> 32);
         out_keys[i] = (uint32_t)w->sortbuf[i];
-        out_scores[i] = enc == PROMOTED ? 100.0f : u2f(enc - 1u);
+        out_scores[i] = u2f(enc - 1u);
     }
     return n;
 }
@@ -479,7 +545,16 @@ uint32_t ngo_search(const ngo_index* ix, const char* query, float threshold, uin
                     uint32_t* out_keys, float* out_scores, uint32_t cap) {
     workspace w;
     ws_init(&w, ix);
-    uint32_t n = search_ws(ix, &w, query, threshold, limit, out_keys, out_scores, cap);
+    uint32_t n = search_ws(ix, &w, query, threshold, limit, out_keys, out_scores, cap, NULL);
+    ws_free(&w);
+    return n;
+}
+
+uint32_t ngo_search_amb(const ngo_index* ix, const char* query, float threshold, uint32_t limit,
+                        uint32_t* out_keys, float* out_scores, uint32_t cap, int* ambiguous) {
+    workspace w;
+    ws_init(&w, ix);
+    uint32_t n = search_ws(ix, &w, query, threshold, limit, out_keys, out_scores, cap, ambiguous);
     ws_free(&w);
     return n;
 }
@@ -502,7 +577,7 @@ static void* batch_worker(void* p) {
         uint32_t e = i + 16 < a->n ? i + 16 : a->n;
         for (; i < e; ++i)
             a->counts[i] = search_ws(a->ix, &w, a->qs[i], a->thr, a->limit, a->keys + (size_t)i * a->cap,
-                                     a->scores + (size_t)i * a->cap, a->cap);
+                                     a->scores + (size_t)i * a->cap, a->cap, NULL);
     }
     ws_free(&w);
     return NULL;

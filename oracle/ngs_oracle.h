@@ -39,6 +39,12 @@ void ngo_set_valid(ngo_index* ix, const char* chars, int n);
 uint32_t ngo_search(const ngo_index* ix, const char* query, float threshold, uint32_t limit,
                     uint32_t* out_keys, float* out_scores, uint32_t cap);
 
+/* ngo_search, and *ambiguous = 1 when the reference's answer to this query depends on its
+ * unordered_map iteration order beyond ties (a promoted key with another pair scoring above 100
+ * in the same calcScore pass, see ngs_oracle.c); 0 otherwise. Test infrastructure (the fuzz). */
+uint32_t ngo_search_amb(const ngo_index* ix, const char* query, float threshold, uint32_t limit,
+                        uint32_t* out_keys, float* out_scores, uint32_t cap, int* ambiguous);
+
 /* Batch over `threads` pthreads (cpu_baseline). Query i gets slots [i*cap, i*cap+cap). */
 void ngo_search_batch(const ngo_index* ix, const char* const* queries, uint32_t n, float threshold,
                       uint32_t limit, uint32_t* out_counts, uint32_t* out_keys, float* out_scores,

@@ -19,6 +19,8 @@
  * ngs_oracle.c (tests/test_oracle_generic.py), which is pinned to the reference.
  * It is written independently of ngs_oracle.c (hash maps instead of the 21-bit gram table)
  * so that the cross-check is not a check of shared code.
+ * Promotion (hpp:328-335) follows ngs_oracle.c: a promoted key scores 100, an ordinary score;
+ * a group's promoting pairs are taken first (a long promotion overwrites the key's short pairs).
  */
 #define _GNU_SOURCE
 #include "ngs_oracle_g.h"
@@ -28,7 +30,7 @@
 #include <stdlib.h>
 #include <string.h>
 
-#define PROMOTED 0xFFFFFFFFu
+#define ENC100 (0x42C80000u + 1u) /* enc of the score 100: a promoted key */
 #define MAX_G 3
 
 static const char DEFAULT_VALID[] =
@@ -108,6 +110,7 @@ struct ngog_index {
     uint32_t n_terms;            /* terms in first-appearance order (ids are not reordered) */
     ustr* terms;
     kw** tkeys; uint32_t* ntk;   /* term -> (key rank, weight) in insertion order */
+    uint32_t* kt_off; uint32_t* kt_term; /* key rank -> its terms */
     uint32_t n_keys;
     ustr* keys;                  /* by rank: (trimmed raw length, first appearance) */
     float* wild_w; uint32_t* wild_order;
@@ -258,6 +261,19 @@ ngog_index* ngog_build(const uint32_t* const* words, uint64_t size, uint16_t row
             seen[p->key] = 1;
         }
     free(seen); free(order); free(rank);
+    {
+        uint64_t np = 0;
+        ix->kt_off = xcalloc((size_t)ix->n_keys + 1, 4);
+        for (uint32_t t = 0; t < ix->n_terms; ++t)
+            for (uint32_t e = 0; e < ix->ntk[t]; ++e) { ix->kt_off[ix->tkeys[t][e].key + 1]++; ++np; }
+        for (uint32_t k = 0; k < ix->n_keys; ++k) ix->kt_off[k + 1] += ix->kt_off[k];
+        ix->kt_term = xmalloc((size_t)np * 4 + 4);
+        uint32_t* fill = xmalloc((size_t)ix->n_keys * 4 + 4);
+        memcpy(fill, ix->kt_off, (size_t)ix->n_keys * 4);
+        for (uint32_t t = 0; t < ix->n_terms; ++t)
+            for (uint32_t e = 0; e < ix->ntk[t]; ++e) ix->kt_term[fill[ix->tkeys[t][e].key]++] = t;
+        free(fill);
+    }
     ix->wild_order = xmalloc((size_t)ix->n_keys * 4);
     for (uint32_t k = 0; k < ix->n_keys; ++k) ix->wild_order[k] = k;
     qsort_r(ix->wild_order, ix->n_keys, 4, cmp_wild, ix->wild_w);
@@ -283,7 +299,7 @@ void ngog_free(ngog_index* ix) {
     for (uint32_t k = 0; k < ix->n_keys; ++k) free(ix->keys[k].p);
     for (uint64_t i = 0; i < ix->nglist; ++i) if (ix->gl[i].gram != ~0ull) free(ix->gl[i].post);
     free(ix->terms); free(ix->tkeys); free(ix->ntk); free(ix->keys);
-    free(ix->wild_w); free(ix->wild_order); free(ix->gl); free(ix);
+    free(ix->wild_w); free(ix->wild_order); free(ix->gl); free(ix->kt_off); free(ix->kt_term); free(ix);
 }
 
 int ngog_indexed(const ngog_index* ix) { return ix && ix->indexed; }
@@ -328,15 +344,38 @@ static int key_is_query(const ngog_index* ix, ws* w, uint32_t k, const uint32_t*
     return n == m && memcmp(w->k, q, (size_t)m * 4) == 0;
 }
 
-/* calcScore (hpp:310-341) */
-static void emit(const ngog_index* ix, ws* w, uint32_t t, float s, float thr, const uint32_t* q, uint32_t m) {
+/* key k has a long term holding every gram of the query (searchLong: s = 1) at this threshold */
+static int key_long_full(const ngog_index* ix, uint32_t k, const uint32_t* q, uint32_t m, float thr) {
+    const uint32_t g = ix->g;
+    if (m < g || 1.0f < thr) return 0;                                       /* hpp:281, :315 */
+    for (uint32_t p = ix->kt_off[k]; p < ix->kt_off[k + 1]; ++p) {
+        const ustr* s = &ix->terms[ix->kt_term[p]];
+        if (s->n < 2 * g) continue;
+        int all = 1;
+        for (uint32_t i = 0; all && i + g <= m; ++i) {
+            const uint64_t gr = gram_of(q + i, g);
+            int hit = 0;
+            for (uint32_t j = 0; !hit && j + g <= s->n; ++j) hit = gram_of(s->p + j, g) == gr;
+            all = hit;
+        }
+        if (all) return 1;
+    }
+    return 0;
+}
+
+/* calcScore (hpp:310-341); grp 1 = a short score (calcScore's first pass, hpp:393) */
+static void emit(const ngog_index* ix, ws* w, uint32_t t, float s, float thr, const uint32_t* q, uint32_t m,
+                 int grp) {
     if (s < thr) return;                                                     /* hpp:315 */
     int exact = (double)s > 0.999;                                           /* hpp:328 */
     for (uint32_t e = 0; e < ix->ntk[t]; ++e) {
         uint32_t k = ix->tkeys[t][e].key;
         float sc = ix->tkeys[t][e].w * s;                                    /* hpp:326 */
         uint32_t enc = sc > 0.0f ? f2u(sc) + 1u : 1u;
-        if (exact && key_is_query(ix, w, k, q, m)) enc = PROMOTED;           /* hpp:335 */
+        const int promo = exact && key_is_query(ix, w, k, q, m);
+        if (promo) enc = ENC100;                                             /* hpp:335: score = 100 */
+        if (grp && !promo && enc > ENC100 && key_is_query(ix, w, k, q, m) && key_long_full(ix, k, q, m, thr))
+            continue;  /* overwritten by the long pass's promotion */
         if (!w->kenc[k]) w->ktouch[w->nkt++] = k;
         if (enc > w->kenc[k]) w->kenc[k] = enc;
     }
@@ -392,7 +431,7 @@ static uint32_t search_ws(const ngog_index* ix, ws* w, const uint32_t* query, fl
         for (uint32_t t = 0; t < ix->n_terms; ++t) {
             const ustr* s = &ix->terms[t];
             if (m > g && s->n >= 2 * g) continue;                            /* hpp:247: shortLib only */
-            emit(ix, w, t, (float)string_match(q, m, s->p, s->n) / (float)m, thr, q, m); /* hpp:244 */
+            emit(ix, w, t, (float)string_match(q, m, s->p, s->n) / (float)m, thr, q, m, 1); /* hpp:244 */
         }
     }
     if (m >= g) {                                                            /* hpp:281 */
@@ -405,7 +444,7 @@ static uint32_t search_ws(const ngog_index* ix, ws* w, const uint32_t* query, fl
         }
         for (uint32_t i = 0; i < nt; ++i) {
             uint32_t t = w->touched[i];
-            emit(ix, w, t, (float)w->cnt[t] / (float)ng, thr, q, m);          /* hpp:300 */
+            emit(ix, w, t, (float)w->cnt[t] / (float)ng, thr, q, m, 0);       /* hpp:300 */
             w->cnt[t] = 0;
         }
     }
@@ -419,7 +458,7 @@ static uint32_t search_ws(const ngog_index* ix, ws* w, const uint32_t* query, fl
     for (uint32_t i = 0; i < n; ++i) {
         uint32_t enc = ~(uint32_t)(w->sortbuf[i] >> 32);
         out_keys[i] = (uint32_t)w->sortbuf[i];
-        out_scores[i] = enc == PROMOTED ? 100.0f : u2f(enc - 1u);
+        out_scores[i] = u2f(enc - 1u);
     }
     return n;
 }

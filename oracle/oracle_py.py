@@ -39,6 +39,9 @@ def lib():
         L.ngo_search.restype = C.c_uint32
         L.ngo_search.argtypes = [C.c_void_p, C.c_char_p, C.c_float, C.c_uint32, C.POINTER(C.c_uint32),
                                  C.POINTER(C.c_float), C.c_uint32]
+        L.ngo_search_amb.restype = C.c_uint32
+        L.ngo_search_amb.argtypes = [C.c_void_p, C.c_char_p, C.c_float, C.c_uint32, C.POINTER(C.c_uint32),
+                                     C.POINTER(C.c_float), C.c_uint32, C.POINTER(C.c_int)]
         L.ngo_search_batch.argtypes = [C.c_void_p, C.POINTER(C.c_char_p), C.c_uint32, C.c_float, C.c_uint32,
                                        C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_float),
                                        C.c_uint32, C.c_int]
@@ -108,6 +111,17 @@ class OracleIndex:
         """Like dllmain.cpp:82 score(): list of (key bytes, fp32 score)."""
         ids, sc = self.score_ids(query, threshold, limit)
         return [(self.key(k), s) for k, s in zip(ids, sc)]
+
+    def score_amb(self, query, threshold: float = 0.0, limit: int = 100):
+        """score() plus whether the reference's answer depends on its unordered_map order beyond
+        (score, length) ties (a promoted key with another pair above 100, ngs_oracle.c header)."""
+        q = query if isinstance(query, bytes) else query.encode("latin-1")
+        cap = max(1, min(limit if limit else 2**31 - 1, self.n_keys()))
+        keys = (C.c_uint32 * cap)()
+        scores = (C.c_float * cap)()
+        amb = C.c_int(0)
+        n = lib().ngo_search_amb(self.h, q, threshold, limit, keys, scores, cap, C.byref(amb))
+        return [(self.key(k), s) for k, s in zip(keys[:n], scores[:n])], bool(amb.value)
 
     def score_batch(self, queries, threshold: float, limit: int, threads: int = 1):
         """Returns (counts[n], keys[n*cap], scores[n*cap], cap) as ctypes arrays."""

@@ -442,6 +442,8 @@ struct Library {
     float w_max = 0.0f;
     bool rank_lists = false;   // DevIndex.rank_post: one weight (w_uniform), one pair per term, one term per key
     uint32_t w_uniform = 0;
+    // DevIndex.kt_off / kt_term (keys with several pairs), built once in upload() for every replica
+    std::vector<uint32_t> kt_off, kt_term;
 
     // ngsSearchDeviceAsync calls in flight: their context stays out of the pool until
     // ngsSearchDeviceWait (the general path and the statistics need the host afterwards)
@@ -587,18 +589,32 @@ bool upload_replica(Library& L, Replica& R, bool keys_unique, bool first) {
     R.owned.push_back(wild_score);
     pt.mark("replica: gram CSR");
     if (!HIP_CHECK(build_wildcard(wild_w, H.n_keys, wild_key, wild_score, nullptr))) return false;
+    X.kt_off = nullptr;
+    X.kt_term = nullptr;
+    if (!L.kt_off.empty()) {
+        uint32_t *kt_off, *kt_term;
+        if (!(dev_upload(&kt_off, L.kt_off, R.owned) && dev_upload(&kt_term, L.kt_term, R.owned))) return false;
+        X.kt_off = kt_off;
+        X.kt_term = kt_term;
+    }
     X.rank_post = nullptr;
     X.w_uniform = L.w_uniform;
-    if (L.rank_lists) {
+    if (L.rank_lists && n_post <= kRankMaxPostings) {
         // the threshold-0 shortcut's rank lists (4 bytes per posting); an index that cannot have them
-        // (over 2^31 postings) searches without them
+        // (over 2^31 postings, or no memory for them) searches without them
         const uint32_t n_seg = H.gram_mode == 1 ? (uint32_t)H.gram_keys.size() : (uint32_t)kGramSpace;
         uint32_t* rp = nullptr;
-        if (!dev_alloc(&rp, n_post + 4)) return false;
-        R.owned.push_back(rp);
-        const hipError_t e = build_rank_post(gram_off, n_seg, post, n_post, tk, H.n_short, H.n_keys, rp, nullptr);
-        if (e == hipSuccess) X.rank_post = rp;
-        else if (e != hipErrorNotSupported && !HIP_CHECK(e)) return false;
+        if (hipMalloc(&rp, sizeof(uint32_t) * (n_post + 4)) == hipSuccess) {
+            const hipError_t e = build_rank_post(gram_off, n_seg, post, n_post, tk, H.n_short, H.n_keys, rp, nullptr);
+            if (e == hipSuccess) {
+                R.owned.push_back(rp);
+                X.rank_post = rp;
+            } else {
+                (void)hipFree(rp);
+                if (e != hipErrorNotSupported && !HIP_CHECK(e)) return false;
+            }
+        }
+        (void)hipGetLastError();
         pt.mark("replica: rank lists");
     }
     X.gram_off = gram_off;
@@ -676,10 +692,29 @@ bool upload(Library& L, const std::vector<int>& devs) {
         std::memcpy(&w, &kw.y, sizeof w);
         if (w > L.w_max) L.w_max = w;  // NaN weights score +0 (pair_enc) and never raise the bound
     }
-    // the threshold-0 shortcut (DevIndex.rank_post) needs one record shape per hit count: one weight
+    // the threshold-0 shortcut (DevIndex.rank_post) needs one record shape per hit count: one weight.
+    // Its one-hit prefix entries stand in for multi-hit records only while a one-hit score is at most
+    // the record's own: w * fl(1/n) <= 100 (a promoted record) needs w <= 200 (n >= 2)
     L.rank_lists = keys_unique && L.tk_identity && !H.tk.empty() && !std::getenv("NGS_NO_RANK_LISTS");
     L.w_uniform = H.tk.empty() ? 0u : H.tk.front().y;
     for (size_t i = 0; L.rank_lists && i < H.tk.size(); ++i) L.rank_lists = H.tk[i].y == L.w_uniform;
+    {
+        float wu;
+        std::memcpy(&wu, &L.w_uniform, sizeof wu);
+        if (!(wu <= 200.0f)) L.rank_lists = false;
+    }
+    // key -> terms for keys with several pairs (DevIndex.kt_off, key_promoted_long)
+    L.kt_off.clear();
+    L.kt_term.clear();
+    if (!keys_unique) {
+        L.kt_off.assign((size_t)H.n_keys + 1, 0);
+        for (const uint2& kw : H.tk) L.kt_off[kw.x + 1]++;
+        for (uint32_t k = 0; k < H.n_keys; ++k) L.kt_off[k + 1] += L.kt_off[k];
+        L.kt_term.resize(H.tk.size() + 1);
+        std::vector<uint32_t> fill(L.kt_off.begin(), L.kt_off.end() - 1);
+        for (uint32_t t = 0; (size_t)t + 1 < H.tk_off.size(); ++t)
+            for (uint32_t p = H.tk_off[t]; p < H.tk_off[t + 1]; ++p) L.kt_term[fill[H.tk[p].x]++] = t;
+    }
     pt.mark("upload: index shape checks");
     for (int d : devs) {
         L.reps.push_back(std::make_unique<Replica>());
@@ -716,6 +751,8 @@ bool upload(Library& L, const std::vector<int>& devs) {
     }
     L.device = devs.front();
     free_uploaded(L.host);
+    std::vector<uint32_t>().swap(L.kt_off);
+    std::vector<uint32_t>().swap(L.kt_term);
     pt.mark("upload: replicas placed");
     return true;
 }

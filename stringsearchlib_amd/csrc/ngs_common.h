@@ -29,8 +29,10 @@ constexpr uint32_t kMaxGramSize = 3;
 
 // Score encoding shared by every stage: enc = bits(max(w*s, +0.0f)) + 1 for finite
 // non-negative scores (fp32 bits of non-negative floats order like the floats), 0 = "key
-// absent", kPromoted = exact match promoted to 100 (nGramSearch.hpp:328-335).
-constexpr uint32_t kPromoted = 0xFFFFFFFFu;
+// absent". An exact match promoted to 100 (nGramSearch.hpp:328-335) is the score 100 itself,
+// kPromoted: ScoreComparer (nGramSearch.h:262-269) ranks a key with w*s > 100 above it and
+// orders a key at exactly 100 against it by length.
+constexpr uint32_t kPromoted = 0x42C80000u + 1u;  // bits(100.0f) + 1
 
 // Candidate record = (~enc) << 32 | key: ascending order == reference order
 // (score desc, then key rank asc; key ranks are assigned by (length, first appearance)).
@@ -283,6 +285,11 @@ struct DevIndex {  // passed by value to kernels; all pointers are device pointe
     // the key ranks of its postings in ascending order (the offsets of post); null otherwise.
     const uint32_t* rank_post;
     uint32_t w_uniform;         // ... the weight's bits
+    // key -> its terms (the pairs transposed), for keys with several pairs: whether a long term
+    // promotes a key whose short pair scores above 100 (key_promoted_long); null when every key
+    // has one pair (keys_unique)
+    const uint32_t* kt_off;     // [n_keys + 1] -> kt_term
+    const uint32_t* kt_term;
 };
 
 constexpr uint64_t kGramEmpty = ~0ull;

@@ -54,6 +54,8 @@ hipError_t launch_pack_pairs(const uint32_t* n, const uint32_t* k, const float* 
 // Wildcard answer (nGramSearch.hpp:356-369): keys sorted by (weight desc, rank asc).
 hipError_t build_wildcard(const float* d_w, uint32_t n_keys, uint32_t* d_keys, float* d_scores, hipStream_t s);
 
+// hipcub's int item count bounds the rank lists' segmented sort
+constexpr uint64_t kRankMaxPostings = 0x7FFFFFFFull;
 // Rank lists of an index (DevIndex.rank_post): out[i] = tk[n_short + post[i]].x, each gram's
 // segment gram_off[c] .. gram_off[c + 1] (c < n_seg) sorted ascending. out holds n_post + 4 entries.
 hipError_t build_rank_post(const uint64_t* gram_off, uint32_t n_seg, const uint32_t* post, uint64_t n_post,

@@ -190,19 +190,10 @@ __device__ bool key_equals_query(const DevIndex& X, uint32_t k, const void* q, u
     return true;
 }
 
-// calcScore's per-pair value (nGramSearch.hpp:326-335) as an order-preserving encoding.
-__device__ __forceinline__ uint32_t pair_enc(uint2 kw, float s, bool promo_possible, const DevIndex& X,
-                                             const void* q, uint32_t qcs, uint32_t m, const uint32_t* valid) {
-    const float sc = __uint_as_float(kw.y) * s;
-    uint32_t enc = sc > 0.0f ? __float_as_uint(sc) + 1u : 1u;  // std::max(w*s, 0.0f) (entry default)
-    if (promo_possible && key_equals_query(X, kw.x, q, qcs, m, valid)) enc = kPromoted;
-    return enc;
-}
-
 // The (key, weight) pairs [p, pe) of survivor term t (calcScore, nGramSearch.hpp:318-336), or none
 // when not even the index's largest weight lifts the term's score s into the running top-L: every
-// pair scores max(w * s, 0) <= max(w_max * s, 0) in fp32, and a record enters only below tau. (An
-// exact match, promoted to 100, is never pruned.) At threshold 0 most survivors share one gram
+// pair scores max(w * s, 0) <= max(w_max * s, 0) in fp32, and a record enters only below tau. (A
+// term that can promote an exact match, s > 0.999, is never pruned.) At threshold 0 most survivors share one gram
 // with the query and are dropped here without a load.
 __device__ __forceinline__ void term_pairs(const DevIndex& X, uint32_t t, float s, bool promo, uint64_t tau,
                                            uint32_t& p, uint32_t& pe) {
@@ -356,6 +347,51 @@ __device__ __forceinline__ uint32_t gram_at(const DevIndex& X, QF qf, uint32_t i
     }
 }
 
+// calcScore merges a query's short scores first and its long scores after them
+// (nGramSearch.hpp:393-394), and a promotion (hpp:335) overwrites what the key had so far: a short
+// pair scoring above 100 of a key that a long term promotes never shows. That long term holds
+// every gram of the query (count n: s = 1 > 0.999) and passes the threshold. Only a key with
+// several pairs can have both (DevIndex.kt_off is null when every key has one).
+__device__ bool key_promoted_long(const DevIndex& X, uint32_t k, const void* q, uint32_t qcs, uint32_t m, float thr) {
+    const uint32_t g = X.gsz, cs = X.csize;
+    if (m < g || 1.0f < thr) return false;  // hpp:281, :315
+    auto qf = [&](uint32_t i) { return char_at(static_cast<const uint8_t*>(q), i, qcs); };
+    for (uint32_t p = X.kt_off[k]; p < X.kt_off[k + 1]; ++p) {
+        const uint32_t t = X.kt_term[p];
+        if (t < X.n_short) continue;
+        const uint64_t a = X.term_off[t], len = X.term_off[t + 1] - a;
+        bool all = true;
+        for (uint32_t i = 0; all && i + g <= m; ++i) {
+            if (gram_at(X, qf, i) == UINT32_MAX) return false;  // a gram with no list is never counted
+            bool hit = false;
+            for (uint64_t j = 0; !hit && j + g <= len; ++j) {
+                bool eq = true;
+                for (uint32_t c = 0; eq && c < g; ++c) eq = char_at(X.term_bytes, a + j + c, cs) == qf(i + c);
+                hit = eq;
+            }
+            all = hit;
+        }
+        if (all) return true;
+    }
+    return false;
+}
+
+// calcScore's per-pair value (nGramSearch.hpp:326-335) as an order-preserving encoding: the
+// score max(w*s, +0), or 100 for an exact match (kPromoted, an ordinary score in ScoreComparer).
+// shortg: the pair's score came from the short search (searchShort, hpp:262-270). 0: the pair
+// never shows (a long promotion of its key overwrites it, key_promoted_long).
+__device__ __forceinline__ uint32_t pair_enc(uint2 kw, float s, bool promo_possible, bool shortg,
+                                             const DevIndex& X, const void* q, uint32_t qcs, uint32_t m,
+                                             const uint32_t* valid, float thr) {
+    const float sc = __uint_as_float(kw.y) * s;
+    const uint32_t enc = sc > 0.0f ? __float_as_uint(sc) + 1u : 1u;  // std::max(w*s, 0.0f) (entry default)
+    if (promo_possible && key_equals_query(X, kw.x, q, qcs, m, valid)) return kPromoted;
+    if (shortg && enc > kPromoted && X.kt_off && key_equals_query(X, kw.x, q, qcs, m, valid) &&
+        key_promoted_long(X, kw.x, q, qcs, m, thr))
+        return 0u;
+    return enc;
+}
+
 // ---------------------------------------------------------------- fused kernel -------
 struct FastSmem {
     uint32_t table[kTableSlots];   // (term - lo + 1) << 8 | count
@@ -443,16 +479,17 @@ struct EmitState {
     uint32_t p, pe;  // pending (key, weight) pairs of the current term
     float s;
     bool promo;
+    bool shortg;     // the term's score is a short-search one
 };
 
 // Appends the pending pairs; false = buffer full (the pair is retried after a flush).
 __device__ __forceinline__ bool emit_pending(EmitState& st, FastSmem& S, const DevIndex& X, uint64_t tau,
-                                             uint32_t m, const uint32_t* valid) {
+                                             uint32_t m, const uint32_t* valid, float thr) {
     while (st.p < st.pe) {
         const uint2 kw = X.tk[st.p];
-        const uint32_t enc = pair_enc(kw, st.s, st.promo, X, S.q, 4u, m, valid);
+        const uint32_t enc = pair_enc(kw, st.s, st.promo, st.shortg, X, S.q, 4u, m, valid, thr);
         const uint64_t rec = ((uint64_t)(~enc) << 32) | kw.x;
-        if (rec < tau) {
+        if (enc && rec < tau) {
             const uint32_t idx = atomicAdd(&S.cand_n, 1u);
             if (idx >= (uint32_t)kCandCap) return false;
             S.cand[idx] = rec;
@@ -467,13 +504,13 @@ __device__ __forceinline__ bool emit_pending(EmitState& st, FastSmem& S, const D
 template <class Next>
 __device__ void produce(FastSmem& S, const DevIndex& X, const SearchParams& P, uint32_t m, uint32_t L,
                         unsigned* err, Next next) {
-    EmitState st{0, 0, 0.0f, false};
+    EmitState st{0, 0, 0.0f, false, false};
     bool done = false;
     for (uint32_t rounds = 0;; ++rounds) {
         bool full = false;
         const uint64_t tau = S.tau;
         while (!full) {
-            if (st.p < st.pe && !emit_pending(st, S, X, tau, m, P.valid)) { full = true; break; }
+            if (st.p < st.pe && !emit_pending(st, S, X, tau, m, P.valid, P.thr)) { full = true; break; }
             if (done) break;
             const int r = next(st);
             if (r == 0) done = true;
@@ -587,6 +624,7 @@ __device__ void long_part(FastSmem& S, const DevIndex& X, const SearchParams& P,
         ++surv;
         st.s = s;
         st.promo = (double)s > 0.999;            // nGramSearch.hpp:328
+        st.shortg = false;
         term_pairs(X, t, s, st.promo, S.tau, st.p, st.pe);
         return 1;
     });
@@ -664,6 +702,7 @@ __device__ void fast_one(const uint32_t q, FastSmem& S, const DevIndex& X, const
             ++surv;
             st.s = s;
             st.promo = (double)s > 0.999;
+            st.shortg = true;
             term_pairs(X, id, s, st.promo, S.tau, st.p, st.pe);
             return 1;
         });
@@ -814,7 +853,7 @@ __device__ void fast_one(const uint32_t q, FastSmem& S, const DevIndex& X, const
         const uint64_t r = S.cand[i];
         const uint32_t enc = ~(uint32_t)(r >> 32);
         out_k[ob + i] = (uint32_t)r;
-        out_s[ob + i] = enc == kPromoted ? 100.0f : __uint_as_float(enc - 1u);
+        out_s[ob + i] = __uint_as_float(enc - 1u);
     }
     if (tid == 0) {
         out_n[q] = nres;
@@ -1203,8 +1242,8 @@ __device__ void wave_emit(SM& S, const DevIndex& X, const SearchParams& P, uint3
             uint64_t rec = kNoCand;
             if (p < pe) {
                 const uint2 kw = X.tk[p++];
-                const uint32_t enc = pair_enc(kw, s, promo, X, S.q, 4u, m, P.valid);
-                rec = ((uint64_t)(~enc) << 32) | kw.x;
+                const uint32_t enc = pair_enc(kw, s, promo, (code & 0x80u) != 0, X, S.q, 4u, m, P.valid, P.thr);
+                if (enc) rec = ((uint64_t)(~enc) << 32) | kw.x;
             }
             if (cand_n + 64 > (uint32_t)kWaveCand) wave_trim(S, cand_n, tau, L, X.keys_unique != 0);
             const bool want = rec < tau;
@@ -2124,7 +2163,7 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
         const uint64_t r = S.cand()[i];
         const uint32_t enc = ~(uint32_t)(r >> 32);
         out_k[ob + i] = (uint32_t)r;
-        out_s[ob + i] = enc == kPromoted ? 100.0f : __uint_as_float(enc - 1u);
+        out_s[ob + i] = __uint_as_float(enc - 1u);
     }
     if (lane == 0) out_n[q] = cand_n;
     if (lane == 0 && !(P.dbg & 32u)) {  // dbg 32: no stats atomics
@@ -3394,7 +3433,8 @@ __device__ __forceinline__ void emit_query(EmitSmem& S, const uint32_t q, const 
             uint32_t p = 0, pe = 0;
             if (i < sn) term_pairs(X, T[0], s, promo, tau, p, pe);  // p == T[0] unless pruned
             uint64_t rec = kNoCand;
-            if (p < pe) rec = ((uint64_t)(~pair_enc(K[0], s, promo, X, S.q, 4u, m, P.valid)) << 32) | K[0].x;
+            // (tier 1a leaves long survivors only: it hands every short-search query over)
+            if (p < pe) rec = ((uint64_t)(~pair_enc(K[0], s, promo, false, X, S.q, 4u, m, P.valid, P.thr)) << 32) | K[0].x;
             if (cand_n + 64 > (uint32_t)kWaveCand) wave_trim<RADIX>(S, cand_n, tau, L, X.keys_unique != 0);
             const bool want = rec < tau;
             const unsigned long long bw = __ballot(want);
@@ -3437,7 +3477,7 @@ __device__ __forceinline__ void emit_query(EmitSmem& S, const uint32_t q, const 
             uint64_t rec = kNoCand;
             if (p < pe) {
                 const uint2 kw = X.tk[p++];
-                const uint32_t enc = pair_enc(kw, s, promo, X, S.q, 4u, m, P.valid);
+                const uint32_t enc = pair_enc(kw, s, promo, false, X, S.q, 4u, m, P.valid, P.thr);
                 rec = ((uint64_t)(~enc) << 32) | kw.x;
             }
             if (cand_n + 64 > (uint32_t)kWaveCand) wave_trim<RADIX>(S, cand_n, tau, L, X.keys_unique != 0);
@@ -3461,7 +3501,7 @@ __device__ __forceinline__ void emit_query(EmitSmem& S, const uint32_t q, const 
         const uint64_t r = S.cand()[i];
         const uint32_t enc = ~(uint32_t)(r >> 32);
         out_k[ob + i] = (uint32_t)r;
-        out_s[ob + i] = enc == kPromoted ? 100.0f : __uint_as_float(enc - 1u);
+        out_s[ob + i] = __uint_as_float(enc - 1u);
     }
     if (lane == 0) {
         out_n[q] = cand_n;
@@ -3565,7 +3605,7 @@ __global__ __launch_bounds__(64) void k_merge(DevIndex X, SearchParams P, const 
             const uint64_t r = S.cand()[k];
             const uint32_t enc = ~(uint32_t)(r >> 32);
             out_k[ob + k] = (uint32_t)r;
-            out_s[ob + k] = enc == kPromoted ? 100.0f : __uint_as_float(enc - 1u);
+            out_s[ob + k] = __uint_as_float(enc - 1u);
         }
         if (lane == 0) {
             out_n[q] = cand_n;
@@ -3576,12 +3616,13 @@ __global__ __launch_bounds__(64) void k_merge(DevIndex X, SearchParams P, const 
 }
 
 // ---------------------------------------------------------------- general path -------
-__device__ __forceinline__ void emit_global(const DevIndex& X, uint32_t t, float s, const uint8_t* q, uint32_t m,
-                                            const uint32_t* valid, uint32_t* kenc) {
+__device__ __forceinline__ void emit_global(const DevIndex& X, uint32_t t, float s, bool shortg, const uint8_t* q,
+                                            uint32_t m, const SearchParams& P, uint32_t* kenc) {
     const bool promo = (double)s > 0.999;
     for (uint32_t p = X.tk_off[t]; p < X.tk_off[t + 1]; ++p) {
         const uint2 kw = X.tk[p];
-        atomicMax(&kenc[kw.x], pair_enc(kw, s, promo, X, q, X.csize, m, valid));
+        const uint32_t enc = pair_enc(kw, s, promo, shortg, X, q, X.csize, m, P.valid, P.thr);
+        if (enc) atomicMax(&kenc[kw.x], enc);
     }
 }
 
@@ -3609,7 +3650,7 @@ __global__ __launch_bounds__(256) void k_gen_long(DevIndex X, SearchParams P, co
                 const uint32_t c = atomicExch(&C[t], 0u);  // first visitor owns the term
                 if (c) {
                     const float s = (float)c / fn;
-                    if (!(s < P.thr)) emit_global(X, X.n_short + t, s, qs, m, P.valid, K);
+                    if (!(s < P.thr)) emit_global(X, X.n_short + t, s, false, qs, m, P, K);
                 }
             }
         }
@@ -3633,7 +3674,7 @@ __global__ __launch_bounds__(256) void k_gen_short(DevIndex X, SearchParams P, c
     const float fm = (float)m;
     for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < end; t += gridDim.x * blockDim.x) {
         const float s = (float)string_match(peq, qc, m, X, t) / fm;
-        if (!(s < P.thr)) emit_global(X, t, s, qs, m, P.valid, K);
+        if (!(s < P.thr)) emit_global(X, t, s, true, qs, m, P, K);
     }
 }
 
@@ -3660,7 +3701,7 @@ __global__ __launch_bounds__(256) void k_gen_write(const uint64_t* __restrict__ 
         const uint64_t r = sorted[i];
         const uint32_t enc = ~(uint32_t)(r >> 32);
         out_k[ob + i] = (uint32_t)r;
-        out_s[ob + i] = enc == kPromoted ? 100.0f : __uint_as_float(enc - 1u);
+        out_s[ob + i] = __uint_as_float(enc - 1u);
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) out_n[q] = cnt;
 }
@@ -3694,7 +3735,7 @@ hipError_t build_rank_post(const uint64_t* gram_off, uint32_t n_seg, const uint3
                            const uint2* tk, uint32_t n_short, uint32_t n_keys, uint32_t* out, hipStream_t s) {
     hipError_t e = hipMemsetAsync(out + n_post, 0, 4 * sizeof(uint32_t), s);  // the 16-byte pad
     if (e != hipSuccess || !n_post) return e;
-    if (n_post > 0x7FFFFFFFull) return hipErrorNotSupported;  // hipcub's int item count
+    if (n_post > kRankMaxPostings) return hipErrorNotSupported;  // hipcub's int item count
     uint32_t* a = nullptr;
     void* temp = nullptr;
     size_t bytes = 0;

@@ -162,6 +162,25 @@ def appendix_a():
                             (".%$ @0123456789abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ\xff\x80\x81",
                              [("x\xffy", 0.0, 0), ("\xff", 0.0, 5), ("zz\xff", 0.3, 0), ("\x80\x81abc", 0.0, 4)]),
                             ("ABC", [("abc", 0.0, 0), ("CAB", 0.0, 0), ("LONGWORD", 0.0, 4)])]))
+    # exact-match promotion against scores above, at and below 100 (nGramSearch.hpp:326-337 with
+    # ScoreComparer h:262-269: a promoted key is the score 100, nothing more)
+    lim = [1, 3, 0]
+    out.append(dict(name="promotion", rowSize=1,
+                    words=["ABCDEFGH", "abcdefgh", "ABCDEFGX", "ABCDEFGHIJ", "BIGWEIGHT1", "BIGWEIGHT2", "XYZW"],
+                    weights=[1.0, 150.0, 1.0, 1000.0, 1000.0, 100.0, 1.0],
+                    phases=[(None, [(q, t, l) for q in ["ABCDEFGH", "abcdefgh", "ABCDEFGHIJ", "BIGWEIGHT1",
+                                                        "BIGWEIGHT2", "BIGWEIGHT", "XYZW", "ABCDEFG"]
+                                    for t in (0.0, 0.3) for l in lim])]))
+    # aliases: w*s == 100 on a shorter key beside a promoted one; a short alias above 100 that the
+    # long pass's promotion overwrites (short scores are merged first, hpp:393-394); a short
+    # promotion under a long alias above 100 (max-merged after it)
+    out.append(dict(name="promotion_alias", rowSize=2,
+                    words=["XY", "ABCDEFGH", "ABCDEFGH", "ABCDEFGX", "ABCDEFG", "ABCDE", "ABCD", "ABCXXXXX",
+                           "QRSTU", "QRSTUVWX", "lower", "LOWERCASE"],
+                    weights=[1.0, 100.0, 1000.0, 1.0, 1.0, 150.0, 1.0, 1000.0, 2.0, 150.0, 1.0, 1000.0],
+                    phases=[(None, [(q, t, l) for q in ["ABCDEFGH", "ABCDEFG", "ABCD", "QRSTU", "QRSTUVWX",
+                                                        "LOWER", "lower", "XY", "ABC"]
+                                    for t in (0.0, 0.3) for l in lim])]))
     return out
 
 
@@ -199,6 +218,15 @@ def synthetic():
     cases = [(q, t, l) for q in qs[:20] for t, l in [(0.3, 50)]] + [(q, 0.0, 30) for q in qs[20:30]] + \
             [(q[:4], 0.25, 40) for q in qs[30:36]] + [(q[:2], 0.5, 40) for q in qs[36:40]]
     out.append(dict(name="synth_rows4", rowSize=4, weights=wts, words=words, phases=[(None, cases)]))
+
+    # S5: weighted with weights around the promotion score (1, 100, 150, 1000, 0, -1), exact keys
+    words, _, rng = gen_corpus(2000, seed=23)
+    pool = [1.0, 100.0, 150.0, 1000.0, 0.0, -1.0, 0.5, 2.0]
+    wts = [pool[rng.next() % len(pool)] for _ in words]
+    qs = gen_queries(words, 1, 40, rng)
+    cases = [(q, 0.3, 100) for q in qs[:20]] + [(q, 0.0, 10) for q in qs[20:40]]
+    cases += [(w, t, l) for w in words[:24] for t, l in [(0.3, 5), (0.0, 1)]]
+    out.append(dict(name="synth_bigw", rowSize=1, weights=wts, words=words, phases=[(None, cases)]))
 
     # S4: many short terms (len 1..12): Levenshtein over shortLib
     words, _, rng = gen_corpus(1500, seed=5, min_len=1, span=12)
