@@ -178,21 +178,36 @@ def cpu_baseline(corpus: Corpus, cfg: dict, raw: bytes, offs: list, target_s: fl
                       f"host threads; index build {build_s:.1f}s not timed"}
 
 
-def dropin_path(L, h, cfg: dict, raw: bytes, offs: list, n_batches: int = 3, n_single: int = 300):
+HOST_PHASES = ("pack_queries", "copy_in_and_queue", "kernels_wait", "device_pack_and_offsets_back",
+               "records_back_and_marshal", "whole_call")
+
+
+def dropin_path(L, h, cfg: dict, raw: bytes, offs: list, n_batches: int = 20, n_single: int = 300):
     """The reference's own entry points on the bench index: scoreBatch over the whole batch (host
-    strings in, new[]'d char** / float* out, released) and single-query score() latency."""
+    strings in, new[]'d char** / float* out, released) and single-query score() latency. The host
+    phases of the timed scoreBatch calls (ngsHostPhases) come with them, in ms per call."""
     B = len(offs) - 1
     qs = [raw[offs[i]:offs[i + 1]] for i in range(B)]
     arr = (C.c_char_p * B)(*qs)
     counts = (C.c_uint32 * B)()
     res, sc = C.POINTER(C.POINTER(C.c_char))(), C.POINTER(C.c_float)()
-    L.scoreBatch(h, arr, B, cfg["threshold"], cfg["limit"], counts, C.byref(res), C.byref(sc))  # warm
-    L.release(h, res, sc)
-    t = time.perf_counter()
-    for _ in range(n_batches):
+    for _ in range(2):  # warm: contexts, pinned staging, the result arrays' heap
         L.scoreBatch(h, arr, B, cfg["threshold"], cfg["limit"], counts, C.byref(res), C.byref(sc))
         L.release(h, res, sc)
+    ph = (C.c_uint64 * 8)()
+    L.ngsHostPhases(ph, 8, 1)
+    per_call = []
+    t = time.perf_counter()
+    for _ in range(n_batches):
+        t1 = time.perf_counter()
+        L.scoreBatch(h, arr, B, cfg["threshold"], cfg["limit"], counts, C.byref(res), C.byref(sc))
+        L.release(h, res, sc)
+        per_call.append(time.perf_counter() - t1)
     batch_s = (time.perf_counter() - t) / n_batches
+    L.ngsHostPhases(ph, 8, 1)
+    ncalls = max(1, ph[6])
+    phases = {name: round(ph[i] / ncalls / 1e6, 4) for i, name in enumerate(HOST_PHASES)}
+    per_call.sort()
     lat = []
     for i in range(n_single + 10):
         t = time.perf_counter()
@@ -201,12 +216,17 @@ def dropin_path(L, h, cfg: dict, raw: bytes, offs: list, n_batches: int = 3, n_s
         L.release(h, res, sc)
     lat = sorted(lat[10:])
     return {"scorebatch_mqs": round(B / batch_s / 1e6, 4), "scorebatch_ms": round(batch_s * 1e3, 3),
+            "scorebatch_calls": n_batches, "scorebatch_ms_min": round(per_call[0] * 1e3, 3),
+            "scorebatch_ms_p50": round(per_call[len(per_call) // 2] * 1e3, 3),
+            "scorebatch_host_phases_ms": phases,
             "score_us_mean": round(sum(lat) / len(lat) * 1e6, 1), "score_us_p50": round(lat[len(lat) // 2] * 1e6, 1)}
 
 
 def c1_latency(device: int, n: int = 2000):
-    """BASELINE configs[0] shape: 1k-row ASCII corpus, gSize 3, rowSize 1, one query per score()
-    call (the reference's SearchTest harness measures 14.7 us per query on its CPU DLL)."""
+    """BASELINE configs[0]: 1k-row ASCII corpus, gSize 3, rowSize 1, no weights, one query per
+    score() call at threshold 0 and limit 100 (the reference's SearchTest
+    harness measures 14.7 us per query on its CPU DLL). c1_score_us_* are at that
+    configuration; c1_thr03_score_us_* repeat them at threshold 0.3."""
     L = _native.lib()
     corpus = Corpus(1000, seed=1)
     h = build_index(corpus, False, device)
@@ -214,11 +234,11 @@ def c1_latency(device: int, n: int = 2000):
     qs = [raw[offs[i]:offs[i + 1]] for i in range(256)]
     res, sc = C.POINTER(C.POINTER(C.c_char))(), C.POINTER(C.c_float)()
 
-    def timed():
+    def timed(thr):
         lat = []
         for i in range(n + 20):
             t = time.perf_counter()
-            L.score(h, qs[i % 256], C.byref(res), C.byref(sc), 0.3, 100)
+            L.score(h, qs[i % 256], C.byref(res), C.byref(sc), thr, 100)
             lat.append(time.perf_counter() - t)
             L.release(h, res, sc)
         lat = sorted(lat[20:])
@@ -226,12 +246,14 @@ def c1_latency(device: int, n: int = 2000):
 
     # the default path: on a library this small score() starts the persistent server kernel by
     # itself after its 4th call (the 20 untimed calls cover that)
-    out = dict(zip(("c1_score_us_mean", "c1_score_us_p50"), timed()))
+    out = {"c1_config": "1k rows, no weights, threshold 0, limit 100, one query per score() call"}
+    out.update(zip(("c1_score_us_mean", "c1_score_us_p50"), timed(0.0)))
+    out.update(zip(("c1_thr03_score_us_mean", "c1_thr03_score_us_p50"), timed(0.3)))
     if hasattr(L, "ngsServeState"):
         out["c1_score_served"] = L.ngsServeState(h) == 2
     # the same calls with the server turned off (ngsServe(h, 0)): a kernel launch sequence per call
     if hasattr(L, "ngsServe") and L.ngsServe(h, 0) == 0:
-        out.update(zip(("c1_launch_us_mean", "c1_launch_us_p50"), timed()))
+        out.update(zip(("c1_launch_us_mean", "c1_launch_us_p50"), timed(0.0)))
     L.dispose(h)
     corpus.free()
     return out
@@ -249,12 +271,16 @@ class StepLoop:
     ranks of the elapsed time. tests/test_bench_loop.py drives it on CPU (gloo, world size 2)
     with the oracle standing in for the library."""
 
-    def __init__(self, L, h, d_raw, d_off, B, threshold, limit, stride, depth, world, dev, stream):
+    def __init__(self, L, h, d_raw, d_off, B, threshold, limit, stride, depth, world, dev, stream,
+                 gather_cap=None):
         self.L, self.h, self.d_raw, self.d_off, self.B = L, h, d_raw, d_off, B
         self.threshold, self.limit, self.stride = threshold, limit, stride
         self.depth, self.world, self.dev, self.stream = max(1, depth), world, dev, stream
         self.nbuf = self.depth + 1 if self.depth > 1 else (2 if world > 1 else 1)
         self.gbs = [shard.PackedGather(B, stride, B, dev) for _ in range(self.nbuf)]
+        # the record capacity of the packed gathers (N > 1): held by every rank, grown when a retired
+        # gather's all-reduced total overflowed it (then gathered again), no host read in the step
+        self.cap = shard.GatherCap(B, stride, gather_cap)
         self.st = _native.NgsStats()
         self.pending = {}  # buffer index -> in-flight top-k gather (N > 1)
         self.inflight = collections.deque()  # (ticket, buffer index) of queued batches (depth > 1)
@@ -269,7 +295,7 @@ class StepLoop:
         self.ktimes.append((self.st.fast_kernel_ms, self.st.prep_kernel_ms, self.st.general_ms))
         if self.world > 1:  # packed on the device, gathered up to the largest record count of the ranks
             gb = self.gbs[i].pack(getattr(self.L, "ngsPackResults", None), self.stream)
-            pg = shard.gather_packed(gb, async_op=True)  # overlaps the next batches
+            pg = shard.gather_packed(gb, async_op=True, cap=self.cap)  # overlaps the next batches
             self.gather_words.append(pg.words)
             self.pending[i] = pg
             if self.keep_gathers:
@@ -319,6 +345,7 @@ class StepLoop:
         for _ in range(warmup):
             self.step()
         self.drain()
+        self.regathers_warmup = self.cap.regathers
         self.ktimes.clear()
         self.gathered.clear()
         self.gather_words.clear()
@@ -480,7 +507,9 @@ def main():
         out["detail"]["gather"] = {
             "bytes_per_rank_step": round(4 * sum(loop.gather_words) / len(loop.gather_words)),
             "fixed_layout_bytes": 4 * (1 + B * (1 + 2 * stride)),
-            "note": "packed [batch, total, counts, {key, score} records] up to the largest total of the ranks"}
+            "regathers": int(loop.cap.regathers), "cap_records": int(loop.cap.total),
+            "note": "packed [batch, total, counts, {key, score} records] up to a record capacity every rank "
+                    "holds; an overflowing batch is gathered again whole when its gather is retired"}
     if rank == 0 and world == 1 and not args.no_dropin and not corpus.wide:
         out["detail"]["dropin"] = dropin_path(L, h, cfg, raw, offs)
         out["detail"]["dropin"].update(c1_latency(local))

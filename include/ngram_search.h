@@ -261,6 +261,13 @@ NGS_API uint32_t ngsLoadIndex(const char* path);
  * first 16 hex digits of the SHA-256 of the sources the library was compiled from. */
 NGS_API const char* ngsVersion(void);
 
+/* Diagnostics: the host batch path's phases (scoreBatch / searchBatch / batch score paths of more
+ * than 16 queries), nanoseconds summed over the calls since the last reset: [0] query packing,
+ * [1] copies in + kernels queued, [2] kernels waited for, [3] device pack + offsets back,
+ * [4] records back + marshalling, [5] whole calls, [6] number of calls. Writes min(n, 7) values,
+ * resets them all if `reset`, returns 7. */
+NGS_API int ngsHostPhases(uint64_t* out, int n, int reset);
+
 /* Diagnostics: per-phase time of the LDS kernels (s_memtime shader-clock ticks, summed over
  * waves / blocks) in the instrumented build libngram_search_prof.so; -1 in the regular build. */
 NGS_API int ngsPhaseStats(uint64_t* out, int n, int reset);

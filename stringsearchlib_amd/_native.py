@@ -164,6 +164,8 @@ def lib():
     L.ngsSaveIndex.argtypes = [u32, cp]
     L.ngsLoadIndex.restype = u32
     L.ngsLoadIndex.argtypes = [cp]
+    L.ngsHostPhases.restype = C.c_int
+    L.ngsHostPhases.argtypes = [C.POINTER(C.c_uint64), C.c_int, C.c_int]
     L.ngsPhaseStats.restype = C.c_int
     L.ngsPhaseStats.argtypes = [C.POINTER(C.c_uint64), C.c_int, C.c_int]
     version = L.ngsVersion().decode()

@@ -61,16 +61,31 @@ bool hip_ok(hipError_t e, const char* what) {
 }
 #define HIP_CHECK(expr) hip_ok((expr), #expr)
 
-// NGS_HOST_TIMING=1 (diagnostics): the host batch path prints its phases (microseconds since
-// the previous mark) to stderr
+// Phases of the host batch path (scoreBatch / searchBatch): nanoseconds summed over the calls since
+// the last reset, read by ngsHostPhases (bench.py's detail.dropin). NGS_HOST_TIMING=1 also prints
+// each phase (microseconds since the previous mark) to stderr.
+enum HostPhase : int {
+    kHpPack = 0,      // query lengths, offsets and bytes packed into pinned staging
+    kHpQueue,         // H2D copies and the kernels queued
+    kHpWait,          // the kernels, waited for
+    kHpPackBack,      // the device pack of the results and the offsets back
+    kHpRecords,       // the records back, marshalled into the new[]'d arrays as they land
+    kHpCall,          // the whole call (scoreBatch / searchBatch)
+    kHpCalls,         // (count) calls
+    kHpN
+};
+std::atomic<uint64_t> g_host_phase[kHpN];
 struct HostTimer {
     bool on;
     std::chrono::steady_clock::time_point t;
     HostTimer() : on(std::getenv("NGS_HOST_TIMING") != nullptr), t(std::chrono::steady_clock::now()) {}
-    void mark(const char* what) {
-        if (!on) return;
+    void mark(int id, const char* what) {
         const auto n = std::chrono::steady_clock::now();
-        std::fprintf(stderr, "[ngs host] %-28s %9.1f us\n", what, std::chrono::duration<double, std::micro>(n - t).count());
+        g_host_phase[id].fetch_add((uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(n - t).count(),
+                                   std::memory_order_relaxed);
+        if (on)
+            std::fprintf(stderr, "[ngs host] %-28s %9.1f us\n", what,
+                         std::chrono::duration<double, std::micro>(n - t).count());
         t = n;
     }
 };
@@ -1204,7 +1219,7 @@ bool queue_host_chunk(Library& L, Replica& R, Context& c, const CharT* const* qu
             for (size_t i = a; i < e; ++i)
                 if (queries[q0 + i]) std::memcpy(hr + ho[i], queries[q0 + i], ho[i + 1] - ho[i]);
         });
-        ht.mark("pack queries");
+        ht.mark(kHpPack, "pack queries");
         ok = ensure_queries(c, B, qbytes) && ensure_outputs(c, B, stride) &&
              HIP_CHECK(hipMemcpyAsync(c.d_raw, c.h_raw.p, qbytes, hipMemcpyHostToDevice, c.stream)) &&
              HIP_CHECK(hipMemcpyAsync(c.d_off, ho, sizeof(uint64_t) * (B + 1), hipMemcpyHostToDevice, c.stream));
@@ -1218,7 +1233,7 @@ bool queue_host_chunk(Library& L, Replica& R, Context& c, const CharT* const* qu
     if (queue_search(L, R, c, h.d_raw, h.d_off, B, qbytes, thr, Lm, (uint32_t)stride, h.d_n, h.d_k, h.d_s, c.stream,
                      h.P, h.small) != 0)
         return false;
-    ht.mark("copy in + queue kernels");
+    ht.mark(kHpQueue, "copy in + queue kernels");
     return !h.small || HIP_CHECK(hipMemcpyAsync(c.h_sio, c.d_sio, kSioStats + h.block, hipMemcpyDeviceToHost, c.stream));
 }
 
@@ -1237,7 +1252,7 @@ bool finish_host_chunk(Library& L, Replica& R, HostChunk& h, uint32_t Lm, std::v
     const int frc = finish_search(L, R, c, B, h.P, h.d_off, h.d_n, h.d_k, h.d_s, c.stream, h.small);
     if (frc == kRetryQcap) t_last_error = kErrQueryBuffer;  // cannot happen: the host path sizes the buffer
     if (frc != 0) return false;
-    ht.mark("wait for kernels");
+    ht.mark(kHpWait, "wait for kernels");
     if (h.small) {
         const uint32_t* counts3 = reinterpret_cast<const uint32_t*>(c.h_sio) + kStatSlots * 16;
         if (counts3[0]) {  // the general path ran after the read-back: read the results again
@@ -1276,7 +1291,7 @@ bool finish_host_chunk(Library& L, Replica& R, HostChunk& h, uint32_t Lm, std::v
         !HIP_CHECK(hipMemcpyAsync(c.h_res.p, c.d_pos, sizeof(uint32_t) * (B + 1), hipMemcpyDeviceToHost, c.stream)) ||
         !HIP_CHECK(hipStreamSynchronize(c.stream)))
         return false;
-    ht.mark("pack + offsets back");
+    ht.mark(kHpPackBack, "pack + offsets back");
     const uint32_t total = c.h_res.as<uint32_t>()[B];
     for (uint32_t i = 0; i < B; ++i) counts[q0 + i] = c.h_res.as<uint32_t>()[i + 1] - c.h_res.as<uint32_t>()[i];
     const size_t esz = h.pcs ? sizeof(uint64_t) : sizeof(uint32_t);
@@ -1306,7 +1321,7 @@ bool finish_host_chunk(Library& L, Replica& R, HostChunk& h, uint32_t Lm, std::v
         emit(static_cast<const void*>(hr + a * esz), reinterpret_cast<const float*>(hr + rb) + a, (uint32_t)n, last,
              total);
     }
-    ht.mark("records back + emit");
+    ht.mark(kHpRecords, "records back + emit");
     return true;
 }
 
@@ -1653,17 +1668,18 @@ uint32_t batch_query(uint32_t handle, const CharT* const* queries, uint32_t nq, 
             delete[] out_s;
             return 0;
         }
-        ht.mark("search + marshal (chunks)");
+        ht.mark(kHpCall, "search + marshal (chunks)");
+        g_host_phase[kHpCalls].fetch_add(1, std::memory_order_relaxed);
         std::copy(cnt.begin(), cnt.end(), counts);
         *results = res;
         if (scores) *scores = out_s;
         return (uint32_t)off;
     }
     if (!host_search(*L, queries, nq, thr, limit, cnt, keys, sc)) return 0;
-    ht.mark("search (all chunks)");
     std::copy(cnt.begin(), cnt.end(), counts);
     const uint32_t n = marshal(*L, keys, sc, results, scores);
-    ht.mark("marshal");
+    ht.mark(kHpCall, "search + marshal");
+    if (nq >= kSmallBatch) g_host_phase[kHpCalls].fetch_add(1, std::memory_order_relaxed);
     return n;
 }
 
@@ -2310,6 +2326,13 @@ NGS_API uint32_t ngsLoadIndex(const char* path) {
         }
     }
     return handle;
+}
+
+NGS_API int ngsHostPhases(uint64_t* out, int n, int reset) {
+    const int k = std::min<int>(n, kHpN);
+    for (int i = 0; i < k; ++i) out[i] = reset ? g_host_phase[i].exchange(0) : g_host_phase[i].load();
+    for (int i = k; reset && i < kHpN; ++i) g_host_phase[i].store(0);
+    return kHpN;
 }
 
 NGS_API int ngsPhaseStats(uint64_t* out, int n, int reset) {

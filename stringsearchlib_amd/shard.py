@@ -7,10 +7,13 @@ nothing else crosses ranks.
 
 bench.py's step loop gathers packed records (PackedGather): a finished batch's results are
 packed on the device (ngsPackResults: a prefix sum of the counts and one {key, score} pair per
-record), the ranks agree on the largest record count with one 8-byte all-reduce, and the gather
-moves [batch, total, counts, records] only up to that count, so the bytes on xGMI follow the
-results (about 20 per query at C3) instead of the output stride (100). The gather itself runs on
-RCCL's stream beside the next batch's kernels. GatherBuffer / gather_to_root are the fixed-size
+record) and the gather moves [batch, total, counts, records] up to a record capacity every rank
+already holds (GatherCap), so the bytes on xGMI follow the results (about 20 per query at C3)
+instead of the output stride (100), with no host read in the step. An 8-byte all-reduce of the
+batch's largest total travels beside the gather; when the gather is retired (its buffer is about
+to be rewritten, a step or more later) every rank reads that total, and if it exceeded the
+capacity the buffers are gathered again whole and the capacity grows. The gathers run on RCCL's
+stream beside the next batch's kernels. GatherBuffer / gather_to_root are the fixed-size
 form (no size agreement: batch x stride records per rank), kept for callers that hold tensors.
 """
 from __future__ import annotations
@@ -190,34 +193,98 @@ class PackedGather:
         return counts, rec[:, 0].contiguous(), rec[:, 1].contiguous().view(torch.float32)
 
 
-class PendingPacked:
-    """An in-flight packed gather: ``complete()`` orders the current stream after it; ``wait()`` returns
-    the per-rank (counts, keys, scores) on rank 0 and None elsewhere."""
+class GatherCap:
+    """The record capacity (per rank) of the packed gathers: a number every rank holds without
+    exchanging it, because it only changes in PendingPacked.complete(), which every rank calls for
+    the same gather at the same step. It starts at a quarter of the fixed layout (``initial``
+    overrides) and grows past any overflowing total by an eighth."""
 
-    def __init__(self, work, pg: PackedGather, bufs, rank, words):
+    def __init__(self, pad_b: int, stride: int, initial: int | None = None):
+        self.limit = max(1, pad_b * stride)
+        self.total = min(self.limit, max(1, initial if initial is not None else self.limit // 4))
+        self.regathers = 0
+
+    def observe(self, total: int) -> bool:
+        """The all-reduced largest total of a retired gather; True if it overflowed the capacity."""
+        over = total > self.total
+        if over:
+            self.total = min(self.limit, total + total // 8 + 64)
+        return over
+
+
+class PendingPacked:
+    """An in-flight packed gather: ``complete()`` orders the current stream after it, reads the
+    batch's all-reduced largest total (copied to the host beside the gather, so the read waits for
+    nothing newer) and gathers the buffers again in full if the capacity was too small;
+    ``wait()`` returns the per-rank (counts, keys, scores) on rank 0 and None elsewhere."""
+
+    def __init__(self, work, pg: PackedGather, bufs, rank, words, group, cap: GatherCap, tot_work, tot_host,
+                 tot_event):
         self.work, self.pg, self.bufs, self.rank, self.words = work, pg, bufs, rank, words
+        self.group, self.cap, self.tot_work, self.tot_host, self.tot_event = group, cap, tot_work, tot_host, tot_event
+        self.done = False
+        self.regathered = False
 
     def complete(self):
+        if self.done:
+            return
+        self.done = True
         self.work.wait()
+        if self.tot_event is not None:
+            self.tot_event.synchronize()
+        else:
+            self.tot_work.wait()
+        total = int(self.tot_host[0])
+        if total > (self.words - 2 - self.pg.pad_b) // 2:  # some rank's records did not fit: gather them whole
+            words = PackedGather.words(self.pg.pad_b, total)
+            world = dist.get_world_size(self.group)
+            bufs = [torch.empty(words, dtype=torch.int32, device=self.pg.buf.device)
+                    for _ in range(world)] if self.rank == 0 else None
+            dist.gather(self.pg.buf[:words], bufs, dst=0, group=self.group)
+            self.bufs, self.words, self.regathered = bufs, words, True
+            self.cap.regathers += 1
+        self.cap.observe(total)
 
     def wait(self):
-        self.work.wait()
+        self.complete()
         if self.rank != 0:
             return None
         return [PackedGather.decode(b, self.pg.pad_b) for b in self.bufs]
 
 
-def gather_packed(pg: PackedGather, group=None, async_op: bool = False):
-    """Gathers every rank's packed buffer (already packed) on rank 0: one 8-byte all-reduce agrees on
-    the largest record count (a host read of it), then one gather of the buffers' prefixes of that
-    size. Bytes per rank: 4 * (2 + pad_b + 2 * max total)."""
+def gather_packed(pg: PackedGather, group=None, async_op: bool = False, cap: GatherCap | None = None):
+    """Gathers every rank's packed buffer (already packed) on rank 0: the prefix of
+    ``cap.total`` records (a quarter of the fixed layout without a cap), plus an 8-byte all-reduce of the
+    largest total that PendingPacked.complete() checks. No host read of this batch. Bytes per rank:
+    4 * (2 + pad_b + 2 * cap.total)."""
+    cap = cap or GatherCap(pg.pad_b, pg.stride)
     tot = pg.buf[1:2].to(torch.int64)
-    dist.all_reduce(tot, op=dist.ReduceOp.MAX, group=group)
-    words = PackedGather.words(pg.pad_b, int(tot.item()))
+    tot_work = dist.all_reduce(tot, op=dist.ReduceOp.MAX, group=group, async_op=True)
+    tot_host, tot_event = tot, None
+    if tot.is_cuda:  # the total to pinned host memory on a side stream, ordered after the all-reduce
+        side = _side_stream(tot.device)
+        side.wait_stream(torch.cuda.current_stream(tot.device))
+        with torch.cuda.stream(side):
+            tot_work.wait()
+            tot_host = torch.empty(1, dtype=torch.int64, pin_memory=True)
+            tot_host.copy_(tot, non_blocking=True)
+            tot_event = torch.cuda.Event()
+            tot_event.record(side)
+        tot.record_stream(side)
+    words = PackedGather.words(pg.pad_b, cap.total)
     rank = dist.get_rank(group)
     world = dist.get_world_size(group)
     send = pg.buf[:words]
     bufs = [torch.empty(words, dtype=torch.int32, device=pg.buf.device) for _ in range(world)] if rank == 0 else None
     work = dist.gather(send, bufs, dst=0, group=group, async_op=True)
-    pending = PendingPacked(work, pg, bufs, rank, words)
+    pending = PendingPacked(work, pg, bufs, rank, words, group, cap, tot_work, tot_host, tot_event)
     return pending if async_op else pending.wait()
+
+
+_SIDE = {}
+
+
+def _side_stream(device):
+    if device not in _SIDE:
+        _SIDE[device] = torch.cuda.Stream(device)
+    return _SIDE[device]

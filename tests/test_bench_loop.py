@@ -6,7 +6,9 @@ buffers the loop hands it, so the loop itself runs as on the GPU box: gather buf
 up to `depth` batches in flight, a batch's gather issued when it completes and ordered before its
 buffer is rewritten (PendingGather.complete), the drain inside the timed region, the barriers and
 the max-over-ranks elapsed time. Rank 0 decodes every gathered buffer of the timed steps and
-checks each against the whole batch scored in one piece.
+checks each against the whole batch scored in one piece. The packed gathers start at a record
+capacity below what the batches return (gather_cap), so the first ones overflow: they are
+gathered again whole when retired and the capacity grows; the later ones fit.
 """
 import ctypes as C
 import os
@@ -79,7 +81,7 @@ class FakeLib:
         return 0
 
 
-def _worker(rank, world, port, depth, result_path):
+def _worker(rank, world, port, depth, result_path, gather_cap):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -95,7 +97,8 @@ def _worker(rank, world, port, depth, result_path):
             offs.append(offs[-1] + len(q))
         off = torch.tensor(offs, dtype=torch.int64)
         fake = FakeLib(oi, [raw, off])
-        loop = bench.StepLoop(fake, 1, raw, off, B, THR, LIMIT, LIMIT, depth, world, torch.device("cpu"), None)
+        loop = bench.StepLoop(fake, 1, raw, off, B, THR, LIMIT, LIMIT, depth, world, torch.device("cpu"), None,
+                              gather_cap=gather_cap)
         for gb in loop.gbs:
             fake.register(gb.counts, gb.keys, gb.scores)
         loop.keep_gathers = True
@@ -115,6 +118,9 @@ def _worker(rank, world, port, depth, result_path):
         # the packed gather moves the records, not B x stride
         assert len(loop.gather_words) == steps
         assert all(w < 1 + B * (1 + 2 * LIMIT) for w in loop.gather_words), loop.gather_words
+        if gather_cap is not None:  # the overflow path ran during the warm-up, then the capacity held
+            assert loop.regathers_warmup >= 1 and loop.cap.total > gather_cap
+            assert loop.cap.regathers == loop.regathers_warmup, (loop.cap.regathers, loop.regathers_warmup)
         if rank == 0:
             assert len(loop.gathered) == steps
             want = [tuple(map(list, oi.score_ids(q, THR, LIMIT))) for q in queries[:B * world]]
@@ -142,7 +148,8 @@ def _worker(rank, world, port, depth, result_path):
 
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("depth", [1, 2, 3])
-def test_step_loop_two_ranks(tmp_path, depth):
+@pytest.mark.parametrize("gather_cap", [None, 4])
+def test_step_loop_two_ranks(tmp_path, depth, gather_cap):
     out = tmp_path / "result.txt"
-    mp.spawn(_worker, args=(2, _free_port(), depth, str(out)), nprocs=2, join=True)
+    mp.spawn(_worker, args=(2, _free_port(), depth, str(out), gather_cap), nprocs=2, join=True)
     assert out.read_text() == "ok"
