@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -37,7 +38,6 @@ constexpr size_t kGeneralBudget = size_t(2) << 30;   // bytes of dense general-p
 constexpr uint32_t kSmallBatch = 16;                 // host batches up to this many queries take the latency path
 constexpr size_t kSmallBlock = size_t(1) << 20;      // ... if their output block is at most this many bytes
 constexpr size_t kPartBudget = size_t(1) << 30;      // bytes of sliced tier-1b partial results per call
-constexpr uint32_t kSmallWaves = 1;                  // ... with this many waves per query (k_wave<W>)
 constexpr uint32_t kSmallSlices = 32;                // ... or term-id slices per query (sliced k_wave<1>)
 constexpr size_t kSmallQ = size_t(64) << 10;         // ... and if their offsets + bytes fit this many bytes
 // the latency path's one block, device and pinned host: statistics | results | queries
@@ -220,7 +220,7 @@ struct Context {
     hipStream_t stream = nullptr;
     hipStream_t side = nullptr;      // the heavy list (cmin 2) beside tier 1a
     hipStream_t side2 = nullptr;     // tier 1b on the full list (cmin 1, short search) beside both
-    hipEvent_t fork = nullptr, join = nullptr, join2 = nullptr;
+    hipEvent_t join = nullptr, join2 = nullptr;
     hipEvent_t prep_ev = nullptr, lists_ev = nullptr;  // k_prep done (s), heavy / full lists merged (side)
     hipEvent_t in_ev = nullptr;   // ngsSearchDeviceAsync: the caller's stream up to the call
     hipEvent_t ev[6] = {};
@@ -285,7 +285,7 @@ struct Context {
         if (h_sio) hipHostFree(h_sio);
         for (hipEvent_t e : ev)
             if (e) hipEventDestroy(e);
-        for (hipEvent_t e : {fork, join, join2, prep_ev, lists_ev, in_ev})
+        for (hipEvent_t e : {join, join2, prep_ev, lists_ev, in_ev})
             if (e) hipEventDestroy(e);
         for (hipEvent_t e : piece_ev)
             if (e) hipEventDestroy(e);
@@ -334,6 +334,34 @@ struct Replica {
     std::vector<void*> owned;
     std::mutex pool_mu;
     std::vector<std::unique_ptr<Context>> pool;
+    // DevIndex.kt_flag per validChar set in use (indexes with kt_off only): made once per set, kept
+    // until dispose (a launch in flight may still read an older set's)
+    std::mutex kflag_mu;
+    std::vector<std::pair<std::array<uint32_t, 8>, uint8_t*>> kflags;
+
+    // the index as the kernels of a search under `valid` see it (kt_flag for that set); false on a
+    // HIP failure
+    bool index_for(const uint32_t valid[8], DevIndex& X) {
+        X = dev;
+        X.kt_flag = nullptr;
+        if (!dev.kt_off) return true;
+        std::array<uint32_t, 8> v;
+        std::copy(valid, valid + 8, v.begin());
+        std::lock_guard<std::mutex> g(kflag_mu);
+        for (auto& e : kflags)
+            if (e.first == v) {
+                X.kt_flag = e.second;
+                return true;
+            }
+        uint8_t* f = nullptr;
+        if (!HIP_CHECK(hipSetDevice(device)) || !HIP_CHECK(hipMalloc(&f, std::max<size_t>(dev.n_keys, 1)))) return false;
+        owned.push_back(f);
+        // synchronously: a search on another stream may use the set as soon as it is listed
+        if (!HIP_CHECK(build_key_flags(dev, valid, f, nullptr)) || !HIP_CHECK(hipStreamSynchronize(nullptr))) return false;
+        kflags.emplace_back(v, f);
+        X.kt_flag = f;
+        return true;
+    }
 
     ~Replica() {
         pool.clear();
@@ -354,7 +382,6 @@ struct Replica {
         c->device = device;
         // (the side streams are made by the first call whose batch needs them, queue_search)
         if (!HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) ||
-            !HIP_CHECK(hipEventCreateWithFlags(&c->fork, hipEventDisableTiming)) ||
             !HIP_CHECK(hipEventCreateWithFlags(&c->join, hipEventDisableTiming)) ||
             !HIP_CHECK(hipEventCreateWithFlags(&c->join2, hipEventDisableTiming)) ||
             !HIP_CHECK(hipEventCreateWithFlags(&c->prep_ev, hipEventDisableTiming)) ||
@@ -404,6 +431,7 @@ struct Server {
     uint32_t* list2 = nullptr;
     uint64_t seq = 0;
     bool launched = false;
+    uint32_t launch_valid[8] = {};  // the validChar set of its DevIndex.kt_flag
 
     bool init(int dev) {
         device = dev;
@@ -923,7 +951,7 @@ bool ensure_general(const Replica& R, Context& c, hipStream_t s) {
 // lists, no side streams; the latency path of score() and small batches).
 int queue_search(Library& L, Replica& R, Context& c, const uint8_t* d_raw, const uint64_t* d_off, uint32_t B,
                  uint64_t qbytes, float thr, uint32_t limit, uint32_t stride, uint32_t* d_n, uint32_t* d_k,
-                 float* d_s, hipStream_t s, SearchParams& P, bool small, bool defer_heavy = false) {
+                 float* d_s, hipStream_t s, SearchParams& P, bool small) {
     // small: the statistics go to the latency block (zeroed by k_prep, read back by the caller
     // together with the results)
     DevStats* sd = small ? reinterpret_cast<DevStats*>(c.d_sio) : c.d_stats;
@@ -938,28 +966,8 @@ int queue_search(Library& L, Replica& R, Context& c, const uint8_t* d_raw, const
         return e ? (uint32_t)std::strtoul(e, nullptr, 0) : 0u;
     }();
     P.dbg = dbg;
-    static const uint32_t waves = [] {  // experiment override of the tier-1 waves per query
-        const char* e = std::getenv("NGS_WAVES");
-        const uint32_t w = e ? (uint32_t)std::strtoul(e, nullptr, 0) : kDefaultWaves;
-        return w == 0 || w == 1 || w == 2 || w == 4 ? w : kDefaultWaves;
-    }();
-    static const uint32_t small_waves = [] {  // waves per query of the latency path
-        const char* e = std::getenv("NGS_SMALL_WAVES");
-        const uint32_t w = e ? (uint32_t)std::strtoul(e, nullptr, 0) : kSmallWaves;
-        return w == 1 || w == 2 || w == 4 ? w : kSmallWaves;
-    }();
-    P.waves = small ? small_waves : waves;
-    static const uint32_t heavy_waves = [] {
-        const char* e = std::getenv("NGS_HEAVY_WAVES");
-        const uint32_t w = e ? (uint32_t)std::strtoul(e, nullptr, 0) : kHeavyWaves;
-        return w == 1 || w == 2 || w == 4 ? w : kHeavyWaves;
-    }();
-    P.heavy_waves = heavy_waves;
-    static const uint32_t heavy_grid = [] {
-        const char* e = std::getenv("NGS_HEAVY_GRID");
-        return e ? (uint32_t)std::strtoul(e, nullptr, 0) : kHeavyGrid;
-    }();
-    P.heavy_grid = heavy_grid;
+    // tier 1: the lean kernel with tier 1b on its hand-overs (batches), or tier 1b alone (the latency path)
+    P.waves = small ? 1u : 0u;
     {
         std::lock_guard<std::mutex> g(L.valid_mu);
         std::memcpy(P.valid, L.valid, sizeof(P.valid));
@@ -1026,14 +1034,16 @@ int queue_search(Library& L, Replica& R, Context& c, const uint8_t* d_raw, const
     if (!small && !HIP_CHECK(hipMemsetAsync(c.d_stats, 0, sizeof(DevStats) * (kStatSlots + 1 + 2 * kListSlots), s)))
         return -4;
     if (timing) HIP_CHECK(hipEventRecord(c.ev[0], s));
-    if (!HIP_CHECK(launch_prep(d_raw, d_off, B, P, c.d_norm, c.d_qm, R.dev.csize, R.dev, c.d_heavy, gc + 3, c.d_full,
+    DevIndex X;
+    if (!R.index_for(P.valid, X)) return -4;
+    if (!HIP_CHECK(launch_prep(d_raw, d_off, B, P, c.d_norm, c.d_qm, X.csize, X, c.d_heavy, gc + 3, c.d_full,
                                gc + 5, c.d_lslots, c.d_lctr, s, side, c.prep_ev, c.lists_ev)))
         return -4;
     if (timing) HIP_CHECK(hipEventRecord(c.ev[1], s));
     if (timing) HIP_CHECK(hipEventRecord(c.ev[2], s));
-    if (!HIP_CHECK(launch_fast(R.dev, P, c.d_norm, d_off, c.d_qm, d_n, d_k, d_s, c.d_list2, gc + 1, c.d_fb, gc + 2,
+    if (!HIP_CHECK(launch_fast(X, P, c.d_norm, d_off, c.d_qm, d_n, d_k, d_s, c.d_list2, gc + 1, c.d_fb, gc + 2,
                                c.d_fb2, gc + 4, c.d_heavy, gc + 3, c.d_full, gc + 5, c.d_glist, gc, sd, s, side,
-                               side2, c.fork, c.join, c.join2, c.lists_ev, defer_heavy, all_heavy && !NGS_NO_SKIP_EMPTY)))
+                               side2, c.join, c.join2, c.lists_ev, all_heavy && !NGS_NO_SKIP_EMPTY)))
         return -4;
     if (timing) HIP_CHECK(hipEventRecord(c.ev[3], s));
     // the statistics and the path counts in one read-back (the general path adds no statistics)
@@ -1059,12 +1069,14 @@ int finish_search(Library& L, Replica& R, Context& c, uint32_t B, const SearchPa
             return -4;
         std::sort(gl.begin(), gl.end());
         if (!ensure_general(R, c, s)) return -4;
+        DevIndex X;
+        if (!R.index_for(P.valid, X)) return -4;
         if (timing) HIP_CHECK(hipEventRecord(c.ev[4], s));
         for (uint32_t g0 = 0; g0 < ngen; g0 += c.gen.G) {
             const uint32_t G = std::min(c.gen.G, ngen - g0);
             if (!HIP_CHECK(hipMemcpyAsync(c.d_group, gl.data() + g0, sizeof(uint32_t) * G, hipMemcpyHostToDevice, s)))
                 return -4;
-            if (!HIP_CHECK(run_general(R.dev, P, c.d_norm, d_off, c.d_qm, c.d_group, gl.data() + g0, G, c.gen, d_n,
+            if (!HIP_CHECK(run_general(X, P, c.d_norm, d_off, c.d_qm, c.d_group, gl.data() + g0, G, c.gen, d_n,
                                        d_k, d_s, s)))
                 return -4;
         }
@@ -1525,6 +1537,8 @@ bool serve_query(Library& L, const char* query, float thr, uint32_t limit, std::
         if (!host_normalise(L.valid, query, b->q, kServeMaxQuery, m)) return false;
         std::memcpy(b->valid, L.valid, sizeof(b->valid));
     }
+    // a running server reads the key flags of the validChar set it was launched with
+    if (R.dev.kt_off && !sv->stopped() && std::memcmp(sv->launch_valid, b->valid, sizeof(b->valid)) != 0) sv->stop();
     b->thr = thr;
     b->limit = Lm;
     b->m = m;
@@ -1536,7 +1550,10 @@ bool serve_query(Library& L, const char* query, float thr, uint32_t limit, std::
         SearchParams P{};
         P.n_queries = 1;
         P.nslices = 1;
-        sv->launched = HIP_CHECK(launch_serve(R.dev, P, sv->d, sv->scratch, sv->list2, kServeIdleMs, kServeLifeMs,
+        DevIndex X;
+        if (!R.index_for(b->valid, X)) return false;
+        std::memcpy(sv->launch_valid, b->valid, sizeof(sv->launch_valid));
+        sv->launched = HIP_CHECK(launch_serve(X, P, sv->d, sv->scratch, sv->list2, kServeIdleMs, kServeLifeMs,
                                               sv->stream));
         return sv->launched;
     };
@@ -1985,20 +2002,8 @@ NGS_API int ngsSearchDeviceAsync(uint32_t handle, const uint8_t* dQueryBytes, co
             L->batches.fetch_sub(1, std::memory_order_acq_rel);
             return -4;
         }
-        // NGS_DEFER_HEAVY (experiment): 1 = the heavy chain waits for the main launch (launch_fast),
-        // -1 = when another batch is in flight. Measured on C3 at depth 2 in one box: 35.5-35.7 Mq/s
-        // either way against 36.5-36.6 with the chains side by side (the default, 0)
-        static const int defer_mode = [] {
-            const char* e = std::getenv("NGS_DEFER_HEAVY");
-            return e ? std::atoi(e) : 0;
-        }();
-        bool defer = defer_mode == 1;
-        if (defer_mode < 0) {
-            std::lock_guard<std::mutex> g(L->pend_mu);
-            defer = !L->pending.empty();
-        }
         pd.rc = queue_search(*L, *Rp, c, dQueryBytes, dQueryOffsets, nQueries, qbytes, threshold, Lm, outStride,
-                             dCounts, dKeys, dScores, c.stream, pd.P, false, defer);
+                             dCounts, dKeys, dScores, c.stream, pd.P, false);
     }
     std::lock_guard<std::mutex> g(L->pend_mu);
     *ticket = L->next_ticket++;

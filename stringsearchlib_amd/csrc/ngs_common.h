@@ -206,22 +206,12 @@ constexpr uint32_t kBackPieceMin = 131072;        // ... of at least this many r
 #define NGS_NO_SKIP_EMPTY 0  // 1: launch the main k_emit and hand-over tier 1b even when all queries are heavy
 #endif
 constexpr uint32_t kOneStreamBatch = 16384;     // batches up to this size run on one stream per call
-#ifndef NGS_HEAVY_FUSE
-#define NGS_HEAVY_FUSE 0  // measured slower: C2 18.1-18.7 against 32.9-34.9 Mq/s, C3 30.7-32.1 against 34.6-35.5 (one box)
-#endif
-constexpr bool kHeavyFuse = NGS_HEAVY_FUSE != 0;  // the heavy list's lean launch and k_emit as one kernel (k_heavy)
-#ifndef NGS_HEAVY_FUSE_WPS
-#define NGS_HEAVY_FUSE_WPS 5
-#endif
-constexpr int kHeavyFuseWavesPerSimd = NGS_HEAVY_FUSE_WPS;  // ... its occupancy target (the emit needs ~97 VGPRs)
-constexpr uint32_t kHeavyWaves = 1;             // ... on this many waves per query
-constexpr uint32_t kHeavyGrid = 4096;           // ... by this many workgroups (grid-stride)
-constexpr bool kSidePriority = false;           // ... on a highest-priority stream
+constexpr uint32_t kHeavyGrid = 4096;           // the heavy list's launches: this many workgroups (grid-stride)
+constexpr bool kSidePriority = false;           // side streams at the highest priority (NGS_SIDE_PRIO; measured no faster)
 #ifndef NGS_SHRINK2
 #define NGS_SHRINK2 0
 #endif
 constexpr uint32_t kShrink2 = NGS_SHRINK2;      // cmin 2 sketch parts: cap and target >> this
-constexpr uint32_t kDefaultWaves = 0;           // tier 1: 0 = lean kernel + full kernel on its hand-overs; 1, 2, 4 = full kernel only
 constexpr int kWaveTarget = kWaveCap * 5 / 8;   // postings per exact part the bucket grouping aims at
 #ifndef NGS_TGT8
 #define NGS_TGT8 5
@@ -285,11 +275,16 @@ struct DevIndex {  // passed by value to kernels; all pointers are device pointe
     // the key ranks of its postings in ascending order (the offsets of post); null otherwise.
     const uint32_t* rank_post;
     uint32_t w_uniform;         // ... the weight's bits
-    // key -> its terms (the pairs transposed), for keys with several pairs: whether a long term
-    // promotes a key whose short pair scores above 100 (key_promoted_long); null when every key
-    // has one pair (keys_unique)
+    // key -> its terms (the pairs transposed), for keys with several pairs; null when every key
+    // has one pair (keys_unique). kt_flag (per validChar set, k_key_flags): 1 = a long term
+    // promotes the key when it is queried, after its short pairs (pair_enc drops those above 100)
     const uint32_t* kt_off;     // [n_keys + 1] -> kt_term
     const uint32_t* kt_term;
+    const uint8_t* kt_flag;
+};
+
+struct ValidSet {  // a 256-bit validChar set by value (kernel argument)
+    uint32_t w[8];
 };
 
 constexpr uint64_t kGramEmpty = ~0ull;
@@ -301,9 +296,7 @@ struct SearchParams {
     uint32_t n_queries;
     uint32_t valid[8];   // 256-bit validChar mask (h:307-313 / setValidChar)
     uint32_t dbg;        // ablation switches for performance experiments (NGS_DEBUG); 0 in production
-    uint32_t waves;      // tier 1: 0 = lean 1a + full 1b, or 1, 2, 4 waves per query in the full kernel only (NGS_WAVES)
-    uint32_t heavy_waves;  // waves per query of tier 1b on the heavy list (kHeavyWaves; NGS_HEAVY_WAVES)
-    uint32_t heavy_grid;   // workgroups of tier 1b on the heavy list (kHeavyGrid; NGS_HEAVY_GRID)
+    uint32_t waves;      // tier 1: 0 = lean 1a + full 1b (batches), 1 = the full kernel alone (latency path)
     uint32_t lean_all;     // tier 1a also takes heavy queries (its launch over the heavy list)
     // deferred calcScore (kDeferEmit): per query the survivor count (kNoEmit = none) and
     // kEmitCap survivor slots, terms and hit counts

@@ -28,8 +28,8 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
                        uint32_t* count2, uint32_t* fb, uint32_t* fbc, uint32_t* fb2, uint32_t* fbc2,
                        const uint32_t* heavy, const uint32_t* hcount, const uint32_t* full,
                        const uint32_t* fcount, uint32_t* glist, uint32_t* gcount, DevStats* stats, hipStream_t s,
-                       hipStream_t side, hipStream_t side2, hipEvent_t fork, hipEvent_t join, hipEvent_t join2,
-                       hipEvent_t lists_ev, bool defer_heavy = false, bool all_heavy = false);
+                       hipStream_t side, hipStream_t side2, hipEvent_t join, hipEvent_t join2,
+                       hipEvent_t lists_ev, bool all_heavy = false);
 
 // The low-latency server (ngsServe): one persistent one-wave workgroup on `s` serving requests
 // from `blk` (coherent pinned host memory, device view) until blk->stop, or until no request
@@ -53,6 +53,9 @@ hipError_t launch_pack_pairs(const uint32_t* n, const uint32_t* k, const float* 
 
 // Wildcard answer (nGramSearch.hpp:356-369): keys sorted by (weight desc, rank asc).
 hipError_t build_wildcard(const float* d_w, uint32_t n_keys, uint32_t* d_keys, float* d_scores, hipStream_t s);
+
+// DevIndex.kt_flag of an index with kt_off / kt_term under one validChar set (k_key_flags)
+hipError_t build_key_flags(const DevIndex& X, const uint32_t valid[8], uint8_t* flags, hipStream_t s);
 
 // hipcub's int item count bounds the rank lists' segmented sort
 constexpr uint64_t kRankMaxPostings = 0x7FFFFFFFull;

@@ -347,48 +347,20 @@ __device__ __forceinline__ uint32_t gram_at(const DevIndex& X, QF qf, uint32_t i
     }
 }
 
-// calcScore merges a query's short scores first and its long scores after them
-// (nGramSearch.hpp:393-394), and a promotion (hpp:335) overwrites what the key had so far: a short
-// pair scoring above 100 of a key that a long term promotes never shows. That long term holds
-// every gram of the query (count n: s = 1 > 0.999) and passes the threshold. Only a key with
-// several pairs can have both (DevIndex.kt_off is null when every key has one).
-__device__ bool key_promoted_long(const DevIndex& X, uint32_t k, const void* q, uint32_t qcs, uint32_t m, float thr) {
-    const uint32_t g = X.gsz, cs = X.csize;
-    if (m < g || 1.0f < thr) return false;  // hpp:281, :315
-    auto qf = [&](uint32_t i) { return char_at(static_cast<const uint8_t*>(q), i, qcs); };
-    for (uint32_t p = X.kt_off[k]; p < X.kt_off[k + 1]; ++p) {
-        const uint32_t t = X.kt_term[p];
-        if (t < X.n_short) continue;
-        const uint64_t a = X.term_off[t], len = X.term_off[t + 1] - a;
-        bool all = true;
-        for (uint32_t i = 0; all && i + g <= m; ++i) {
-            if (gram_at(X, qf, i) == UINT32_MAX) return false;  // a gram with no list is never counted
-            bool hit = false;
-            for (uint64_t j = 0; !hit && j + g <= len; ++j) {
-                bool eq = true;
-                for (uint32_t c = 0; eq && c < g; ++c) eq = char_at(X.term_bytes, a + j + c, cs) == qf(i + c);
-                hit = eq;
-            }
-            all = hit;
-        }
-        if (all) return true;
-    }
-    return false;
-}
-
 // calcScore's per-pair value (nGramSearch.hpp:326-335) as an order-preserving encoding: the
 // score max(w*s, +0), or 100 for an exact match (kPromoted, an ordinary score in ScoreComparer).
 // shortg: the pair's score came from the short search (searchShort, hpp:262-270). 0: the pair
-// never shows (a long promotion of its key overwrites it, key_promoted_long).
+// never shows: calcScore merges the short scores before the long ones (hpp:393-394) and a
+// promotion overwrites what the key had, so a short pair above 100 of a key that a long term
+// promotes is lost (DevIndex.kt_flag: the key has such a long term; the query is the key).
 __device__ __forceinline__ uint32_t pair_enc(uint2 kw, float s, bool promo_possible, bool shortg,
                                              const DevIndex& X, const void* q, uint32_t qcs, uint32_t m,
-                                             const uint32_t* valid, float thr) {
+                                             const uint32_t* valid) {
     const float sc = __uint_as_float(kw.y) * s;
     const uint32_t enc = sc > 0.0f ? __float_as_uint(sc) + 1u : 1u;  // std::max(w*s, 0.0f) (entry default)
-    if (promo_possible && key_equals_query(X, kw.x, q, qcs, m, valid)) return kPromoted;
-    if (shortg && enc > kPromoted && X.kt_off && key_equals_query(X, kw.x, q, qcs, m, valid) &&
-        key_promoted_long(X, kw.x, q, qcs, m, thr))
-        return 0u;
+    // one key test for both (the key is the query): promoted, or an overwritten short pair
+    const bool test = promo_possible || (shortg && enc > kPromoted && X.kt_flag && X.kt_flag[kw.x]);
+    if (test && key_equals_query(X, kw.x, q, qcs, m, valid)) return promo_possible ? kPromoted : 0u;
     return enc;
 }
 
@@ -484,10 +456,10 @@ struct EmitState {
 
 // Appends the pending pairs; false = buffer full (the pair is retried after a flush).
 __device__ __forceinline__ bool emit_pending(EmitState& st, FastSmem& S, const DevIndex& X, uint64_t tau,
-                                             uint32_t m, const uint32_t* valid, float thr) {
+                                             uint32_t m, const uint32_t* valid) {
     while (st.p < st.pe) {
         const uint2 kw = X.tk[st.p];
-        const uint32_t enc = pair_enc(kw, st.s, st.promo, st.shortg, X, S.q, 4u, m, valid, thr);
+        const uint32_t enc = pair_enc(kw, st.s, st.promo, st.shortg, X, S.q, 4u, m, valid);
         const uint64_t rec = ((uint64_t)(~enc) << 32) | kw.x;
         if (enc && rec < tau) {
             const uint32_t idx = atomicAdd(&S.cand_n, 1u);
@@ -510,7 +482,7 @@ __device__ void produce(FastSmem& S, const DevIndex& X, const SearchParams& P, u
         bool full = false;
         const uint64_t tau = S.tau;
         while (!full) {
-            if (st.p < st.pe && !emit_pending(st, S, X, tau, m, P.valid, P.thr)) { full = true; break; }
+            if (st.p < st.pe && !emit_pending(st, S, X, tau, m, P.valid)) { full = true; break; }
             if (done) break;
             const int r = next(st);
             if (r == 0) done = true;
@@ -1242,7 +1214,7 @@ __device__ void wave_emit(SM& S, const DevIndex& X, const SearchParams& P, uint3
             uint64_t rec = kNoCand;
             if (p < pe) {
                 const uint2 kw = X.tk[p++];
-                const uint32_t enc = pair_enc(kw, s, promo, (code & 0x80u) != 0, X, S.q, 4u, m, P.valid, P.thr);
+                const uint32_t enc = pair_enc(kw, s, promo, (code & 0x80u) != 0, X, S.q, 4u, m, P.valid);
                 if (enc) rec = ((uint64_t)(~enc) << 32) | kw.x;
             }
             if (cand_n + 64 > (uint32_t)kWaveCand) wave_trim(S, cand_n, tau, L, X.keys_unique != 0);
@@ -3434,7 +3406,7 @@ __device__ __forceinline__ void emit_query(EmitSmem& S, const uint32_t q, const 
             if (i < sn) term_pairs(X, T[0], s, promo, tau, p, pe);  // p == T[0] unless pruned
             uint64_t rec = kNoCand;
             // (tier 1a leaves long survivors only: it hands every short-search query over)
-            if (p < pe) rec = ((uint64_t)(~pair_enc(K[0], s, promo, false, X, S.q, 4u, m, P.valid, P.thr)) << 32) | K[0].x;
+            if (p < pe) rec = ((uint64_t)(~pair_enc(K[0], s, promo, false, X, S.q, 4u, m, P.valid)) << 32) | K[0].x;
             if (cand_n + 64 > (uint32_t)kWaveCand) wave_trim<RADIX>(S, cand_n, tau, L, X.keys_unique != 0);
             const bool want = rec < tau;
             const unsigned long long bw = __ballot(want);
@@ -3477,7 +3449,7 @@ __device__ __forceinline__ void emit_query(EmitSmem& S, const uint32_t q, const 
             uint64_t rec = kNoCand;
             if (p < pe) {
                 const uint2 kw = X.tk[p++];
-                const uint32_t enc = pair_enc(kw, s, promo, false, X, S.q, 4u, m, P.valid, P.thr);
+                const uint32_t enc = pair_enc(kw, s, promo, false, X, S.q, 4u, m, P.valid);
                 rec = ((uint64_t)(~enc) << 32) | kw.x;
             }
             if (cand_n + 64 > (uint32_t)kWaveCand) wave_trim<RADIX>(S, cand_n, tau, L, X.keys_unique != 0);
@@ -3534,44 +3506,6 @@ __global__ __launch_bounds__(64 * kEmitWaves) void k_emit(DevIndex X, SearchPara
     }
 }
 
-// The heavy list's launch with its k_emit fused (kHeavyFuse): each wave scores its query's survivors
-// (emit_query) right after counting them (lean_query), over the same LDS (the sketch table is dead by
-// then), so a query's calcScore and top-L overlap the other queries' counting instead of waiting for
-// the whole launch, and one launch and its drain leave the heavy chain (C2: every query).
-union HeavySmem {
-    WaveSmem<1, true> w;
-    EmitSmem e;
-};
-
-template <bool ONES>
-__global__ __launch_bounds__(64, kHeavyFuseWavesPerSimd) void k_heavy(DevIndex X, SearchParams P,
-                                                                     const uint8_t* __restrict__ qnorm,
-                                                                     const uint64_t* __restrict__ qoff,
-                                                                     const uint32_t* __restrict__ qm,
-                                                                     uint32_t* __restrict__ out_n,
-                                                                     uint32_t* __restrict__ out_k,
-                                                                     float* __restrict__ out_s,
-                                                                     uint32_t* __restrict__ list2,
-                                                                     uint32_t* __restrict__ count2,
-                                                                     DevStats* __restrict__ stats,
-                                                                     uint32_t* __restrict__ fb, uint32_t* __restrict__ fbc,
-                                                                     const uint32_t* __restrict__ qlist,
-                                                                     const uint32_t* __restrict__ qcount) {
-    __shared__ HeavySmem U;
-    const uint32_t cnt = *qcount;  // the heavy list, grid-stride
-    for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
-        const uint32_t q = qlist[i];
-        if constexpr (NGS_LEAN_GROUPS == 2)
-            lean_query_g<ONES>(U.w, q, X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats, fb, fbc);
-        else
-            lean_query<ONES>(U.w, q, X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats, fb, fbc);
-        wave_sync();
-        __threadfence();  // the survivor slots and the count written above are read back below
-        emit_query<true, NGS_EMIT_DEPTH>(U.e, q, true, X, P, qnorm, qoff, qm, out_n, out_k, out_s, stats);
-        wave_sync();
-    }
-}
-
 // Joins the slices of sliced tier 1b (SearchParams.prec / pcnt): per query of the list, the
 // slices' top-L records through the running top-L (key-max dedup, tau pruning), then results.
 __global__ __launch_bounds__(64) void k_merge(DevIndex X, SearchParams P, const uint32_t* __restrict__ qlist,
@@ -3621,7 +3555,7 @@ __device__ __forceinline__ void emit_global(const DevIndex& X, uint32_t t, float
     const bool promo = (double)s > 0.999;
     for (uint32_t p = X.tk_off[t]; p < X.tk_off[t + 1]; ++p) {
         const uint2 kw = X.tk[p];
-        const uint32_t enc = pair_enc(kw, s, promo, shortg, X, q, X.csize, m, P.valid, P.thr);
+        const uint32_t enc = pair_enc(kw, s, promo, shortg, X, q, X.csize, m, P.valid);
         if (enc) atomicMax(&kenc[kw.x], enc);
     }
 }
@@ -3706,6 +3640,53 @@ __global__ __launch_bounds__(256) void k_gen_write(const uint64_t* __restrict__ 
     if (blockIdx.x == 0 && threadIdx.x == 0) out_n[q] = cnt;
 }
 
+// DevIndex.kt_flag under one validChar set: key k (several pairs) can be promoted by a long term
+// and has a short-search pair that the promotion then overwrites (pair_enc). The query that promotes
+// k is k's own normalised text nk (escapeBlank + trim, hpp:330-334, upper case already: the query
+// is upper-cased), so the flag is a property of the key: nk has at least g characters, no lower
+// case, every g-gram of nk has a list (narrow: characters < 0x80) and some long term of k holds
+// them all (searchLong counts n of n: s = 1, which passes every threshold that the short pair
+// passed); and k has a short term, or nk is short enough (m <= g) for the full-library scan to
+// score long terms too.
+__global__ void k_key_flags(DevIndex X, ValidSet V, uint8_t* __restrict__ flags) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= X.n_keys) return;
+    uint8_t f = 0;
+    const uint32_t p0 = X.kt_off[k], p1 = X.kt_off[k + 1], g = X.gsz, cs = X.csize;
+    if (p1 - p0 >= 2) {
+        uint64_t a = X.key_off[k], e = X.key_off[k + 1] - 1;  // drop the NUL
+        while (a < e && dev_space(esc_cs(V.w, char_at(X.key_bytes, a, cs), cs))) ++a;
+        while (e > a && dev_space(esc_cs(V.w, char_at(X.key_bytes, e - 1, cs), cs))) --e;
+        const uint64_t m = e - a;
+        bool ok = m >= g;
+        bool has_short = m <= X.full_scan_len;
+        for (uint32_t p = p0; p < p1; ++p) has_short |= X.kt_term[p] < X.n_short;
+        ok = ok && has_short;
+        for (uint64_t i = 0; ok && i < m; ++i) {
+            const uint32_t c = esc_cs(V.w, char_at(X.key_bytes, a + i, cs), cs);
+            ok = !(c >= 'a' && c <= 'z') && (X.gram_mode ? c <= 0x1FFFFFu : c < 0x80u);
+        }
+        for (uint32_t p = p0; ok && !f && p < p1; ++p) {
+            const uint32_t t = X.kt_term[p];
+            if (t < X.n_short) continue;
+            const uint64_t ta = X.term_off[t], tl = X.term_off[t + 1] - ta;
+            bool all = true;
+            for (uint64_t i = 0; all && i + g <= m; ++i) {
+                bool hit = false;
+                for (uint64_t j = 0; !hit && j + g <= tl; ++j) {
+                    bool eq = true;
+                    for (uint32_t c = 0; eq && c < g; ++c)
+                        eq = char_at(X.term_bytes, ta + j + c, cs) == esc_cs(V.w, char_at(X.key_bytes, a + i + c, cs), cs);
+                    hit = eq;
+                }
+                all = hit;
+            }
+            f = all ? 1 : 0;
+        }
+    }
+    flags[k] = f;
+}
+
 __global__ void k_wild_records(const float* __restrict__ w, uint32_t n, uint64_t* __restrict__ rec) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n) return;
@@ -3756,6 +3737,14 @@ hipError_t build_rank_post(const uint64_t* gram_off, uint32_t n_seg, const uint3
     hipFree(a);
     hipFree(temp);
     return e;
+}
+
+hipError_t build_key_flags(const DevIndex& X, const uint32_t valid[8], uint8_t* flags, hipStream_t s) {
+    if (!X.n_keys) return hipSuccess;
+    ValidSet V;
+    for (int i = 0; i < 8; ++i) V.w[i] = valid[i];
+    hipLaunchKernelGGL(k_key_flags, dim3((X.n_keys + 255) / 256), dim3(256), 0, s, X, V, flags);
+    return hipGetLastError();
 }
 
 hipError_t build_wildcard(const float* d_w, uint32_t n_keys, uint32_t* d_keys, float* d_scores, hipStream_t s) {
@@ -3884,11 +3873,11 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
                        uint32_t* count2, uint32_t* fb, uint32_t* fbc, uint32_t* fb2, uint32_t* fbc2,
                        const uint32_t* heavy, const uint32_t* hcount, const uint32_t* full,
                        const uint32_t* fcount, uint32_t* glist, uint32_t* gcount, DevStats* stats, hipStream_t s,
-                       hipStream_t side, hipStream_t side2, hipEvent_t fork, hipEvent_t join, hipEvent_t join2,
-                       hipEvent_t lists_ev, bool defer_heavy, bool all_heavy) {
+                       hipStream_t side, hipStream_t side2, hipEvent_t join, hipEvent_t join2,
+                       hipEvent_t lists_ev, bool all_heavy) {
     if (!P.n_queries) return hipSuccess;
     hipError_t e = hipSuccess;
-    switch (P.waves) {  // waves per query (SearchParams.waves, NGS_WAVES; 0 = tier 1a + 1b)
+    switch (P.waves) {  // SearchParams.waves: 0 = tier 1a + 1b (batches), 1 = tier 1b alone (latency path)
         case 0: {
             // beside tier 1a: the heavy list through the lean kernel, k_emit and tier 1b on its
             // hand-overs (side), and the full list through tier 1b (side2)
@@ -3898,7 +3887,7 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
             // path-count line (zeroed per call with it)
             const uint32_t g1s = std::min<uint32_t>(P.n_queries * std::max<uint32_t>(P.nslices, 1u),
                                                     std::min<uint32_t>(persistent_slots(kWaveWavesPerSimd), kTier1bGrid));
-            const uint32_t gh = std::min<uint32_t>(P.n_queries, P.heavy_grid ? P.heavy_grid : 4096);
+            const uint32_t gh = std::min<uint32_t>(P.n_queries, kHeavyGrid);
             const uint32_t gfull = std::min<uint32_t>(P.n_queries, std::min<uint32_t>(persistent_slots(kWaveWavesPerSimd), kTier1bGrid));
             SearchParams PM = P, PHO = P;  // the main and the heavy hand-over launches
             PM.qhead = gcount + 8;
@@ -3917,20 +3906,13 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
             // then the heavy list's chain on side, which is already ordered after k_prep with k_lists
             // queued on it (launch_prep): queued second, so that it starts soon after k_lists (the
             // host queues ~15 operations per call; at C2 this launch carries every query)
-            // defer_heavy: the heavy list's chain starts when the main launch has finished (a batch
-            // queued behind another one in flight: its main launch then has the GPU to itself, and the
-            // heavy chain runs beside the next batch's)
-            if (defer_heavy && kMainFirst && side != s &&
-                ((e = hipEventRecord(fork, s)) != hipSuccess || (e = hipStreamWaitEvent(side, fork, 0)) != hipSuccess))
-                return e;
+            // (the heavy chain deferred until the main launch ends measured slower at C3, 35.5-35.7
+            // against 36.5-36.6 Mq/s; fused with its k_emit into one kernel slower too, C2 18 against
+            // 33-35: profiles/r04_s2_ab_defer_heavy.txt, r04_s2_ab_heavy_fuse.txt)
             if (kHeavyLean) {
                 SearchParams PH = P;
                 PH.lean_all = 1;
-                if (kHeavyFuse) {
-                    hipLaunchKernelGGL((k_heavy<kLeanOnes>), dim3(gh), dim3(64), 0, side, X, PH, qnorm, off, qm, out_n,
-                                       out_k, out_s, list2, count2, stats, fb2, fbc2, heavy, hcount);
-                    dbg_check(side, "k_heavy (heavy list)");
-                } else {
+                {
                     // part_ones is compiled in only where a lean query can have cmin 1: without rank lists,
                     // at a threshold the shortest lean query (n_min grams) passes with one hit
                     const uint32_t n_min = (X.n_short ? X.short_query_len : X.full_scan_len + 1) - X.gsz + 1;
@@ -3959,15 +3941,7 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
             if ((e = hipEventRecord(join, side)) != hipSuccess) return e;
             // side2 waits for the lists
             if ((e = hipStreamWaitEvent(side2, lists_ev, 0)) != hipSuccess) return e;
-            if (P.heavy_waves == 4) {
-                hipLaunchKernelGGL(k_wave<4>, dim3(gh), dim3(256), 0, side2, X, P, qnorm, off, qm, out_n, out_k,
-                                   out_s, list2, count2, stats, full, fcount);
-                dbg_check(side2, "k_wave<4> (full list)");
-            } else if (P.heavy_waves == 2) {
-                hipLaunchKernelGGL(k_wave<2>, dim3(gh), dim3(128), 0, side2, X, P, qnorm, off, qm, out_n, out_k,
-                                   out_s, list2, count2, stats, full, fcount);
-                dbg_check(side2, "k_wave<2> (full list)");
-            } else {
+            {
                 // unsliced: its cmin-1 parts are all counted exactly, and four slices of a C2 query
                 // measured 17 % slower than one wave (the hand-over lists below gain from slicing)
                 SearchParams PF = P;
@@ -4014,16 +3988,8 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
                 dbg_check(s, "k_merge");
             }
             break;
-        case 2:
-            hipLaunchKernelGGL(k_wave<2>, dim3(P.n_queries), dim3(128), 0, s, X, P, qnorm, off, qm, out_n, out_k,
-                               out_s, list2, count2, stats, (const uint32_t*)nullptr, (const uint32_t*)nullptr);
-            dbg_check(s, "k_wave");
-            break;
         default:
-            hipLaunchKernelGGL(k_wave<4>, dim3(P.n_queries), dim3(256), 0, s, X, P, qnorm, off, qm, out_n, out_k,
-                               out_s, list2, count2, stats, (const uint32_t*)nullptr, (const uint32_t*)nullptr);
-            dbg_check(s, "k_wave");
-            break;
+            return hipErrorInvalidValue;
     }
     const uint32_t grid2 = std::min<uint32_t>(P.n_queries, 1024);
     hipLaunchKernelGGL(k_fast, dim3(grid2), dim3(kFastThreads), 0, s, X, P, qnorm, off, qm, out_n, out_k, out_s,
