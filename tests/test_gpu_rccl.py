@@ -54,16 +54,25 @@ def test_rccl_gather_of_device_results_one_rank():
             assert got == w, f"q#{i}"
             o += n
         assert o == keys.numel()
-        # the packed form of bench.py's step loop: ngsPackResults on the device, then the gather
-        # of the buffer's prefix up to the largest record count
+        # the packed form of bench.py's step loop: ngsPackResults on the device, then the gather of
+        # the buffer's prefix up to a record capacity every rank holds (shard.GatherCap). Too small a
+        # capacity first: the retired gather reads the all-reduced total (copied to pinned memory on a
+        # side stream), gathers the buffer again whole and grows the capacity; then it fits
         pg = shard.PackedGather(len(qs), stride, pad_b=len(qs) + 5, device=dev)
-        gi.search_device(raw.data_ptr(), off.data_ptr(), len(qs), 0.3, 16, stride, pg.counts.data_ptr(),
-                         pg.keys.data_ptr(), pg.scores.data_ptr(), stream)
-        pend = shard.gather_packed(pg.pack(ssl._native.lib().ngsPackResults, stream), async_op=True)
-        assert pend.words == 2 + len(qs) + 5 + 2 * o
-        (pc, pk, ps), = pend.wait()
-        assert torch.equal(pc, counts) and torch.equal(pk, keys) and torch.equal(ps.view(torch.int32),
-                                                                              scores.view(torch.int32))
+        cap = shard.GatherCap(len(qs) + 5, stride, initial=8)
+        for rnd in range(2):
+            gi.search_device(raw.data_ptr(), off.data_ptr(), len(qs), 0.3, 16, stride, pg.counts.data_ptr(),
+                             pg.keys.data_ptr(), pg.scores.data_ptr(), stream)
+            pend = shard.gather_packed(pg.pack(ssl._native.lib().ngsPackResults, stream), async_op=True, cap=cap)
+            sent = pend.words
+            (pc, pk, ps), = pend.wait()
+            assert torch.equal(pc, counts) and torch.equal(pk, keys) and torch.equal(ps.view(torch.int32),
+                                                                                  scores.view(torch.int32))
+            if rnd == 0:
+                assert sent == 2 + len(qs) + 5 + 2 * 8 and pend.regathered and pend.words == 2 + len(qs) + 5 + 2 * o
+                assert cap.regathers == 1 and cap.total >= o
+            else:
+                assert not pend.regathered and cap.regathers == 1 and sent == 2 + len(qs) + 5 + 2 * cap.total
         gi.dispose()
     finally:
         dist.destroy_process_group()
