@@ -16,6 +16,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <limits>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <shared_mutex>
@@ -808,8 +809,8 @@ bool upload(Library& L, const std::vector<int>& devs) {
 // to tier 1b (C4 420 -> 452 ms, C5 20.3 -> 21.7 ms per batch, profiles/r03_s4_ab_ecap.txt).
 uint32_t emit_cap_forced() {  // NGS_ECAP: fixed slots per query, no growth (experiments)
     static const uint32_t forced = [] {
-        const char* e = std::getenv("NGS_ECAP");
-        return e ? std::max<uint32_t>(64, (uint32_t)std::strtoul(e, nullptr, 0)) : 0u;
+        const char* e = std::getenv("NGS_ECAP");  // (at least the rank-list tail, kRankInfo, plus 64)
+        return e ? std::max<uint32_t>(kRankInfo + 64, (uint32_t)std::strtoul(e, nullptr, 0)) : 0u;
     }();
     return forced;
 }
@@ -818,7 +819,7 @@ uint32_t emit_cap(size_t B) {
     if (const uint32_t forced = emit_cap_forced()) return forced;
     static const uint32_t init = [] {  // NGS_ECAP_INIT: the slots a context starts with (tests)
         const char* e = std::getenv("NGS_ECAP_INIT");
-        return e ? std::max<uint32_t>(64, (uint32_t)std::strtoul(e, nullptr, 0)) : 0u;
+        return e ? std::max<uint32_t>(kRankInfo + 64, (uint32_t)std::strtoul(e, nullptr, 0)) : 0u;
     }();
     if (init) return init;
     return B <= kEmitWideBatch ? std::max(kEmitCap, kEmitCapWide) : kEmitCap;
@@ -1633,6 +1634,10 @@ uint32_t one_query(uint32_t handle, const CharT* query, CharT*** results, float*
     if (sizeof(CharT) == 1 && !L->serving.load(std::memory_order_acquire)) maybe_auto_serve(*L);
     if (sizeof(CharT) == 1 && L->serving.load(std::memory_order_acquire) && serve_query(*L, reinterpret_cast<const char*>(query), thr, limit, keys, sc))
         return marshal(*L, keys, sc, results, scores);
+    // the regular path's kernels while a server exists (it was busy with another thread's request,
+    // or cannot take this query): stop it first, since its stream may share a hardware queue with
+    // ours and a resident server would hold our launches until its idle exit
+    BatchGuard bg(L->serving.load(std::memory_order_acquire) ? L : nullptr);
     if (!host_search(*L, &query, 1, thr, limit, counts, keys, sc)) return 0;
     return marshal(*L, keys, sc, results, scores);
 }
@@ -1644,7 +1649,8 @@ uint32_t batch_query(uint32_t handle, const CharT* const* queries, uint32_t nq, 
     std::shared_lock<std::shared_mutex> lk(g_lock);
     Library* L = find_lib(handle);
     if (!L || !L->host.indexed || !queries || !counts || L->host.csize != sizeof(CharT)) return 0;
-    BatchGuard bg(batch_mark(L, nq));
+    // (a small batch takes the latency path and stops a running server like score()'s fallback)
+    BatchGuard bg(L->serving.load(std::memory_order_acquire) ? L : batch_mark(L, nq));
     std::vector<uint32_t> cnt, keys;
     std::vector<float> sc;
     HostTimer ht;
@@ -1968,7 +1974,15 @@ NGS_API int ngsSearchDeviceAsync(uint32_t handle, const uint8_t* dQueryBytes, co
     if (!Rp) return -3;
     hipStream_t s = (hipStream_t)stream;
     BatchGuard bg(L);  // the server stops here; the pending call keeps it stopped until its Wait
-    L->batches.fetch_add(1, std::memory_order_acq_rel);
+    // the batch mark the pending call holds until its Wait; released here on any early return
+    struct Mark {
+        Library* L;
+        bool armed = true;
+        explicit Mark(Library* l) : L(l) { L->batches.fetch_add(1, std::memory_order_acq_rel); }
+        ~Mark() {
+            if (armed) L->batches.fetch_sub(1, std::memory_order_acq_rel);
+        }
+    } mark(L);
     Library::Pending pd;
     pd.R = Rp;
     pd.dq = dQueryBytes;
@@ -1984,22 +1998,17 @@ NGS_API int ngsSearchDeviceAsync(uint32_t handle, const uint8_t* dQueryBytes, co
         if (!HIP_CHECK(hipMemsetAsync(dCounts, 0, sizeof(uint32_t) * nQueries, s))) return -4;
     } else {
         pd.c = Rp->acquire();
-        if (!pd.c) {
-            L->batches.fetch_sub(1, std::memory_order_acq_rel);
-            return -4;
-        }
+        if (!pd.c) return -4;
         Context& c = *pd.c;
         uint64_t qbytes = 0;
         if (!c.qcap && !(HIP_CHECK(hipMemcpyAsync(&qbytes, dQueryOffsets + nQueries, sizeof(uint64_t),
                                                  hipMemcpyDeviceToHost, s)) &&
                          HIP_CHECK(hipStreamSynchronize(s)))) {
             Rp->give_back(std::move(pd.c));
-            L->batches.fetch_sub(1, std::memory_order_acq_rel);
             return -4;
         }
         if (!HIP_CHECK(hipEventRecord(c.in_ev, s)) || !HIP_CHECK(hipStreamWaitEvent(c.stream, c.in_ev, 0))) {
             Rp->give_back(std::move(pd.c));
-            L->batches.fetch_sub(1, std::memory_order_acq_rel);
             return -4;
         }
         pd.rc = queue_search(*L, *Rp, c, dQueryBytes, dQueryOffsets, nQueries, qbytes, threshold, Lm, outStride,
@@ -2008,6 +2017,7 @@ NGS_API int ngsSearchDeviceAsync(uint32_t handle, const uint8_t* dQueryBytes, co
     std::lock_guard<std::mutex> g(L->pend_mu);
     *ticket = L->next_ticket++;
     L->pending.emplace(*ticket, std::move(pd));
+    mark.armed = false;  // ngsSearchDeviceWait releases it
     return 0;
 }
 
@@ -2079,15 +2089,18 @@ NGS_API int ngsServe(uint32_t handle, int enable) {
 NGS_API int ngsPackResults(const uint32_t* dCounts, const uint32_t* dKeys, const float* dScores, uint32_t n,
                            uint32_t stride, uint32_t* dOffsets, uint32_t* dRecords, void* stream) {
     if (!dCounts || !dOffsets || (n && (!dKeys || !dScores || !dRecords || !stride))) return -3;
-    // the scan's scratch, one grow-only buffer per device (calls on one device serialise here)
+    // the scan's scratch: one grow-only buffer per (device, stream), so that calls on different
+    // streams never share one while their scans run; a buffer is replaced only after its stream's
+    // earlier work has finished with it. (The mutex orders the host-side bookkeeping only.)
     static std::mutex mu;
-    static std::unordered_map<int, std::pair<void*, size_t>> temp;
+    static std::map<std::pair<int, hipStream_t>, std::pair<void*, size_t>> temp;
     int dev = 0;
     if (!HIP_CHECK(hipGetDevice(&dev))) return -4;
     std::lock_guard<std::mutex> g(mu);
-    auto& t = temp[dev];
+    auto& t = temp[{dev, (hipStream_t)stream}];
     const size_t need = pack_pairs_temp_bytes(n);
     if (need > t.second) {
+        if (t.first && !HIP_CHECK(hipStreamSynchronize((hipStream_t)stream))) return -4;
         if (t.first) (void)hipFree(t.first);
         t = {nullptr, 0};
         if (!HIP_CHECK(hipMalloc(&t.first, std::max<size_t>(need, 1 << 16)))) return -4;

@@ -1,5 +1,5 @@
-"""Run by test_gpu_slots.py in a process of its own with NGS_ECAP_INIT=64 (read once per process):
-contexts start with 64 survivor slots per query, so a corpus with a few hundred survivors per
+"""Run by test_gpu_slots.py in a process of its own with NGS_ECAP_INIT=256 (read once per process; the least it takes):
+contexts start with 256 survivor slots per query, so a corpus with 259-712 survivors per
 query fills them; the later calls must run with more slots, and every call's answer must equal
 the oracle's. Prints one JSON line."""
 import json

@@ -104,3 +104,52 @@ def test_auto_serve_c1_default_path():
         assert_exact(g2.score(q, 0.3, 100), oi.score(q, 0.3, 100), f"no server q={q!r}")
     assert g2.serve_state() == 0
     g2.dispose()
+
+
+def test_regular_path_beside_a_busy_server_is_not_held():
+    """while one thread keeps the server kernel busy, another thread's calls that take the
+    regular path (a 16-query batch, and score() at limit 0, which the server cannot take) stop the
+    server before launching, so they never wait for its 200 ms idle exit behind a shared hardware
+    queue. Every call is timed and every answer checked."""
+    import threading
+
+    words, _, rng = ssl.synth.gen_corpus(1000, seed=7)
+    qs = ssl.synth.gen_queries(words, 1, 64, rng)
+    gi = ssl.StringIndex(words, 1, None)
+    gi.serve(False)
+    want1 = {q: gi.score(q, 0.3, 100) for q in qs}
+    want0 = {q: gi.score(q, 0.0, 0) for q in qs[:16]}
+    wantb = gi.score_batch(qs[:16], 0.3, 100)
+    gi.serve(True)
+    stop = threading.Event()
+    errors = []
+
+    def busy():
+        i = 0
+        while not stop.is_set():
+            q = qs[i % len(qs)]
+            if gi.score(q, 0.3, 100) != want1[q]:
+                errors.append(f"served q={q!r}")
+            i += 1
+
+    t = threading.Thread(target=busy)
+    t.start()
+    try:
+        time.sleep(0.05)
+        worst = 0.0
+        for r in range(30):
+            t0 = time.perf_counter()
+            got = gi.score_batch(qs[:16], 0.3, 100)
+            worst = max(worst, time.perf_counter() - t0)
+            assert got == wantb, f"batch round {r}"
+            q = qs[r % 16]
+            t0 = time.perf_counter()
+            got = gi.score(q, 0.0, 0)
+            worst = max(worst, time.perf_counter() - t0)
+            assert got == want0[q], f"limit-0 q={q!r}"
+    finally:
+        stop.set()
+        t.join()
+    assert not errors, errors[:5]
+    assert worst < 0.1, f"a regular-path call took {worst * 1e3:.1f} ms beside the busy server"
+    gi.dispose()

@@ -16,15 +16,15 @@ pytestmark = pytest.mark.gpu
 
 
 def test_slots_grow_and_stay_exact():
-    env = dict(os.environ, NGS_ECAP_INIT="64")
+    env = dict(os.environ, NGS_ECAP_INIT="256")
     child = os.path.join(os.path.dirname(os.path.abspath(__file__)), "slots_child.py")
     p = subprocess.run([sys.executable, child], env=env, capture_output=True, text=True, timeout=400)
     assert p.returncode == 0, p.stderr[-3000:]
     r = json.loads(p.stdout.strip().splitlines()[-1])
     assert not r["fails"], "\n".join(r["fails"])
     slots, full = r["slots"], r["slot_full"]
-    assert slots[0] == 64 and full[0] > 0, r  # the first call fills 64 slots and hands those over
-    assert slots[:6] == sorted(slots[:6]) and slots[5] > 64, r  # later calls have more
+    assert slots[0] == 256 and full[0] > 0, r  # the first call fills 256 slots and hands those over
+    assert slots[:6] == sorted(slots[:6]) and slots[5] > 256, r  # later calls have more
     assert full[5] < full[0], r
     assert max(r["bytes"]) <= 16 << 30, r  # the budget holds after a large batch
     calm = r["calm_slots"]
