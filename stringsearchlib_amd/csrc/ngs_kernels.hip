@@ -23,7 +23,7 @@ namespace {
 
 #ifdef NGS_PHASE_STAMPS
 // Diagnostic build only (make prof): block-time per phase of k_fast, in 100 MHz ticks.
-__device__ unsigned long long g_phase[32];
+__device__ unsigned long long g_phase[48];  // [16, 32) the packed lean kernel, [32, 48) lean_query_g
 #define STAMP(i)                                                          \
     if (threadIdx.x == 0) {                                               \
         const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();   \
@@ -2768,6 +2768,10 @@ __device__ __forceinline__ void lean_query_g(WaveSmem<1, true>& S, const uint32_
     }
     const uint32_t n = m - X.gsz + 1;  // grams of the query (hpp:29-36)
     const uint32_t n_long = X.n_terms - X.n_short;
+#ifdef NGS_PHASE_STAMPS
+    unsigned long long wt_ = __builtin_amdgcn_s_memtime();
+    unsigned long long wacc_[16] = {};
+#endif
     // lane c holds the fp32 score of c hits, (float)c / n (hpp:300); the smallest passing count
     const float sc_long = lane <= n ? (float)lane / (float)n : 0.0f;
     const unsigned long long pm = __ballot(lane <= n && lane > 0 && !(sc_long < P.thr));
@@ -2816,6 +2820,7 @@ __device__ __forceinline__ void lean_query_g(WaveSmem<1, true>& S, const uint32_
         grow = lane < ng ? r2 : 0;
     }
     const uint64_t p_total = wave_sum((uint64_t)glen);
+    WSTAMP(0);
     const bool sketch = cmin >= kSketchMinCmin && cmin <= kSketchMax;
     const bool ones = ONES && cmin == 1;  // part_ones (the heavy list's launch only)
     if (p_total && cmin <= n && !sketch && !ones) { bail(); return; }  // exact counting: tier 1b
@@ -2867,6 +2872,7 @@ __device__ __forceinline__ void lean_query_g(WaveSmem<1, true>& S, const uint32_
         const uint32_t wmax = (uint32_t)max64(1, min64(K, kMaxPartSpan / max(span, 1u)));
         const uint32_t w = (uint32_t)max64(1, min64(wmax, (uint64_t)K * (kGroupTarget >> shrink) / p_total));
         const uint32_t skrow = lrow * (K + 1);
+        WSTAMP(1);
         gptr<uint4> post4 = (gptr<uint4>)reinterpret_cast<const uint4*>(X.post);
         asm volatile("" : "+s"(post4));
         const uint32_t a0 = (uint32_t)lbase & 3u;      // list start within its 16-byte chunk
@@ -2976,6 +2982,9 @@ __device__ __forceinline__ void lean_query_g(WaveSmem<1, true>& S, const uint32_
             cur += len;
         };
         // ---- count a part; false: the query goes to tier 1b ----
+#ifdef NGS_PHASE_STAMPS
+        uint32_t last_nc = 0;  // candidates of the last part counted (phase statistics)
+#endif
         auto count = [&](const uint4 (&v)[kDmaRounds], const PartGroups& ps) -> bool {
             if (surv_n + 64 > (uint32_t)kWaveSurv) {
                 if (!spill()) { slot_full(); return false; }
@@ -2991,6 +3000,9 @@ __device__ __forceinline__ void lean_query_g(WaveSmem<1, true>& S, const uint32_
             } else {
                 nc = lean_sketch_g(S, v, ps.R, k0, G, ps.nch, ps.head, ps.len, cmin, X.n_short, X.n_terms, surv_n);
             }
+#ifdef NGS_PHASE_STAMPS
+            last_nc = nc;
+#endif
             return nc <= 64;  // above: a wrapped counter or too many candidates
         };
         // software pipeline in registers: part i+1's loads are in flight while part i is counted
@@ -3005,13 +3017,25 @@ __device__ __forceinline__ void lean_query_g(WaveSmem<1, true>& S, const uint32_
             const PartGroups cs = ps;
             uint32_t nch = 0, len = 0;
             const bool hp = plan(nch, len);
+            WSTAMP(2);
             if (hp) stage(pv, ps, nch, len);
+            WSTAMP(4);
             if (cs.R && !count(cv, cs)) { bail(); return; }  // count part i while part i+1 is in flight
+            WSTAMP(5);
+            WCOUNT(11, cs.R ? 1 : 0);
+            WCOUNT(13, cs.R);
+            WCOUNT(14, cs.R ? last_nc : 0);
+            WCOUNT(15, cs.R && last_nc == 0 ? 1 : 0);
             ps.R = hp ? ps.R : 0u;
             if (!hp) break;
         }
     }
     if (!spill()) { slot_full(); bail(); return; }
+    WSTAMP(6);
+#ifdef NGS_PHASE_STAMPS
+    if (lane == 0)
+        for (int i = 0; i < 16; ++i) atomicAdd(&g_phase[32 + i], wacc_[i]);
+#endif
     if (lane == 0) P.esn[q] = spilled | (P.lean_all ? kEmitHeavy : 0u);
     if (lane == 0 && !(P.dbg & 32u)) {
         DevStats* sl = stats + (q & (kStatSlots - 1));
@@ -3774,14 +3798,14 @@ hipError_t build_wildcard(const float* d_w, uint32_t n_keys, uint32_t* d_keys, f
 
 int phase_stats(unsigned long long* out, int n, bool reset) {
 #ifdef NGS_PHASE_STAMPS
-    unsigned long long h[32];
+    unsigned long long h[48];
     if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_phase), sizeof(h)) != hipSuccess) return -1;
-    for (int i = 0; i < n && i < 32; ++i) out[i] = h[i];
+    for (int i = 0; i < n && i < 48; ++i) out[i] = h[i];
     if (reset) {
-        unsigned long long z[32] = {};
+        unsigned long long z[48] = {};
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof(z)) != hipSuccess) return -1;
     }
-    return 32;
+    return 48;
 #else
     (void)out; (void)n; (void)reset;
     return -1;

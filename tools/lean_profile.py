@@ -28,22 +28,27 @@ def main():
         qs = [q[:qlen] for q in qs]
     arr = (C.c_char_p * B)(*qs)
     counts = (C.c_uint32 * B)()
-    out = (C.c_uint64 * 32)()
+    out = (C.c_uint64 * 48)()
     for it in range(2):
-        L.ngsPhaseStats(out, 32, 1)
+        L.ngsPhaseStats(out, 48, 1)
         res, sc = C.POINTER(C.POINTER(C.c_char))(), C.POINTER(C.c_float)()
         L.scoreBatch(h, arr, B, thr, 100, counts, C.byref(res), C.byref(sc))
         L.release(h, res, sc)
-        L.ngsPhaseStats(out, 32, 1)
-    w = [out[16 + i] for i in range(16)]
-    tot = sum(w[:len(PHASES)])
-    print(f"lean kernel: {tot / B:.0f} cycles per query (wave time)")
-    for i, nm in enumerate(PHASES):
-        print(f"  {nm:12s} {w[i] / B:9.0f} cyc/query  {100 * w[i] / max(tot, 1):5.1f} %")
-    parts = max(1, w[11])
-    print(f"  parts/query {w[11] / B:.1f}  slow-plan iterations/query {w[12] / B:.2f}  rounds/part {w[13] / parts:.2f}"
-          f"  candidates/part {w[14] / parts:.2f}  cold parts {100 * w[15] / parts:.0f} %")
-    print(f"  per part: plan {(w[2] + w[3]) / parts:.0f}  stage {w[4] / parts:.0f}  sketch {w[5] / parts:.0f} cycles")
+        L.ngsPhaseStats(out, 48, 1)
+    st = _native.NgsStats()
+    L.ngsLastStats(h, C.byref(st))
+    # [32, 48): the main launch (lean_query_g, lane groups); [16, 32): the heavy list's (lean_query)
+    for title, base, nq in (("main launch (lean_query_g)", 32, B - st.heavy_queries),
+                            ("heavy list (lean_query)", 16, max(1, st.heavy_queries))):
+        w = [out[base + i] for i in range(16)]
+        tot = sum(w[:len(PHASES)])
+        print(f"{title}: {nq} queries, {tot / nq:.0f} cycles per query (wave time)")
+        for i, nm in enumerate(PHASES):
+            print(f"  {nm:12s} {w[i] / nq:9.0f} cyc/query  {100 * w[i] / max(tot, 1):5.1f} %")
+        parts = max(1, w[11])
+        print(f"  parts/query {w[11] / nq:.1f}  slow-plan iterations/query {w[12] / nq:.2f}  rounds/part "
+              f"{w[13] / parts:.2f}  candidates/part {w[14] / parts:.2f}  cold parts {100 * w[15] / parts:.0f} %")
+        print(f"  per part: plan {(w[2] + w[3]) / parts:.0f}  stage {w[4] / parts:.0f}  sketch {w[5] / parts:.0f} cycles")
 
 
 if __name__ == "__main__":
