@@ -1040,8 +1040,7 @@ int queue_search(Library& L, Replica& R, Context& c, const uint8_t* d_raw, const
     if (!HIP_CHECK(launch_prep(d_raw, d_off, B, P, c.d_norm, c.d_qm, X.csize, X, c.d_heavy, gc + 3, c.d_full,
                                gc + 5, c.d_lslots, c.d_lctr, s, side, c.prep_ev, c.lists_ev)))
         return -4;
-    if (timing) HIP_CHECK(hipEventRecord(c.ev[1], s));
-    if (timing) HIP_CHECK(hipEventRecord(c.ev[2], s));
+    if (timing) HIP_CHECK(hipEventRecord(c.ev[1], s));  // the end of k_prep is the start of the tier-1 phase
     if (!HIP_CHECK(launch_fast(X, P, c.d_norm, d_off, c.d_qm, d_n, d_k, d_s, c.d_list2, gc + 1, c.d_fb, gc + 2,
                                c.d_fb2, gc + 4, c.d_heavy, gc + 3, c.d_full, gc + 5, c.d_glist, gc, sd, s, side,
                                side2, c.join, c.join2, c.lists_ev, all_heavy && !NGS_NO_SKIP_EMPTY)))
@@ -1137,7 +1136,7 @@ int finish_search(Library& L, Replica& R, Context& c, uint32_t B, const SearchPa
         st.main_postings = ds.main_postings;
         st.main_lists = ds.main_lists;
         if (hipEventElapsedTime(&ms, c.ev[0], c.ev[1]) == hipSuccess) st.prep_kernel_ms = ms;
-        if (hipEventElapsedTime(&ms, c.ev[2], c.ev[3]) == hipSuccess) st.fast_kernel_ms = ms;
+        if (hipEventElapsedTime(&ms, c.ev[1], c.ev[3]) == hipSuccess) st.fast_kernel_ms = ms;
         if (ngen && hipEventElapsedTime(&ms, c.ev[4], c.ev[5]) == hipSuccess) st.general_ms = ms;
         std::lock_guard<std::mutex> g(L.stats_mu);
         L.last = st;

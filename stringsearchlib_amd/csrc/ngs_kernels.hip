@@ -3883,11 +3883,14 @@ hipError_t launch_prep(const uint8_t* raw, const uint64_t* off, uint32_t B, cons
     dbg_check(s, "k_prep");
     if (lists) {  // on the side stream: the main tier-1a launch needs only k_prep's output
         hipError_t e;
-        if ((e = hipEventRecord(prep_ev, s)) != hipSuccess || (e = hipStreamWaitEvent(side, prep_ev, 0)) != hipSuccess)
+        // (one-stream calls, side == s: no cross-stream ordering to queue; a C2 step is ~0.1 ms of
+        // GPU time for ~20 host calls, so each one left out counts)
+        if (side != s &&
+            ((e = hipEventRecord(prep_ev, s)) != hipSuccess || (e = hipStreamWaitEvent(side, prep_ev, 0)) != hipSuccess))
             return e;
         hipLaunchKernelGGL(k_lists, dim3(1), dim3(64), 0, side, slots, ctr, cap, heavy, hcount, full, fcount);
         dbg_check(side, "k_lists");
-        if ((e = hipEventRecord(lists_ev, side)) != hipSuccess) return e;
+        if (side != s && (e = hipEventRecord(lists_ev, side)) != hipSuccess) return e;
     }
     return hipGetLastError();
 }
@@ -3962,9 +3965,9 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
                     dbg_check(side, "k_merge (heavy hand-overs)");
                 }
             }
-            if ((e = hipEventRecord(join, side)) != hipSuccess) return e;
-            // side2 waits for the lists
-            if ((e = hipStreamWaitEvent(side2, lists_ev, 0)) != hipSuccess) return e;
+            if (side != s && side2 != side && (e = hipEventRecord(join, side)) != hipSuccess) return e;
+            // side2 waits for the lists (recorded on side in launch_prep when side != s)
+            if (side2 != side && side != s && (e = hipStreamWaitEvent(side2, lists_ev, 0)) != hipSuccess) return e;
             {
                 // unsliced: its cmin-1 parts are all counted exactly, and four slices of a C2 query
                 // measured 17 % slower than one wave (the hand-over lists below gain from slicing)
@@ -3975,7 +3978,7 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
                                    out_s, list2, count2, stats, full, fcount);
                 dbg_check(side2, "k_wave<1> (full list)");
             }
-            if ((e = hipEventRecord(join2, side2)) != hipSuccess) return e;
+            if (side2 != s && (e = hipEventRecord(join2, side2)) != hipSuccess) return e;
             if (!kMainFirst) main_lean();
             // all_heavy (every lean query on the heavy list, e.g. threshold 0): the main launch finishes
             // no query and hands none over (it returns before either for a heavy or full one), so its
@@ -3997,7 +4000,9 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
                                    out_n, out_k, out_s, stats);
                 dbg_check(s, "k_merge (hand-overs)");
             }
-            if ((e = hipStreamWaitEvent(s, join, 0)) != hipSuccess || (e = hipStreamWaitEvent(s, join2, 0)) != hipSuccess)
+            // (join2 is recorded after join when side2 is side: then it alone orders s after both)
+            if ((side != s && side2 != side && (e = hipStreamWaitEvent(s, join, 0)) != hipSuccess) ||
+                (side2 != s && (e = hipStreamWaitEvent(s, join2, 0)) != hipSuccess))
                 return e;
             break;
         }
