@@ -216,11 +216,15 @@ typedef struct {
     uint64_t slot_full_queries; /* handed to tier 1b because their survivor slots were full (the
                                    context's slots grow for later calls) */
     uint64_t survivor_slots;   /* survivor slots per query the call ran with */
-    uint64_t survivor_slot_bytes; /* bytes of survivor slots the call's context held (rows x slots x
-                                     5; at most 16 GiB, and grown slots go back after 16 calls in a
-                                     row that fill none of them) */
+    uint64_t survivor_slot_bytes; /* bytes of survivor slots and arena the call's context held (rows x
+                                     slots x 5 + arena blocks x 1,024 x 5; the slots at most 16 GiB,
+                                     and grown slots go back after 16 calls in a row that fill none) */
     uint64_t main_postings;    /* postings and lists of the queries the main tier-1a launch finished */
     uint64_t main_lists;
+    uint64_t arena_blocks;     /* survivor arena: blocks (1,024 survivors each) the call's context holds
+                                  (queries whose survivors outgrow their slots go on there) */
+    uint64_t arena_used;       /* ... blocks the call took (past arena_blocks: it ran out, those
+                                  queries went to tier 1b, and later calls get a larger arena) */
 } ngs_stats;
 NGS_API int ngsSetTiming(uint32_t handle, int enable);
 /* The last failure of a call on this thread (0: none); clear != 0 resets it. A HIP error code, or

@@ -32,7 +32,8 @@ class NgsStats(C.Structure):
                 ("handover_queries", C.c_uint64), ("tier2_queries", C.c_uint64),
                 ("heavy_queries", C.c_uint64), ("full_queries", C.c_uint64),
                 ("slot_full_queries", C.c_uint64), ("survivor_slots", C.c_uint64),
-                ("survivor_slot_bytes", C.c_uint64), ("main_postings", C.c_uint64), ("main_lists", C.c_uint64)]
+                ("survivor_slot_bytes", C.c_uint64), ("main_postings", C.c_uint64), ("main_lists", C.c_uint64),
+                ("arena_blocks", C.c_uint64), ("arena_used", C.c_uint64)]
 
 
 def build(jobs: int = 4) -> None:

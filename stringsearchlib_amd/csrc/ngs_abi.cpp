@@ -249,6 +249,14 @@ struct Context {
     uint32_t* d_esn = nullptr;     // tier 1a survivor lists for k_emit: count per query,
     uint32_t* d_est = nullptr;     // kEmitCap terms and
     uint8_t* d_esc = nullptr;      // kEmitCap hit counts per query
+    // the survivor arena (SearchParams.at): ablocks blocks of kArenaBlock entries, a chain link per
+    // block and a first block per query (ebcap rows); grown (arena_grow) after a call ran out of it
+    uint32_t* d_eovf = nullptr;
+    uint32_t* d_anext = nullptr;
+    uint32_t* d_at = nullptr;
+    uint8_t* d_ac = nullptr;
+    uint32_t ablocks = 0, arena_grow = 0;
+    size_t eorows = 0;
     uint64_t* d_prec = nullptr;    // sliced tier 1b: top-L records per (query, slice)
     uint32_t* d_pcnt = nullptr;    // ... and their counts
     size_t pcap = 0, pncap = 0;    // records d_prec holds, counts d_pcnt holds
@@ -279,6 +287,7 @@ struct Context {
         hipSetDevice(device);
         for (void* p : {(void*)d_raw, (void*)d_off, (void*)d_norm, (void*)d_qm, (void*)d_glist, (void*)d_list2, (void*)d_fb, (void*)d_fb2, (void*)d_heavy, (void*)d_full, (void*)d_lslots,
                         (void*)d_esn, (void*)d_est, (void*)d_esc, (void*)d_prec, (void*)d_pcnt,
+                        (void*)d_eovf, (void*)d_anext, (void*)d_at, (void*)d_ac,
                         (void*)d_group, (void*)d_stats, (void*)d_sio, (void*)d_out, (void*)d_pos, (void*)d_pk, (void*)d_ps, d_ptemp, (void*)gen.cnt,
                         (void*)gen.kenc, (void*)gen.list, (void*)gen.sorted, (void*)gen.lcount, gen.temp})
             if (p) hipFree(p);
@@ -875,6 +884,32 @@ bool ensure_queries(Context& c, size_t B, size_t bytes) {
     return true;
 }
 
+// The survivor arena of a context (SearchParams.at): kArenaInit blocks of kArenaBlock entries to
+// start with (a C3 query has ~35 survivors, so only outliers ever use it), after a call that ran out
+// four times as many or twice what it asked for (its failed requests undercount the need), within
+// kArenaBudget bytes. A query's first-block word per row of the batch.
+constexpr uint32_t kArenaInit = 1024;                // 1M survivors, 5 MB
+constexpr uint64_t kArenaBudget = 4ull << 30;
+bool ensure_arena(Context& c, size_t B) {
+    const uint32_t want = std::max<uint32_t>({kArenaInit, c.ablocks, c.arena_grow});
+    if (!c.d_eovf || B > c.eorows) {
+        if (c.d_eovf) { hipFree(c.d_eovf); c.d_eovf = nullptr; }
+        const size_t nb = std::max<size_t>(B, 1024);
+        if (!dev_alloc(&c.d_eovf, nb)) return false;
+        c.eorows = nb;
+    }
+    if (!c.d_at || want > c.ablocks) {
+        for (void** p : {(void**)&c.d_anext, (void**)&c.d_at, (void**)&c.d_ac})
+            if (*p) { hipFree(*p); *p = nullptr; }
+        c.ablocks = 0;
+        if (!dev_alloc(&c.d_anext, want) || !dev_alloc(&c.d_at, (size_t)want * kArenaBlock) ||
+            !dev_alloc(&c.d_ac, (size_t)want * kArenaBlock))
+            return false;
+        c.ablocks = want;
+    }
+    return true;
+}
+
 // Sliced tier 1b's partial results: B * slices * limit records. Within kPartBudget bytes, else the
 // call runs tier 1b unsliced (returns the slice count to use).
 uint32_t ensure_parts(Context& c, size_t B, uint32_t limit, uint32_t slices) {
@@ -978,6 +1013,15 @@ int queue_search(Library& L, Replica& R, Context& c, const uint8_t* d_raw, const
     P.est = c.d_est;
     P.esc = c.d_esc;
     P.ecap = c.ecap;
+    if (!small) {  // (the latency path runs tier 1b alone: no tier-1a survivors)
+        if (!ensure_arena(c, B)) return -4;
+        P.eovf = c.d_eovf;
+        P.anext = c.d_anext;
+        P.at = c.d_at;
+        P.ac = c.d_ac;
+        P.ablocks = c.ablocks;
+        P.actr = gc + kArenaCtrWord;
+    }
     static const uint32_t list_slices = [] {  // term-id slices of the hand-over / full lists' tier 1b
         const char* e = std::getenv("NGS_SLICES");
         const uint32_t v = e ? (uint32_t)std::strtoul(e, nullptr, 0) : kSlices;
@@ -1102,7 +1146,16 @@ int finish_search(Library& L, Replica& R, Context& c, uint32_t B, const SearchPa
     // queries that filled their survivor slots ran again in tier 1b: when that is more than 1/64
     // of the batch, this context's later calls get twice the slots (bounded by emit_cap_max);
     // after kCalmCalls calls in a row that filled none of grown slots, half of them go back
-    if (!small) {
+    // the arena's block counter: past its blocks, the arena ran out (those queries went to tier 1b and
+    // count as slot_full): later calls get a larger arena, not more slots per query
+    const uint32_t arena_used = small ? 0u : counts3[kArenaCtrWord];
+    const bool arena_out = !small && P.at && arena_used > P.ablocks;
+    if (arena_out) {
+        const uint64_t want = std::max<uint64_t>(4ull * P.ablocks, 2ull * arena_used);
+        const uint64_t cap = kArenaBudget / ((uint64_t)kArenaBlock * (sizeof(uint32_t) + sizeof(uint8_t)));
+        c.arena_grow = (uint32_t)std::min<uint64_t>(want, cap);
+    }
+    if (!small && !arena_out) {
         if (slot_full * 64 > B) {
             c.calm = 0;
             if (c.ecap < emit_cap_max(B)) c.ecap_grow = std::max(c.ecap_grow, c.ecap * 2);
@@ -1128,7 +1181,10 @@ int finish_search(Library& L, Replica& R, Context& c, uint32_t B, const SearchPa
         st.full_queries = counts3[5];
         st.slot_full_queries = slot_full;
         st.survivor_slots = P.ecap;
-        st.survivor_slot_bytes = (uint64_t)c.ebcap * c.ecap * (sizeof(uint32_t) + sizeof(uint8_t));
+        st.survivor_slot_bytes = ((uint64_t)c.ebcap * c.ecap + (uint64_t)c.ablocks * kArenaBlock) *
+                                 (sizeof(uint32_t) + sizeof(uint8_t));
+        st.arena_blocks = small ? 0u : P.ablocks;
+        st.arena_used = arena_used;
         st.postings = ds.postings;
         st.lists = ds.lists;
         st.results = ds.results;

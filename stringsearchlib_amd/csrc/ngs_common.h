@@ -234,6 +234,12 @@ constexpr uint32_t kRankInfo = 3 * 64;
 // threshold-0 query has thousands of one-hit survivors at C2 (part_ones)
 constexpr uint32_t kEmitCapWide = 4096;
 constexpr uint32_t kEmitCapMax = 32768;              // ... grown up to this many per query
+#ifndef NGS_ARENA
+#define NGS_ARENA 1  // 0 (A/B only): no survivor arena, a query past its slots goes to tier 1b
+#endif
+constexpr uint32_t kArenaBlock = 1024;               // survivor arena block (entries; a multiple of 128)
+constexpr uint32_t kArenaChain = 128;                // blocks one query may chain (k_emit lists them in LDS)
+constexpr uint32_t kArenaCtrWord = 12;               // SearchParams.actr: this word of the path-count line
 constexpr uint64_t kEmitBudget = 16ull << 30;         // ... within this many bytes per context
 constexpr size_t kEmitWideBatch = 262144;             // tier 1a survivors per query spilled to HBM for k_emit
 constexpr uint32_t kWaveMaxGrams = 63;          // counts <= 63: one lane per count value
@@ -316,6 +322,17 @@ struct SearchParams {
     // (ngsSearchDevice does not read the batch's byte count back before launching)
     uint64_t qcap;
     uint32_t* oflow;
+    // batch-wide survivor arena (the main tier-1a launch, lean_query_g): a query whose survivors outgrow
+    // its ecap slots goes on in blocks of kArenaBlock entries taken from *actr (a word of the call's
+    // path-count line, zeroed with it); its first block is eovf[q] - 1 (0: none, reset by k_prep),
+    // a block's successor anext[b] - 1. A counter past ablocks means the arena ran out (the query
+    // went to tier 1b; the host grows the arena for later calls). at == null: no arena.
+    uint32_t* eovf;
+    uint32_t* anext;
+    uint32_t* at;
+    uint8_t* ac;
+    uint32_t* actr;
+    uint32_t ablocks;
     // the latency path: k_prep zeroes these words (the statistics and path counts, which the
     // tier kernels after it accumulate) in place of a memset launch; null otherwise
     uint32_t* zero_stats;

@@ -117,6 +117,7 @@ __global__ __launch_bounds__(64) void k_prep(const uint8_t* __restrict__ raw, co
         nq = qnorm + off[q];
         n = (off[q + 1] - off[q]) / cs;
         if (gl == 0 && P.esn) P.esn[q] = kNoEmit;  // set by tier 1a when it finishes the query (DEFER)
+        if (gl == 0 && P.eovf) P.eovf[q] = 0;        // no arena blocks yet
         over = off[q + 1] > P.qcap;  // the normalised bytes would not fit: the host reruns the call
         if (over) {
             if (gl == 0) atomicOr(P.oflow, 1u);
@@ -2784,6 +2785,7 @@ __device__ __forceinline__ void lean_query_g(WaveSmem<1, true>& S, const uint32_
     if (m < X.short_query_len && X.n_short) { bail(); return; }  // short search: tier 1b
     const uint8_t* qg = qnorm + qoff[q];
     for (uint32_t i = lane; i < m; i += 64) S.q[i] = char_at(qg, i, X.csize);
+    if (lane == 0) S.x_surv_n = 0;  // no arena blocks chained (spill_arena)
     {
         uint4* T4 = reinterpret_cast<uint4*>(S.table);
 #pragma unroll
@@ -2833,9 +2835,54 @@ __device__ __forceinline__ void lean_query_g(WaveSmem<1, true>& S, const uint32_
         ri[64 + lane] = (uint32_t)(gbase >> 32);
         ri[128 + lane] = min(glen, L);
     }
-    // the LDS survivor list to this query's kEmitCap slots in HBM; false if they are full
+    // the LDS survivor list to this query's ecap slots in HBM, and past them to blocks of the batch's
+    // arena (SearchParams.at); false if neither has room
+    // (arena blocks chained so far and the last two of them live in LDS words tier 1a does not use,
+    // not in registers across the part loop: the arena is the rare path)
+    auto spill_arena = [&]() -> bool {  // (rare: survivors past the query's slots)
+        const uint32_t end = spilled + surv_n;
+        const uint32_t k1 = (end - 1u - ecap_q) / kArenaBlock;  // last chained block the spill needs
+        uint32_t a_n = __builtin_amdgcn_readfirstlane(S.x_surv_n), a_last = __builtin_amdgcn_readfirstlane(S.x_cand_n);
+        uint32_t a_prev = __builtin_amdgcn_readfirstlane(S.xcnt);
+        while (a_n <= k1) {
+            if (a_n >= kArenaChain) return false;
+            uint32_t nb = 0;
+            if (lane == 0) nb = atomicAdd(P.actr, 1u);
+            nb = __builtin_amdgcn_readfirstlane(nb);
+            if (nb >= P.ablocks) return false;  // the arena ran out (the counter tells the host)
+            if (lane == 0) {
+                P.anext[nb] = 0;
+                if (a_n == 0) P.eovf[q] = nb + 1u;
+                else P.anext[a_last] = nb + 1u;
+            }
+            a_prev = a_last;
+            a_last = nb;
+            ++a_n;
+        }
+        wave_sync();
+        if (lane == 0) {
+            S.x_surv_n = a_n;
+            S.x_cand_n = a_last;
+            S.xcnt = a_prev;
+        }
+        for (uint32_t i = lane; i < surv_n; i += 64) {
+            const uint32_t p = spilled + i;
+            if (p < ecap_q) {
+                P.est[(size_t)q * P.ecap + p] = S.surv_t[i];
+                P.esc[(size_t)q * P.ecap + p] = S.surv_c[i];
+            } else {
+                const uint32_t ap = p - ecap_q, k = ap / kArenaBlock;
+                const size_t at = (size_t)(k + 1u == a_n ? a_last : a_prev) * kArenaBlock + (ap - k * kArenaBlock);
+                P.at[at] = S.surv_t[i];
+                P.ac[at] = S.surv_c[i];
+            }
+        }
+        spilled = end;
+        surv_n = 0;
+        return true;
+    };
     auto spill = [&]() -> bool {
-        if (spilled + surv_n > ecap_q) return false;
+        if (spilled + surv_n > ecap_q) return NGS_ARENA && P.at && spill_arena();
         uint32_t qs = q, l0 = lane;  // opaque: the slot pointers are made here, not kept (and spilled)
         asm volatile("" : "+s"(qs), "+v"(l0));
         uint32_t* et = P.est + (size_t)qs * P.ecap + spilled;
@@ -3379,6 +3426,11 @@ __device__ __forceinline__ void emit_query(EmitSmem& S, const uint32_t q, const 
     const uint32_t n = m - X.gsz + 1, L = P.limit;
     const float sc_long = lane <= n ? (float)lane / (float)n : 0.0f;  // as wave_query
     const float sc_short = lane <= m ? (float)lane / (float)m : 0.0f;
+    // survivors past the query's slots are in the batch's arena (lean_query_g's spill_arena): the
+    // slots end where tier 1a's did (the rank-list tail is not theirs)
+    const uint32_t ecap_q = P.ecap - (X.rank_post && !(__shfl(sc_long, 1) < P.thr) ? kRankInfo : 0u);
+    const uint32_t sn_all = sn;
+    sn = min(sn, ecap_q);
     uint32_t cand_n = 0;
     uint64_t tau = kNoCand;
     // the query's characters only for an exact-match test (a survivor scoring > 0.999), rare
@@ -3484,6 +3536,50 @@ __device__ __forceinline__ void emit_query(EmitSmem& S, const uint32_t q, const 
         }
         t = t_next;
         code = code_next;
+    }
+    // survivors past the slots (rare: a query that outgrew them): its arena blocks in order, 64 at a
+    // time, without prefetch (lane 0 walks the chain first: a few dependent loads; the block list goes
+    // to rstage, free until emit_rank_prefix)
+    if (NGS_ARENA && sn_all > sn) {
+        const uint32_t na = sn_all - sn;
+        if (lane == 0) {
+            uint32_t bnx = P.eovf[q];
+            for (uint32_t k = 0; k * kArenaBlock < na && k < kArenaChain && bnx; ++k) {
+                S.rstage[k] = bnx - 1u;
+                bnx = P.anext[bnx - 1u];
+            }
+        }
+        wave_sync();
+        for (uint32_t a = 0; a < na; a += 64) {
+            const uint32_t k = a / kArenaBlock, i = a + lane;
+            const size_t off = (size_t)__builtin_amdgcn_readfirstlane(S.rstage[k]) * kArenaBlock + (a - k * kArenaBlock);
+            const bool live = i < na;
+            const uint32_t ta = live ? P.at[off + lane] : 0u, ca = live ? (uint32_t)P.ac[off + lane] : 0u;
+            uint32_t p = 0, pe = 0;
+            const float s_l = __shfl(sc_long, (int)(ca & 63u)), s_s = __shfl(sc_short, (int)(ca & 63u));
+            const float s = (ca & 0x80u) ? s_s : s_l;
+            const bool promo = (double)s > 0.999;  // nGramSearch.hpp:328
+            if (!have_q && __ballot(live && promo)) {
+                const uint8_t* qg = qnorm + qoff[q];
+                for (uint32_t c = lane; c < m; c += 64) S.q[c] = char_at(qg, c, X.csize);
+                wave_sync();
+                have_q = true;
+            }
+            if (live) term_pairs(X, ta, s, promo, tau, p, pe);
+            while (__ballot(p < pe)) {
+                uint64_t rec = kNoCand;
+                if (p < pe) {
+                    const uint2 kw = X.tk[p++];
+                    const uint32_t enc = pair_enc(kw, s, promo, false, X, S.q, 4u, m, P.valid);
+                    rec = ((uint64_t)(~enc) << 32) | kw.x;
+                }
+                if (cand_n + 64 > (uint32_t)kWaveCand) wave_trim<RADIX>(S, cand_n, tau, L, X.keys_unique != 0);
+                const bool want = rec < tau;
+                const unsigned long long bw = __ballot(want);
+                if (want) S.cand()[cand_n + rank_below(bw)] = rec;
+                cand_n += __popcll(bw);
+            }
+        }
     }
     // threshold 0 with rank lists: tier 1a counted this query at cmin 2 (its multi-hit terms, above);
     // its one-hit records come from the first L key ranks of each of its lists

@@ -1,0 +1,32 @@
+"""The batch-wide survivor arena (SearchParams.at): tier 1a's main launch writes a query's survivors
+to its slots and, past them, to blocks of an arena shared by the call, chained per query; k_emit
+reads them back in order (nGramSearch.hpp:310-341 over every survivor). Slots are 256 per query here
+(NGS_ECAP_INIT, read once per process: tests/arena_child.py runs in a child process), so queries of
+a few thousand survivors live mostly in the arena. Checked: answers exact against the oracle on
+every call; the first call runs the arena out (its queries are handed to tier 1b, still exact) and
+the arena grows instead of the slots; later calls fit."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def test_arena_holds_survivors_past_the_slots():
+    env = dict(os.environ, NGS_ECAP_INIT="256")
+    child = os.path.join(os.path.dirname(os.path.abspath(__file__)), "arena_child.py")
+    p = subprocess.run([sys.executable, child], env=env, capture_output=True, text=True, timeout=400)
+    assert p.returncode == 0, p.stderr[-3000:]
+    r = json.loads(p.stdout.strip().splitlines()[-1])
+    assert not r["fails"], "\n".join(r["fails"])
+    s = r["stats"]
+    assert all(x["survivor_slots"] == 256 for x in s[:3]), s  # the slots never grew
+    assert s[0]["heavy_queries"] == 0 and s[0]["fast_queries"] > 0, s  # the main launch's queries
+    assert s[0]["arena_used"] > s[0]["arena_blocks"] and s[0]["slot_full_queries"] > 0, s  # ran out, handed over
+    assert s[1]["arena_blocks"] > s[0]["arena_blocks"], s  # ... and grew
+    assert s[2]["arena_used"] > 0 and s[2]["arena_used"] <= s[2]["arena_blocks"], s
+    assert s[2]["slot_full_queries"] == 0, s
+    assert s[3]["arena_used"] > 0 and s[3]["slot_full_queries"] == 0, s

@@ -2,9 +2,13 @@
 
 C4: 10M rows of UTF-32 strings through indexW with gSize 2 and rowSize 4 (a key and 3 aliases:
 40M words), 2-grams over a 37-symbol alphabet, so the posting lists are dense (~440k postings)
-and the skip table takes 32,768 buckets. Checked: properties on an 8,192-query batch, a seeded
-sample exact against oracle/ngs_oracle_g.c (the gram-size / UTF-32 restatement; parity unpinned
-beyond g = 3, see test_oracle_generic.py), and the batch answer equal to per-query answers.
+and the skip table takes 32,768 buckets. Checked on the full 65,536-query batch, three times (the
+first call grows the survivor arena): every count within the limit, properties on 4,096 decoded
+answers, a seeded sample exact against oracle/ngs_oracle_g.c (the gram-size / UTF-32
+restatement; parity unpinned beyond g = 3, see test_oracle_generic.py), the batch answer equal
+to per-query answers, and the context's survivor memory within 2 GiB: queries whose survivors
+outgrow their 4,096 slots go on in the batch-wide arena instead of growing every query's slots
+(round 4: 32,768 slots per query, 10 GiB).
 
 C5: the per-GPU slice of the 8-GPU config: a 50M-row library (weight NULL) and 131,072 queries
 (2^20 / 8). Checked: properties on every answer, exact self-matches promoted to 100, a seeded
@@ -39,7 +43,9 @@ def _wstr(p):
     return tuple(out)
 
 
-def gpu_batch_w(h, qs, thr, limit):
+def gpu_batch_w(h, qs, thr, limit, decode=None):
+    """scoreBatchW; the answers of the queries in `decode` (all if None) as lists, the others None,
+    and the counts."""
     L = _native.lib()
     n = len(qs)
     bufs, arr = _wide_arr(qs)
@@ -47,13 +53,14 @@ def gpu_batch_w(h, qs, thr, limit):
     res = C.POINTER(U32P)()
     sc = C.POINTER(C.c_float)()
     total = L.scoreBatchW(h, arr, n, thr, limit, counts, C.byref(res), C.byref(sc))
+    want = None if decode is None else set(decode)
     out, o = [], 0
     for i in range(n):
-        out.append([(_wstr(res[o + j]), sc[o + j]) for j in range(counts[i])])
+        out.append([(_wstr(res[o + j]), sc[o + j]) for j in range(counts[i])] if want is None or i in want else None)
         o += counts[i]
     assert o == total
     L.releaseW(h, res, sc)
-    return out
+    return out if decode is None else (out, list(counts))
 
 
 def oracle_batch_w(oh, qs, thr, limit, threads=16):
@@ -81,13 +88,24 @@ def test_c4_full_wide_g2_rowsize4():
     h = bench.build_index(corpus4, False, 0, gram=cfg["gram"])
     L = _native.lib()
     assert L.ngsCharSize(h) == 4 and L.ngsGramSize(h) == 2 and L.getSize(h) > 0
-    raw, offs = corpus4.queries(8192)
+    raw, offs = corpus4.queries(cfg["batch"])
     qs = [tuple(raw[offs[i]:offs[i + 1]]) for i in range(len(offs) - 1)]  # ASCII: one byte per code point
-    got = gpu_batch_w(h, qs, cfg["threshold"], cfg["limit"])
-    for i, g in enumerate(got):
-        check_properties(g, cfg["limit"], f"C4 q#{i}")
     rng = random.Random(4)
     sample = sorted(rng.sample(range(len(qs)), 40))
+    decode = sorted(set(rng.sample(range(len(qs)), 4096)) | set(sample))
+    L.ngsSetTiming(h, 1)
+    st = _native.NgsStats()
+    for call in range(3):
+        got, counts = gpu_batch_w(h, qs, cfg["threshold"], cfg["limit"], decode=decode)
+        L.ngsLastStats(h, C.byref(st))
+        assert max(counts) <= cfg["limit"] and sum(counts) > 0
+        # survivors past the query's slots went on in the arena; no query's slots grew
+        assert st.survivor_slots == 4096 and st.survivor_slot_bytes <= 2 << 30, (st.survivor_slots, st.survivor_slot_bytes)
+        if call == 2:  # the arena held every overflow: no query handed over for its slots
+            assert st.arena_used <= st.arena_blocks and st.slot_full_queries == 0, (st.arena_used, st.arena_blocks)
+    assert st.arena_used > 0  # C4's long tail of survivors (3,589 per query on average) needs it
+    for i in decode:
+        check_properties(got[i], cfg["limit"], f"C4 q#{i}")
     for i in sample[:8]:  # the batch answer is each query's own answer
         assert gpu_batch_w(h, [qs[i]], cfg["threshold"], cfg["limit"])[0] == got[i]
     oh = lib_g().ngog_build(corpus4.wwords, corpus4.n_words, corpus4.row_size, None, cfg["gram"], 1)
