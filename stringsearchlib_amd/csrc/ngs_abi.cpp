@@ -676,6 +676,15 @@ bool upload_replica(Library& L, Replica& R, bool keys_unique, bool first) {
     X.skip = skip;
     X.n_buckets = H.n_buckets;
     X.bucket_span = H.bucket_span;
+    X.skip4 = nullptr;
+    if (NGS_SKIP4 && H.n_buckets >= 8 && H.n_grams) {
+        // tier 1a's part ends for groups of 4k buckets (a quarter of the skip table's bytes)
+        uint32_t* s4 = nullptr;
+        if (!dev_alloc(&s4, (size_t)H.n_grams * (H.n_buckets / 4 + 1))) return false;
+        R.owned.push_back(s4);
+        if (!HIP_CHECK(build_skip4(skip, H.n_grams, H.n_buckets, s4, nullptr))) return false;
+        X.skip4 = s4;
+    }
     X.term_off = term_off;
     X.term_bytes = term_bytes;
     X.tk_off = tk_off;
@@ -811,11 +820,15 @@ bool upload(Library& L, const std::vector<int>& devs) {
 }
 
 // Survivor slots per query of tier 1a (d_est / d_esc, 5 bytes each): the wide cap for batches
-// up to kEmitWideBatch, at every threshold: 1.25 GiB per context at 65,536 queries (2.5 GiB at
-// C5's 131,072; two contexts when two batches are in flight). A query with more survivors than
-// its slots is handed to tier 1b, and large libraries have them at any threshold: sizing the
-// cap by threshold (wide only at thr <= 1/8) handed 26,594 C4 and 7,871 C5 queries per batch
-// to tier 1b (C4 420 -> 452 ms, C5 20.3 -> 21.7 ms per batch, profiles/r03_s4_ab_ecap.txt).
+// up to kEmitWideBatch, at every threshold, halved until the slots fit kEmitWideBytes per context
+// (4,096 up to 52,428 queries, 2,048 at 65,536, 1,024 at C5's 131,072). The main launch's queries
+// with more survivors go on in the batch's survivor arena (ensure_arena), which holds only what
+// they use: C4 (3,960 survivors per query on average, a long tail) takes 1.8 GiB per context this
+// way against 2.2 GiB with 4,096 slots and 10 GiB with round 4's slots grown to 32,768
+// (profiles/r05_s5_c4_arena.txt). Queries of the heavy list's launch have no arena: past their
+// slots they go to tier 1b, and the slots grow when that is frequent (finish_search). Sizing the
+// cap by threshold (wide only at thr <= 1/8) handed 26,594 C4 and 7,871 C5 queries per batch to
+// tier 1b before the arena (profiles/r03_s4_ab_ecap.txt).
 uint32_t emit_cap_forced() {  // NGS_ECAP: fixed slots per query, no growth (experiments)
     static const uint32_t forced = [] {
         const char* e = std::getenv("NGS_ECAP");  // (at least the rank-list tail, kRankInfo, plus 64)
@@ -831,7 +844,10 @@ uint32_t emit_cap(size_t B) {
         return e ? std::max<uint32_t>(kRankInfo + 64, (uint32_t)std::strtoul(e, nullptr, 0)) : 0u;
     }();
     if (init) return init;
-    return B <= kEmitWideBatch ? std::max(kEmitCap, kEmitCapWide) : kEmitCap;
+    if (B > kEmitWideBatch) return kEmitCap;
+    uint32_t cap = std::max(kEmitCap, kEmitCapWide);
+    while (cap > kEmitCap && (uint64_t)B * cap * 5ull > kEmitWideBytes) cap /= 2;
+    return cap;
 }
 
 // The most survivor slots per query a batch of B may grow to: powers of two up to kEmitCapMax,
@@ -886,12 +902,17 @@ bool ensure_queries(Context& c, size_t B, size_t bytes) {
 
 // The survivor arena of a context (SearchParams.at): kArenaInit blocks of kArenaBlock entries to
 // start with (a C3 query has ~35 survivors, so only outliers ever use it), after a call that ran out
-// four times as many or twice what it asked for (its failed requests undercount the need), within
+// 5/4 of the blocks it would have needed (each query it ran out for estimates its own need from the
+// share of its postings counted), at least 3/2 as many, within
 // kArenaBudget bytes. A query's first-block word per row of the batch.
 constexpr uint32_t kArenaInit = 1024;                // 1M survivors, 5 MB
 constexpr uint64_t kArenaBudget = 4ull << 30;
 bool ensure_arena(Context& c, size_t B) {
-    const uint32_t want = std::max<uint32_t>({kArenaInit, c.ablocks, c.arena_grow});
+    static const uint32_t init = [] {  // NGS_ARENA_INIT (tests): a smaller first arena
+        const char* e = std::getenv("NGS_ARENA_INIT");
+        return e ? std::max<uint32_t>(1, (uint32_t)std::strtoul(e, nullptr, 0)) : kArenaInit;
+    }();
+    const uint32_t want = std::max<uint32_t>({init, c.ablocks, c.arena_grow});
     if (!c.d_eovf || B > c.eorows) {
         if (c.d_eovf) { hipFree(c.d_eovf); c.d_eovf = nullptr; }
         const size_t nb = std::max<size_t>(B, 1024);
@@ -1148,10 +1169,13 @@ int finish_search(Library& L, Replica& R, Context& c, uint32_t B, const SearchPa
     // after kCalmCalls calls in a row that filled none of grown slots, half of them go back
     // the arena's block counter: past its blocks, the arena ran out (those queries went to tier 1b and
     // count as slot_full): later calls get a larger arena, not more slots per query
+    // (the queries it ran out for add the blocks they would still need, the next word: the next
+    // call's arena is 5/4 of the estimated need, at least 3/2 of this one)
     const uint32_t arena_used = small ? 0u : counts3[kArenaCtrWord];
     const bool arena_out = !small && P.at && arena_used > P.ablocks;
     if (arena_out) {
-        const uint64_t want = std::max<uint64_t>(4ull * P.ablocks, 2ull * arena_used);
+        const uint64_t need = (uint64_t)P.ablocks + counts3[kArenaCtrWord + 1];
+        const uint64_t want = std::max<uint64_t>(3ull * P.ablocks / 2, 5ull * need / 4);
         const uint64_t cap = kArenaBudget / ((uint64_t)kArenaBlock * (sizeof(uint32_t) + sizeof(uint8_t)));
         c.arena_grow = (uint32_t)std::min<uint64_t>(want, cap);
     }

@@ -233,6 +233,7 @@ constexpr uint32_t kRankInfo = 3 * 64;
 // batches up to kEmitWideBatch queries get kEmitCapWide slots per query (5 bytes each): a
 // threshold-0 query has thousands of one-hit survivors at C2 (part_ones)
 constexpr uint32_t kEmitCapWide = 4096;
+constexpr uint64_t kEmitWideBytes = 1ull << 30;       // ... halved until the batch's slots fit this
 constexpr uint32_t kEmitCapMax = 32768;              // ... grown up to this many per query
 #ifndef NGS_ARENA
 #define NGS_ARENA 1  // 0 (A/B only): no survivor arena, a query past its slots goes to tier 1b
@@ -240,6 +241,7 @@ constexpr uint32_t kEmitCapMax = 32768;              // ... grown up to this man
 constexpr uint32_t kArenaBlock = 1024;               // survivor arena block (entries; a multiple of 128)
 constexpr uint32_t kArenaChain = 128;                // blocks one query may chain (k_emit lists them in LDS)
 constexpr uint32_t kArenaCtrWord = 12;               // SearchParams.actr: this word of the path-count line
+                                                     // (and the next: blocks still needed when it ran out)
 constexpr uint64_t kEmitBudget = 16ull << 30;         // ... within this many bytes per context
 constexpr size_t kEmitWideBatch = 262144;             // tier 1a survivors per query spilled to HBM for k_emit
 constexpr uint32_t kWaveMaxGrams = 63;          // counts <= 63: one lane per count value
@@ -247,6 +249,9 @@ constexpr uint32_t kWaveMaxGrams = 63;          // counts <= 63: one lane per co
 #define NGS_SK2 2     // smallest cmin counted by the sketch (below: exact hash counting)
 #endif
 constexpr uint32_t kSketchMinCmin = NGS_SK2;
+#ifndef NGS_SKIP4
+#define NGS_SKIP4 0  // 1: build skip4; 2: also round tier 1a's bucket groups of >= 4 to a multiple of 4
+#endif
 
 struct DevIndex {  // passed by value to kernels; all pointers are device pointers
     const uint64_t* gram_off;   // [kGramSpace + 1] -> post
@@ -254,6 +259,9 @@ struct DevIndex {  // passed by value to kernels; all pointers are device pointe
     const uint32_t* gram_row;   // [kGramSpace] -> row of skip (UINT32_MAX = empty)
     const uint32_t* skip;       // [rows][n_buckets + 1] offset of the first posting >= b * bucket_span
     uint32_t n_buckets, bucket_span;
+    // every fourth column of skip ([rows][n_buckets / 4 + 1]; null: none): tier 1a's groups of a
+    // multiple of four buckets read their part ends contiguously (NGS_SKIP4)
+    const uint32_t* skip4;
     const uint64_t* term_off;   // [n_terms + 1] -> term_bytes (normalised terms)
     const uint8_t* term_bytes;
     const uint32_t* tk_off;     // [n_terms + 1] -> tk
@@ -309,7 +317,7 @@ struct SearchParams {
     uint32_t* esn;
     uint32_t* est;
     uint8_t* esc;
-    uint32_t ecap;       // survivor slots per query (kEmitCap, or kEmitCapWide for batches <= kEmitWideBatch)
+    uint32_t ecap;       // survivor slots per query (emit_cap: kEmitCap .. kEmitCapWide, grown by the host)
     // sliced tier 1b (kSlices): the full list and the hand-over lists run as nslices term-id
     // slices of each query (one wave each, bucket ranges of the skip table); slice j of query q
     // leaves its top-L records at prec[(q * nslices + j) * limit] and their count at

@@ -2839,6 +2839,7 @@ __device__ __forceinline__ void lean_query_g(WaveSmem<1, true>& S, const uint32_
     // arena (SearchParams.at); false if neither has room
     // (arena blocks chained so far and the last two of them live in LDS words tier 1a does not use,
     // not in registers across the part loop: the arena is the rare path)
+    uint32_t a_held = 0;  // the arena ran out for this query: 1 + the blocks it holds (arena_need)
     auto spill_arena = [&]() -> bool {  // (rare: survivors past the query's slots)
         const uint32_t end = spilled + surv_n;
         const uint32_t k1 = (end - 1u - ecap_q) / kArenaBlock;  // last chained block the spill needs
@@ -2849,7 +2850,10 @@ __device__ __forceinline__ void lean_query_g(WaveSmem<1, true>& S, const uint32_
             uint32_t nb = 0;
             if (lane == 0) nb = atomicAdd(P.actr, 1u);
             nb = __builtin_amdgcn_readfirstlane(nb);
-            if (nb >= P.ablocks) return false;  // the arena ran out (the counter tells the host)
+            if (nb >= P.ablocks) {  // the arena ran out (the counter tells the host)
+                a_held = a_n + 1u;
+                return false;
+            }
             if (lane == 0) {
                 P.anext[nb] = 0;
                 if (a_n == 0) P.eovf[q] = nb + 1u;
@@ -2899,6 +2903,15 @@ __device__ __forceinline__ void lean_query_g(WaveSmem<1, true>& S, const uint32_
     auto slot_full = [&]() {
         if (lane == 0 && !(P.dbg & 32u)) atomicAdd(&stats[q & (kStatSlots - 1)].slot_full, 1u);
     };
+    // a query the arena ran out for: the blocks it would still need, from its survivors so far and
+    // the share of its postings counted (p_done of p_total), for the host's next arena size
+    auto arena_need = [&](uint32_t p_done) {
+        if (!a_held) return;
+        const uint64_t est = (uint64_t)(spilled + surv_n) * p_total / max(p_done, 1u);
+        const uint64_t need = est > ecap_q ? (est - ecap_q + kArenaBlock - 1u) / kArenaBlock : 0u;
+        const uint64_t more = min64(need > a_held - 1u ? need - (a_held - 1u) : 0u, kArenaChain);
+        if (lane == 0) atomicAdd(P.actr + 1, (uint32_t)more);
+    };
     if (p_total && cmin <= n) {
         // ---- lane groups: list j owns lanes [gend_j - gq_j, gend_j), gq_j = 1 + (64 - ng) len_j / P ----
         const uint32_t quota = lane < ng ? 1u + (uint32_t)(((uint64_t)(64u - ng) * glen) / p_total) : 0u;
@@ -2917,8 +2930,15 @@ __device__ __forceinline__ void lean_query_g(WaveSmem<1, true>& S, const uint32_
         const uint32_t capc = has ? min(3u * G, max(2u, (3u * G) >> shrink)) : 0u;
         const uint32_t K = X.n_buckets, span = X.bucket_span;
         const uint32_t wmax = (uint32_t)max64(1, min64(K, kMaxPartSpan / max(span, 1u)));
-        const uint32_t w = (uint32_t)max64(1, min64(wmax, (uint64_t)K * (kGroupTarget >> shrink) / p_total));
-        const uint32_t skrow = lrow * (K + 1);
+        uint32_t w = (uint32_t)max64(1, min64(wmax, (uint64_t)K * (kGroupTarget >> shrink) / p_total));
+#if NGS_SKIP4 >= 2
+        if (X.skip4 && w >= 4) w = ((w + 2u) & ~3u) <= wmax ? (w + 2u) & ~3u : w & ~3u;
+#endif
+        // groups of a multiple of four buckets: part ends from skip4, one contiguous entry per part
+        const bool s4 = NGS_SKIP4 && X.skip4 && (w & 3u) == 0;
+        const uint32_t* sktab = s4 ? X.skip4 : X.skip;
+        const uint32_t sksh = s4 ? 2u : 0u;
+        const uint32_t skrow = lrow * ((K >> sksh) + 1);
         WSTAMP(1);
         gptr<uint4> post4 = (gptr<uint4>)reinterpret_cast<const uint4*>(X.post);
         asm volatile("" : "+s"(post4));
@@ -2927,7 +2947,7 @@ __device__ __forceinline__ void lean_query_g(WaveSmem<1, true>& S, const uint32_
         // entries [s, e) of this lane's list cover 16-byte chunks [(a0 + s) / 4, (a0 + e + 3) / 4)
         auto chunks = [a0](uint32_t s, uint32_t e) -> uint32_t { return e > s ? ((a0 + e + 3) >> 2) - ((a0 + s) >> 2) : 0u; };
         // end of the next bucket group: skip[row][min(K, bn + w)]; lanes without a list load nothing
-        auto next_end = [&](uint32_t bn) -> uint32_t { return X.skip[skrow + min(K, bn + w)]; };
+        auto next_end = [&](uint32_t bn) -> uint32_t { return sktab[skrow + (min(K, bn + w) >> sksh)]; };
         // fill of the fullest list against its cap, in 1/256: sub-part steps aim at 3/4 of it
         auto fill = [&](uint32_t nc) -> uint32_t {
             const uint32_t f = has ? (nc * 256u + capc - 1u) / capc : 0u;
@@ -3034,7 +3054,11 @@ __device__ __forceinline__ void lean_query_g(WaveSmem<1, true>& S, const uint32_
 #endif
         auto count = [&](const uint4 (&v)[kDmaRounds], const PartGroups& ps) -> bool {
             if (surv_n + 64 > (uint32_t)kWaveSurv) {
-                if (!spill()) { slot_full(); return false; }
+                if (!spill()) {
+                    slot_full();
+                    arena_need((uint32_t)wave_sum((uint64_t)(has && k0 == 0 ? cur : 0u)));
+                    return false;
+                }
                 wave_sync();  // the list is read before it is refilled
             }
             uint32_t nc;
@@ -3077,7 +3101,12 @@ __device__ __forceinline__ void lean_query_g(WaveSmem<1, true>& S, const uint32_
             if (!hp) break;
         }
     }
-    if (!spill()) { slot_full(); bail(); return; }
+    if (!spill()) {
+        slot_full();
+        arena_need((uint32_t)p_total);
+        bail();
+        return;
+    }
     WSTAMP(6);
 #ifdef NGS_PHASE_STAMPS
     if (lane == 0)
@@ -3830,7 +3859,22 @@ __global__ void k_rank_fill(const uint32_t* __restrict__ post, const uint2* __re
     if (i < n) out[i] = tk[n_short + post[i]].x;
 }
 
+__global__ void k_skip4(const uint32_t* __restrict__ skip, uint64_t rows, uint32_t K, uint32_t* __restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t c = K / 4 + 1;
+    if (i >= rows * c) return;
+    const uint64_t r = i / c;
+    out[i] = skip[r * (K + 1) + 4u * (uint32_t)(i - r * c)];
+}
+
 }  // namespace
+
+hipError_t build_skip4(const uint32_t* skip, uint64_t rows, uint32_t K, uint32_t* out, hipStream_t s) {
+    const uint64_t n = rows * (K / 4 + 1);
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_skip4, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, skip, rows, K, out);
+    return hipGetLastError();
+}
 
 hipError_t build_rank_post(const uint64_t* gram_off, uint32_t n_seg, const uint32_t* post, uint64_t n_post,
                            const uint2* tk, uint32_t n_short, uint32_t n_keys, uint32_t* out, hipStream_t s) {

@@ -1,8 +1,9 @@
 """The batch-wide survivor arena (SearchParams.at): tier 1a's main launch writes a query's survivors
 to its slots and, past them, to blocks of an arena shared by the call, chained per query; k_emit
 reads them back in order (nGramSearch.hpp:310-341 over every survivor). Slots are 256 per query here
-(NGS_ECAP_INIT, read once per process: tests/arena_child.py runs in a child process), so queries of
-a few thousand survivors live mostly in the arena. Checked: answers exact against the oracle on
+and the arena starts at 256 blocks of 1,024 (NGS_ECAP_INIT, NGS_ARENA_INIT, read once per process:
+tests/arena_child.py runs in a child process), so queries of ~1,900 survivors live mostly in the
+arena. Checked: answers exact against the oracle on
 every call; the first call runs the arena out (its queries are handed to tier 1b, still exact) and
 the arena grows instead of the slots; later calls fit."""
 import json
@@ -16,7 +17,7 @@ pytestmark = pytest.mark.gpu
 
 
 def test_arena_holds_survivors_past_the_slots():
-    env = dict(os.environ, NGS_ECAP_INIT="256")
+    env = dict(os.environ, NGS_ECAP_INIT="256", NGS_ARENA_INIT="256")
     child = os.path.join(os.path.dirname(os.path.abspath(__file__)), "arena_child.py")
     p = subprocess.run([sys.executable, child], env=env, capture_output=True, text=True, timeout=400)
     assert p.returncode == 0, p.stderr[-3000:]
