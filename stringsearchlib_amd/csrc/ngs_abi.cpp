@@ -676,15 +676,7 @@ bool upload_replica(Library& L, Replica& R, bool keys_unique, bool first) {
     X.skip = skip;
     X.n_buckets = H.n_buckets;
     X.bucket_span = H.bucket_span;
-    X.skip4 = nullptr;
-    if (NGS_SKIP4 && H.n_buckets >= 8 && H.n_grams) {
-        // tier 1a's part ends for groups of 4k buckets (a quarter of the skip table's bytes)
-        uint32_t* s4 = nullptr;
-        if (!dev_alloc(&s4, (size_t)H.n_grams * (H.n_buckets / 4 + 1))) return false;
-        R.owned.push_back(s4);
-        if (!HIP_CHECK(build_skip4(skip, H.n_grams, H.n_buckets, s4, nullptr))) return false;
-        X.skip4 = s4;
-    }
+    X.post_per_row = (uint32_t)std::min<uint64_t>(UINT32_MAX, n_post / std::max<uint64_t>(H.n_grams, 1));
     X.term_off = term_off;
     X.term_bytes = term_bytes;
     X.tk_off = tk_off;
@@ -1023,6 +1015,11 @@ int queue_search(Library& L, Replica& R, Context& c, const uint8_t* d_raw, const
         return e ? (uint32_t)std::strtoul(e, nullptr, 0) : 0u;
     }();
     P.dbg = dbg;
+    static const uint32_t hslices = [] {  // NGS_HEAVY_SLICES: term-id slices per heavy query (0: auto)
+        const char* e = std::getenv("NGS_HEAVY_SLICES");
+        return e ? std::min<uint32_t>((uint32_t)std::strtoul(e, nullptr, 0), kHeavyMaxSlices) : 0u;
+    }();
+    P.hslices = hslices;
     // tier 1: the lean kernel with tier 1b on its hand-overs (batches), or tier 1b alone (the latency path)
     P.waves = small ? 1u : 0u;
     {

@@ -170,6 +170,11 @@ constexpr bool kSketchLoose = NGS_SKETCH_LOOSE != 0;
 constexpr uint32_t kListSlots = 64;             // slot lists per routing list in k_prep
 constexpr uint32_t kNoEmit = 0xFFFFFFFFu;       // esn[q]: query not finished by tier 1a
 constexpr uint32_t kEmitHeavy = 0x80000000u;    // esn[q] flag: finished by the heavy-list launch
+// a sliced heavy query's word (SearchParams.eovf, zeroed by k_prep; heavy queries have no arena):
+// survivor slots taken (low 24 bits), slices finished (kHeavyDone each), handed over (kHeavyBailed)
+constexpr uint32_t kHeavySlotMask = 0xFFFFFFu;
+constexpr uint32_t kHeavyDone = 1u << 24;
+constexpr uint32_t kHeavyBailed = 0x80000000u;
 #ifndef NGS_HEAVY_CMIN
 #define NGS_HEAVY_CMIN 2
 #endif
@@ -207,6 +212,10 @@ constexpr uint32_t kBackPieceMin = 131072;        // ... of at least this many r
 #endif
 constexpr uint32_t kOneStreamBatch = 16384;     // batches up to this size run on one stream per call
 constexpr uint32_t kHeavyGrid = 4096;           // the heavy list's launches: this many workgroups (grid-stride)
+constexpr uint32_t kHeavyMaxSlices = 8;         // ... over (query, term-id slice) items, up to this many per query
+constexpr uint32_t kHeavyItems = 4 * kHeavyGrid; // ... as many slices as keep about this many items
+constexpr uint32_t kHeavySliceList = 1024;      // ... on indexes of at least this many postings per list
+constexpr uint64_t kHeavySlicePostings = 3840;  // ... a slice per this many of the query's postings (~16 parts)
 constexpr bool kSidePriority = false;           // side streams at the highest priority (NGS_SIDE_PRIO; measured no faster)
 #ifndef NGS_SHRINK2
 #define NGS_SHRINK2 0
@@ -249,9 +258,6 @@ constexpr uint32_t kWaveMaxGrams = 63;          // counts <= 63: one lane per co
 #define NGS_SK2 2     // smallest cmin counted by the sketch (below: exact hash counting)
 #endif
 constexpr uint32_t kSketchMinCmin = NGS_SK2;
-#ifndef NGS_SKIP4
-#define NGS_SKIP4 0  // 1: build skip4; 2: also round tier 1a's bucket groups of >= 4 to a multiple of 4
-#endif
 
 struct DevIndex {  // passed by value to kernels; all pointers are device pointers
     const uint64_t* gram_off;   // [kGramSpace + 1] -> post
@@ -259,9 +265,7 @@ struct DevIndex {  // passed by value to kernels; all pointers are device pointe
     const uint32_t* gram_row;   // [kGramSpace] -> row of skip (UINT32_MAX = empty)
     const uint32_t* skip;       // [rows][n_buckets + 1] offset of the first posting >= b * bucket_span
     uint32_t n_buckets, bucket_span;
-    // every fourth column of skip ([rows][n_buckets / 4 + 1]; null: none): tier 1a's groups of a
-    // multiple of four buckets read their part ends contiguously (NGS_SKIP4)
-    const uint32_t* skip4;
+    uint32_t post_per_row;      // postings per non-empty gram list (heavy_slices)
     const uint64_t* term_off;   // [n_terms + 1] -> term_bytes (normalised terms)
     const uint8_t* term_bytes;
     const uint32_t* tk_off;     // [n_terms + 1] -> tk
@@ -312,6 +316,9 @@ struct SearchParams {
     uint32_t dbg;        // ablation switches for performance experiments (NGS_DEBUG); 0 in production
     uint32_t waves;      // tier 1: 0 = lean 1a + full 1b (batches), 1 = the full kernel alone (latency path)
     uint32_t lean_all;     // tier 1a also takes heavy queries (its launch over the heavy list)
+    // the heavy list's launch: term-id slices per query (0: from the list's length, heavy_slices;
+    // NGS_HEAVY_SLICES); a sliced query's survivors take slots from eovf[q] (heavy_slot)
+    uint32_t hslices;
     // deferred calcScore (kDeferEmit): per query the survivor count (kNoEmit = none) and
     // kEmitCap survivor slots, terms and hit counts
     uint32_t* esn;

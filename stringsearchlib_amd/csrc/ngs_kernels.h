@@ -57,9 +57,6 @@ hipError_t build_wildcard(const float* d_w, uint32_t n_keys, uint32_t* d_keys, f
 // DevIndex.kt_flag of an index with kt_off / kt_term under one validChar set (k_key_flags)
 hipError_t build_key_flags(const DevIndex& X, const uint32_t valid[8], uint8_t* flags, hipStream_t s);
 
-// DevIndex.skip4 from skip: out[r][j] = skip[r][4j], rows x (K / 4 + 1) entries (K a multiple of 4)
-hipError_t build_skip4(const uint32_t* skip, uint64_t rows, uint32_t K, uint32_t* out, hipStream_t s);
-
 // hipcub's int item count bounds the rank lists' segmented sort
 constexpr uint64_t kRankMaxPostings = 0x7FFFFFFFull;
 // Rank lists of an index (DevIndex.rank_post): out[i] = tk[n_short + post[i]].x, each gram's

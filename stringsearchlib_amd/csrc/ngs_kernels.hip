@@ -2266,15 +2266,37 @@ __device__ __forceinline__ void lean_query(WaveSmem<1, true>& S, const uint32_t 
                                            uint32_t* __restrict__ out_n, uint32_t* __restrict__ out_k,
                                            float* __restrict__ out_s, uint32_t* __restrict__ list2,
                                            uint32_t* __restrict__ count2, DevStats* __restrict__ stats,
-                                           uint32_t* __restrict__ fb, uint32_t* __restrict__ fbc) {
+                                           uint32_t* __restrict__ fb, uint32_t* __restrict__ fbc,
+                                           const uint32_t slc = 0, const uint32_t nsl = 1) {
     const uint32_t lane = lane_id();
+    // term-id slice slc of nsl (the heavy list's launch): the query's slices run on separate waves,
+    // take survivor slots from a per-query word (heavy_slot) and the last to finish publishes the
+    // count; a slice that hands the query over marks it there, and only the first one lists it
+    uint32_t nslq = 1;  // slices of this query (cmin-1 queries run whole, in slice 0)
+    auto finish_slice = [&]() {
+        uint32_t old = 0;
+        if (lane == 0) old = atomicAdd(&P.eovf[q], kHeavyDone);
+        old = __builtin_amdgcn_readfirstlane(old);
+        if (((old / kHeavyDone) & 127u) == nslq - 1u && !(old & kHeavyBailed) && lane == 0)
+            P.esn[q] = (old & kHeavySlotMask) | kEmitHeavy;  // the query's last slice
+    };
     auto bail = [&]() {  // hand the query to tier 1b (nothing of it was written yet)
-        if (lane == 0) fb[atomicAdd(fbc, 1u)] = q;
+        if (nslq > 1) {
+            uint32_t old = 0;
+            if (lane == 0) old = atomicOr(&P.eovf[q], kHeavyBailed);
+            old = __builtin_amdgcn_readfirstlane(old);
+            if (!(old & kHeavyBailed) && lane == 0) fb[atomicAdd(fbc, 1u)] = q;
+            finish_slice();
+        } else if (lane == 0) {
+            fb[atomicAdd(fbc, 1u)] = q;
+        }
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     };
     const uint32_t m = qm[q];
     const uint32_t L = P.limit;
+    // (the whole-query cases below are slice 0's)
     if (m == kQueryWildcard) {  // nGramSearch.hpp:356-369, answer precomputed at index time
+        if (slc) return;
         const uint32_t nk = min(L, X.n_keys);
         const size_t ob = (size_t)q * P.out_stride;
         for (uint32_t i = lane; i < nk; i += 64) {
@@ -2285,11 +2307,11 @@ __device__ __forceinline__ void lean_query(WaveSmem<1, true>& S, const uint32_t 
         return;
     }
     if (m == 0) {  // nothing left after normalisation, nGramSearch.hpp:374-375
-        if (lane == 0) out_n[q] = 0;
+        if (lane == 0 && !slc) out_n[q] = 0;
         return;
     }
     if (m <= X.full_scan_len || m - X.gsz + 1 > kWaveMaxGrams || L > kWaveMaxLimit) {
-        if (lane == 0) list2[atomicAdd(count2, 1u)] = q;  // tier 2 / library-wide path
+        if (lane == 0 && !slc) list2[atomicAdd(count2, 1u)] = q;  // tier 2 / library-wide path
         return;
     }
     const uint32_t n = m - X.gsz + 1;  // grams of the query (hpp:29-36)
@@ -2307,7 +2329,10 @@ __device__ __forceinline__ void lean_query(WaveSmem<1, true>& S, const uint32_t 
     const uint32_t cmin = pm ? (rank ? 2u : (uint32_t)(__ffsll((long long)pm) - 1)) : 1000u;
     // heavy_class() lists these for launches of their own (same test, same cmin)
     if (!P.lean_all && (cmin <= kHeavyCmin || (m < X.short_query_len && X.n_short))) return;
-    if (m < X.short_query_len && X.n_short) { bail(); return; }  // short search: tier 1b
+    if (m < X.short_query_len && X.n_short) {  // short search: tier 1b
+        if (!slc) bail();
+        return;
+    }
     const uint8_t* qg = qnorm + qoff[q];
     for (uint32_t i = lane; i < m; i += 64) S.q[i] = char_at(qg, i, X.csize);
     {
@@ -2349,11 +2374,18 @@ __device__ __forceinline__ void lean_query(WaveSmem<1, true>& S, const uint32_t 
     const bool sketch = cmin >= kSketchMinCmin && cmin <= kSketchMax;
     const bool ones = ONES && cmin == 1;  // part_ones (the heavy list's launch only)
     constexpr bool kG4 = NGS_LEAN_G4 || ONES;  // list chunk bases in LDS (lean_stage)
-    if (p_total && cmin <= n && !sketch && !ones) { bail(); return; }  // exact counting: tier 1b
+    if (p_total && cmin <= n && !sketch && !ones) {  // exact counting: tier 1b
+        if (!slc) bail();
+        return;
+    }
+    // (a slice per kHeavySlicePostings postings, unless NGS_HEAVY_SLICES forces them)
+    nslq = ones || !p_total || cmin > n ? 1u
+         : P.hslices ? nsl : (uint32_t)min64(nsl, max64(1, p_total / kHeavySlicePostings));
+    if (slc >= nslq) return;
     uint32_t surv_n = 0, spilled = 0;
     // rank lists: the query's lists for k_emit (emit_rank_prefix) in its last kRankInfo slots
     const uint32_t ecap_q = P.ecap - (rank ? kRankInfo : 0u);
-    if (rank) {
+    if (rank && !slc) {
         uint32_t* ri = P.est + (size_t)q * P.ecap + ecap_q;
         ri[lane] = (uint32_t)gbase;
         ri[64 + lane] = (uint32_t)(gbase >> 32);
@@ -2361,11 +2393,17 @@ __device__ __forceinline__ void lean_query(WaveSmem<1, true>& S, const uint32_t 
     }
     // the LDS survivor list to this query's kEmitCap slots in HBM; false if they are full
     auto spill = [&]() -> bool {
-        if (spilled + surv_n > ecap_q) return false;
+        uint32_t at = spilled;
+        if (nslq > 1 && surv_n) {  // a sliced query's slots are shared: take them from its word
+            uint32_t b0 = 0;
+            if (lane == 0) b0 = atomicAdd(&P.eovf[q], surv_n);
+            at = __builtin_amdgcn_readfirstlane(b0) & kHeavySlotMask;
+        }
+        if (at + surv_n > ecap_q) return false;
         uint32_t qs = q, l0 = lane;  // opaque: the slot pointers are made here, not kept (and spilled)
         asm volatile("" : "+s"(qs), "+v"(l0));
-        uint32_t* et = P.est + (size_t)qs * P.ecap + spilled;
-        uint8_t* ec = P.esc + (size_t)qs * P.ecap + spilled;
+        uint32_t* et = P.est + (size_t)qs * P.ecap + at;
+        uint8_t* ec = P.esc + (size_t)qs * P.ecap + at;
         for (uint32_t i = l0; i < surv_n; i += 64) {
             et[i] = S.surv_t[i];
             ec[i] = S.surv_c[i];
@@ -2396,6 +2434,8 @@ __device__ __forceinline__ void lean_query(WaveSmem<1, true>& S, const uint32_t 
         const uint32_t wmax = (uint32_t)max64(1, min64(K, kMaxPartSpan / max(span, 1u)));
         const uint32_t w = (uint32_t)max64(1, min64(wmax, (uint64_t)K * (kSketchTarget >> shrink) / p_total));
         const uint32_t* sk = X.skip + (size_t)grow * (K + 1);
+        // this slice's buckets [b0, Kend)
+        const uint32_t b0 = K * slc / nslq, Kend = K * (slc + 1) / nslq;
         // an opaque SGPR pair: otherwise the compiler keeps it inside the 8-dword kernarg tuple it
         // loaded it with and reloads all 8 dwords from VGPR lanes (v_readlane, VALU) every round
         gptr<uint4> post4 = (gptr<uint4>)reinterpret_cast<const uint4*>(X.post);
@@ -2405,9 +2445,9 @@ __device__ __forceinline__ void lean_query(WaveSmem<1, true>& S, const uint32_t 
         // entries [s, e) of this lane's list cover 16-byte chunks [(a0 + s) / 4, (a0 + e + 3) / 4)
         auto chunks = [a0](uint32_t s, uint32_t e) -> uint32_t { return e > s ? ((a0 + e + 3) >> 2) - ((a0 + s) >> 2) : 0u; };
         // end of the next bucket group: skip[row][min(K, bn + w)]; idle lanes load nothing
-        auto next_end = [&](uint32_t bn) -> uint32_t { return sk[min(K, bn + w)]; };
-        uint32_t cur = 0, bnext = 0;
-        uint32_t e_pre = lane < ng ? next_end(0) : 0u;
+        auto next_end = [&](uint32_t bn) -> uint32_t { return sk[min(Kend, bn + w)]; };
+        uint32_t cur = b0 && lane < ng ? sk[b0] : 0u, bnext = b0;
+        uint32_t e_pre = lane < ng ? next_end(b0) : 0u;
         uint32_t in_sub = 0, sub_lo = 0, hi_lim = 0, sub_end = 0, sub_bnext = 0, step = 1;
         // software pipeline in registers: part i+1's loads are in flight while part i is counted
         uint4 pv[kDmaRounds];
@@ -2429,14 +2469,14 @@ __device__ __forceinline__ void lean_query(WaveSmem<1, true>& S, const uint32_t 
             in_sub = __builtin_amdgcn_readfirstlane(in_sub);
             bnext = __builtin_amdgcn_readfirstlane(bnext);
             bool fast = false;
-            if (!in_sub && bnext < K) {  // common case, straight-line: the next bucket group fits
+            if (!in_sub && bnext < Kend) {  // common case, straight-line: the next bucket group fits
                 const uint32_t e = lane < ng ? e_pre : cur;
                 nch = chunks(cur, e);
                 incl = wave_incl_scan(nch);
                 tot = __builtin_amdgcn_readlane(incl, 63);
                 if (tot && tot <= kChunks) {
                     len = e - cur;
-                    bnext = min(K, bnext + w);
+                    bnext = min(Kend, bnext + w);
                     if (!NGS_LEAN_DEFER_SKIP && lane < ng) e_pre = next_end(bnext);
                     have_p = true;
                     fast = true;  // e_pre of the next group loads after this part's loads (below)
@@ -2454,8 +2494,8 @@ __device__ __forceinline__ void lean_query(WaveSmem<1, true>& S, const uint32_t 
                     break;
                 }
                 if (!in_sub) {
-                    if (bnext >= K) break;
-                    const uint32_t bhi = min(K, bnext + w), e = lane < ng ? e_pre : cur;
+                    if (bnext >= Kend) break;
+                    const uint32_t bhi = min(Kend, bnext + w), e = lane < ng ? e_pre : cur;
                     nch = chunks(cur, e);
                     incl = wave_incl_scan(nch);
                     tot = __builtin_amdgcn_readlane(incl, 63);
@@ -2550,12 +2590,15 @@ __device__ __forceinline__ void lean_query(WaveSmem<1, true>& S, const uint32_t 
     if (lane == 0)
         for (int i = 0; i < 16; ++i) atomicAdd(&g_phase[16 + i], wacc_[i]);
 #endif
-    if (lane == 0) P.esn[q] = spilled | (P.lean_all ? kEmitHeavy : 0u);
+    if (nslq > 1) finish_slice();
+    else if (lane == 0) P.esn[q] = spilled | (P.lean_all ? kEmitHeavy : 0u);
     if (lane == 0 && !(P.dbg & 32u)) {
         DevStats* sl = stats + (q & (kStatSlots - 1));
-        atomicAdd(&sl->postings, (unsigned long long)p_total);
-        atomicAdd(&sl->lists, (unsigned long long)ng);
-        atomicAdd(&sl->fast, 1ull);
+        if (!slc) {
+            atomicAdd(&sl->postings, (unsigned long long)p_total);
+            atomicAdd(&sl->lists, (unsigned long long)ng);
+            atomicAdd(&sl->fast, 1ull);
+        }
         atomicAdd(&sl->survivors, (unsigned long long)spilled);
     }
 }
@@ -2930,15 +2973,17 @@ __device__ __forceinline__ void lean_query_g(WaveSmem<1, true>& S, const uint32_
         const uint32_t capc = has ? min(3u * G, max(2u, (3u * G) >> shrink)) : 0u;
         const uint32_t K = X.n_buckets, span = X.bucket_span;
         const uint32_t wmax = (uint32_t)max64(1, min64(K, kMaxPartSpan / max(span, 1u)));
-        uint32_t w = (uint32_t)max64(1, min64(wmax, (uint64_t)K * (kGroupTarget >> shrink) / p_total));
-#if NGS_SKIP4 >= 2
-        if (X.skip4 && w >= 4) w = ((w + 2u) & ~3u) <= wmax ? (w + 2u) & ~3u : w & ~3u;
+        const uint32_t w = (uint32_t)max64(1, min64(wmax, (uint64_t)K * (kGroupTarget >> shrink) / p_total));
+        const uint32_t skrow = lrow * (K + 1);
+#ifdef NGS_SLICE_PROBE
+        // diagnostic build (timing only, answers partial): every query counts term-id slice 0 of
+        // NGS_SLICE_PROBE (NGS_DEBUG & 0x100: slice q mod NGS_SLICE_PROBE), to time list locality
+        const uint32_t nsl = NGS_SLICE_PROBE, slc = (P.dbg & 0x100u) ? q % nsl : 0u;
+        const uint32_t b0 = K * slc / nsl, Kend = K * (slc + 1) / nsl;
+#else
+        constexpr uint32_t b0 = 0;
+        const uint32_t Kend = K;
 #endif
-        // groups of a multiple of four buckets: part ends from skip4, one contiguous entry per part
-        const bool s4 = NGS_SKIP4 && X.skip4 && (w & 3u) == 0;
-        const uint32_t* sktab = s4 ? X.skip4 : X.skip;
-        const uint32_t sksh = s4 ? 2u : 0u;
-        const uint32_t skrow = lrow * ((K >> sksh) + 1);
         WSTAMP(1);
         gptr<uint4> post4 = (gptr<uint4>)reinterpret_cast<const uint4*>(X.post);
         asm volatile("" : "+s"(post4));
@@ -2947,14 +2992,15 @@ __device__ __forceinline__ void lean_query_g(WaveSmem<1, true>& S, const uint32_
         // entries [s, e) of this lane's list cover 16-byte chunks [(a0 + s) / 4, (a0 + e + 3) / 4)
         auto chunks = [a0](uint32_t s, uint32_t e) -> uint32_t { return e > s ? ((a0 + e + 3) >> 2) - ((a0 + s) >> 2) : 0u; };
         // end of the next bucket group: skip[row][min(K, bn + w)]; lanes without a list load nothing
-        auto next_end = [&](uint32_t bn) -> uint32_t { return sktab[skrow + (min(K, bn + w) >> sksh)]; };
+        auto next_end = [&](uint32_t bn) -> uint32_t { return X.skip[skrow + min(Kend, bn + w)]; };
         // fill of the fullest list against its cap, in 1/256: sub-part steps aim at 3/4 of it
         auto fill = [&](uint32_t nc) -> uint32_t {
             const uint32_t f = has ? (nc * 256u + capc - 1u) / capc : 0u;
             return max(1u, __builtin_amdgcn_readlane(wave_incl_max_scan(f), 63));
         };
-        uint32_t cur = 0, bnext = 0;
-        uint32_t e_pre = has ? next_end(0) : 0u;
+        uint32_t cur = 0, bnext = b0;
+        if (b0) cur = has ? X.skip[skrow + b0] : 0u;
+        uint32_t e_pre = has ? next_end(b0) : 0u;
         // the first skip-table read waited for here: the loop header then merges only the back
         // edge's pending loads (with this one pending the wait there was vmcnt(0) on every part)
         asm volatile("" ::"v"(e_pre));
@@ -2966,12 +3012,12 @@ __device__ __forceinline__ void lean_query_g(WaveSmem<1, true>& S, const uint32_
             bool have_p = false;
             in_sub = __builtin_amdgcn_readfirstlane(in_sub);
             bnext = __builtin_amdgcn_readfirstlane(bnext);
-            if (!in_sub && bnext < K) {  // common case, straight-line: the next bucket group fits
+            if (!in_sub && bnext < Kend) {  // common case, straight-line: the next bucket group fits
                 const uint32_t e = has ? e_pre : cur;
                 nch = chunks(cur, e);
                 if (!__ballot(nch > capc) && __ballot(nch != 0)) {
                     len = e - cur;
-                    bnext = min(K, bnext + w);
+                    bnext = min(Kend, bnext + w);
                     if (has) e_pre = next_end(bnext);
                     return true;
                 }
@@ -2986,8 +3032,8 @@ __device__ __forceinline__ void lean_query_g(WaveSmem<1, true>& S, const uint32_
                     break;
                 }
                 if (!in_sub) {
-                    if (bnext >= K) break;
-                    const uint32_t bhi = min(K, bnext + w), e = has ? e_pre : cur;
+                    if (bnext >= Kend) break;
+                    const uint32_t bhi = min(Kend, bnext + w), e = has ? e_pre : cur;
                     nch = chunks(cur, e);
                     if (!__ballot(nch > capc)) {
                         len = e - cur;
@@ -3262,6 +3308,17 @@ __global__ __launch_bounds__(64) void k_serve(DevIndex X, SearchParams P0, Serve
     if (lane == 0) __hip_atomic_store(&blk->alive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Term-id slices per heavy-list query (the most; lean_query takes fewer for a query of fewer
+// postings): SearchParams.hslices, else as many as keep about kHeavyItems (query, slice) items
+// (C3's ~3,800 heavy queries: 4 each), at most kHeavyMaxSlices and one bucket per slice. None on
+// an index of short lists (C2, 1M rows: ~11 parts per query, where the slices' own set-up cost
+// more than they saved: 40.6 -> 36.0 Mq/s, profiles/r05_s7_ab_c2.txt)
+__device__ __forceinline__ uint32_t heavy_slices(const SearchParams& P, uint32_t cnt, const DevIndex& X) {
+    if (!P.hslices && X.post_per_row < kHeavySliceList) return 1;
+    const uint32_t want = P.hslices ? P.hslices : kHeavyItems / max(cnt, 1u);
+    return max(1u, min(min(want, kHeavyMaxSlices), X.n_buckets));
+}
+
 // Tier 1a: the lean wave kernel over every query (qlist == nullptr), or over the heavy list.
 // DEFER: survivors spill to HBM for k_emit (the heavy launch always; the main one if kDeferEmit).
 // ONES: the heavy list's launch, which also takes cmin-1 queries (part_ones); the main launch
@@ -3307,6 +3364,18 @@ __global__ __launch_bounds__(64, PACKED ? kHeavyLeanWavesPerSimd : kLeanWavesPer
         return;
     }
     const uint32_t cnt = *qcount;  // the heavy list, grid-stride
+    if constexpr (PACKED && NGS_LEAN_GROUPS != 2) {
+        // (query, term-id slice) items, a query's slices on neighbouring workgroups: enough slices
+        // that a short list fills the GPU and no query's wave outlasts the rest by much
+        const uint32_t nsl = heavy_slices(P, cnt, X);
+        for (uint32_t i = blockIdx.x; i < cnt * nsl; i += gridDim.x) {
+            const uint32_t k = i / nsl;
+            lean_query<ONES>(S, qlist[k], X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats, fb, fbc,
+                             i - k * nsl, nsl);
+            wave_sync();
+        }
+        return;
+    }
     for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
         one(qlist[i]);
         wave_sync();
@@ -3859,22 +3928,7 @@ __global__ void k_rank_fill(const uint32_t* __restrict__ post, const uint2* __re
     if (i < n) out[i] = tk[n_short + post[i]].x;
 }
 
-__global__ void k_skip4(const uint32_t* __restrict__ skip, uint64_t rows, uint32_t K, uint32_t* __restrict__ out) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t c = K / 4 + 1;
-    if (i >= rows * c) return;
-    const uint64_t r = i / c;
-    out[i] = skip[r * (K + 1) + 4u * (uint32_t)(i - r * c)];
-}
-
 }  // namespace
-
-hipError_t build_skip4(const uint32_t* skip, uint64_t rows, uint32_t K, uint32_t* out, hipStream_t s) {
-    const uint64_t n = rows * (K / 4 + 1);
-    if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k_skip4, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, skip, rows, K, out);
-    return hipGetLastError();
-}
 
 hipError_t build_rank_post(const uint64_t* gram_off, uint32_t n_seg, const uint32_t* post, uint64_t n_post,
                            const uint2* tk, uint32_t n_short, uint32_t n_keys, uint32_t* out, hipStream_t s) {
