@@ -4114,8 +4114,14 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
             PM.qhead = gcount + 8;
             PHO.qhead = gcount + 9;
             // (esn[] was reset by k_prep)
+            // NGS_LEAN_PAD_LDS (diagnostic): dynamic LDS bytes per workgroup of the main launch, to run
+            // the same code at fewer waves per CU (occupancy sensitivity)
+            static const uint32_t pad_lds = [] {
+                const char* e = std::getenv("NGS_LEAN_PAD_LDS");
+                return e ? (uint32_t)std::strtoul(e, nullptr, 0) : 0u;
+            }();
             auto main_lean = [&]() {
-                hipLaunchKernelGGL((k_wave_lean<kDeferEmit, false, false>), dim3(P.n_queries), dim3(64), 0, s, X,
+                hipLaunchKernelGGL((k_wave_lean<kDeferEmit, false, false>), dim3(P.n_queries), dim3(64), pad_lds, s, X,
                                    P, qnorm, off, qm,
                                    out_n, out_k, out_s, list2, count2, stats, fb, fbc, (const uint32_t*)nullptr,
                                    (const uint32_t*)nullptr);
