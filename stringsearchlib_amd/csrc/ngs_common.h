@@ -213,7 +213,7 @@ constexpr uint32_t kBackPieceMin = 131072;        // ... of at least this many r
 constexpr uint32_t kOneStreamBatch = 16384;     // batches up to this size run on one stream per call
 constexpr uint32_t kHeavyGrid = 4096;           // the heavy list's launches: this many workgroups (grid-stride)
 constexpr uint32_t kHeavyMaxSlices = 8;         // ... over (query, term-id slice) items, up to this many per query
-constexpr uint32_t kHeavyItems = 4 * kHeavyGrid; // ... as many slices as keep about this many items
+constexpr uint32_t kHeavyItems = 8 * kHeavyGrid; // ... as many slices as keep about this many items
 constexpr uint32_t kHeavySliceList = 1024;      // ... on indexes of at least this many postings per list
 constexpr uint64_t kHeavySlicePostings = 3840;  // ... a slice per this many of the query's postings (~16 parts)
 constexpr bool kSidePriority = false;           // side streams at the highest priority (NGS_SIDE_PRIO; measured no faster)

@@ -3310,9 +3310,10 @@ __global__ __launch_bounds__(64) void k_serve(DevIndex X, SearchParams P0, Serve
 
 // Term-id slices per heavy-list query (the most; lean_query takes fewer for a query of fewer
 // postings): SearchParams.hslices, else as many as keep about kHeavyItems (query, slice) items
-// (C3's ~3,800 heavy queries: 4 each), at most kHeavyMaxSlices and one bucket per slice. None on
-// an index of short lists (C2, 1M rows: ~11 parts per query, where the slices' own set-up cost
-// more than they saved: 40.6 -> 36.0 Mq/s, profiles/r05_s7_ab_c2.txt)
+// (C3: ~3,800 heavy queries, up to 8 each; an 8-character one takes 4 by its postings), at most
+// kHeavyMaxSlices and one bucket per slice. None on an index of short lists (C2, 1M rows: ~11
+// parts per query, where the slices' own set-up cost more than they saved: 40.6 -> 36.0 Mq/s,
+// profiles/r05_s7_ab_heavy_slices_c2.txt)
 __device__ __forceinline__ uint32_t heavy_slices(const SearchParams& P, uint32_t cnt, const DevIndex& X) {
     if (!P.hslices && X.post_per_row < kHeavySliceList) return 1;
     const uint32_t want = P.hslices ? P.hslices : kHeavyItems / max(cnt, 1u);
