@@ -3366,15 +3366,18 @@ __global__ __launch_bounds__(64, PACKED ? kHeavyLeanWavesPerSimd : kLeanWavesPer
     }
     const uint32_t cnt = *qcount;  // the heavy list, grid-stride
     if constexpr (PACKED && NGS_LEAN_GROUPS != 2) {
-        // (query, term-id slice) items, a query's slices on neighbouring workgroups: enough slices
-        // that a short list fills the GPU and no query's wave outlasts the rest by much
-        const uint32_t nsl = heavy_slices(P, cnt, X);
-        for (uint32_t i = blockIdx.x; i < cnt * nsl; i += gridDim.x) {
-            const uint32_t k = i / nsl;
-            lean_query<ONES>(S, qlist[k], X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats, fb, fbc,
-                             i - k * nsl, nsl);
-            wave_sync();
-        }
+        // (query, term-id slice) items, one per workgroup (heavy_grid sizes the launch for every
+        // item; the rest exit), a query's slices on neighbouring workgroups: enough slices that a
+        // short list fills the GPU and no query's wave outlasts the rest by much. No item loop: in one
+        // the compiler hoists the arguments' loads out of it and the part loop spills (14-18 VGPRs,
+        // whose reloads waited for the next part's loads in the counting: an all-heavy batch of 8,192
+        // 8-character queries 0.98 -> 0.75 ms per call). (Lane-group staging here measured slower
+        // on C2: 32.0-32.8 against 37.1-37.3 Mq/s, profiles/r05_s12_ab_heavy_staging.txt.)
+        const uint32_t nsl = heavy_slices(P, cnt, X), i = blockIdx.x;
+        if (i >= cnt * nsl) return;
+        const uint32_t k = i / nsl;
+        lean_query<ONES>(S, qlist[k], X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats, fb, fbc,
+                         i - k * nsl, nsl);
         return;
     }
     for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
@@ -4090,6 +4093,17 @@ hipError_t launch_prep(const uint8_t* raw, const uint64_t* off, uint32_t B, cons
     return hipGetLastError();
 }
 
+// Workgroups of the heavy list's lean launch: one per (query, slice) item heavy_slices can make
+// from a list of up to n_queries queries. Automatic slicing keeps cnt x slices within
+// max(kHeavyItems, cnt): on long-list indexes max(kHeavyItems, n_queries) workgroups (C3: 65,536 for
+// ~31k items), else one per query (C2); NGS_HEAVY_SLICES: n_queries x that many.
+uint32_t heavy_grid(const DevIndex& X, const SearchParams& P) {
+    const uint64_t B = std::max<uint32_t>(P.n_queries, 1);
+    uint64_t g = P.hslices ? B * std::min<uint32_t>(P.hslices, kHeavyMaxSlices)
+               : X.post_per_row < kHeavySliceList ? B : std::max<uint64_t>(kHeavyItems, B);
+    return (uint32_t)std::min<uint64_t>(g, B * kHeavyMaxSlices);
+}
+
 hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* qnorm, const uint64_t* off,
                        const uint32_t* qm, uint32_t* out_n, uint32_t* out_k, float* out_s, uint32_t* list2,
                        uint32_t* count2, uint32_t* fb, uint32_t* fbc, uint32_t* fb2, uint32_t* fbc2,
@@ -4109,7 +4123,8 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
             // path-count line (zeroed per call with it)
             const uint32_t g1s = std::min<uint32_t>(P.n_queries * std::max<uint32_t>(P.nslices, 1u),
                                                     std::min<uint32_t>(persistent_slots(kWaveWavesPerSimd), kTier1bGrid));
-            const uint32_t gh = std::min<uint32_t>(P.n_queries, kHeavyGrid);
+            const uint32_t gh = std::min<uint32_t>(P.n_queries, kHeavyGrid);  // (the heavy k_emit's grid)
+            const uint32_t ghl = heavy_grid(X, P);                            // the heavy lean launch's
             const uint32_t gfull = std::min<uint32_t>(P.n_queries, std::min<uint32_t>(persistent_slots(kWaveWavesPerSimd), kTier1bGrid));
             SearchParams PM = P, PHO = P;  // the main and the heavy hand-over launches
             PM.qhead = gcount + 8;
@@ -4146,11 +4161,11 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
                     const uint32_t n_min = (X.n_short ? X.short_query_len : X.full_scan_len + 1) - X.gsz + 1;
                     const bool ones = kLeanOnes && (NGS_HEAVY_ONES_ALWAYS || (!X.rank_post && !(1.0f / (float)n_min < P.thr)));
                     if (ones)
-                        hipLaunchKernelGGL((k_wave_lean<true, kLeanOnes, true, true>), dim3(gh), dim3(64), 0, side, X, PH,
+                        hipLaunchKernelGGL((k_wave_lean<true, kLeanOnes, true, true>), dim3(ghl), dim3(64), 0, side, X, PH,
                                            qnorm, off, qm, out_n, out_k, out_s, list2, count2, stats, fb2, fbc2, heavy,
                                            hcount);
                     else
-                        hipLaunchKernelGGL((k_wave_lean<true, false, true, true>), dim3(gh), dim3(64), 0, side, X, PH, qnorm,
+                        hipLaunchKernelGGL((k_wave_lean<true, false, true, true>), dim3(ghl), dim3(64), 0, side, X, PH, qnorm,
                                            off, qm, out_n, out_k, out_s, list2, count2, stats, fb2, fbc2, heavy, hcount);
                     dbg_check(side, "k_wave_lean (heavy list)");
                     hipLaunchKernelGGL(k_emit<true>, dim3((gh + kEmitWaves - 1) / kEmitWaves), dim3(64 * kEmitWaves), 0,
