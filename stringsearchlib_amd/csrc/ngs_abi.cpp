@@ -348,6 +348,10 @@ struct Replica {
     // until dispose (a launch in flight may still read an older set's)
     std::mutex kflag_mu;
     std::vector<std::pair<std::array<uint32_t, 8>, uint8_t*>> kflags;
+    // NGS_SERIAL_MAIN: the last main tier-1a launch of any call on this replica (launch_fast)
+    std::mutex main_mu;
+    hipEvent_t main_ev = nullptr;
+    bool main_rec = false;
 
     // the index as the kernels of a search under `valid` see it (kt_flag for that set); false on a
     // HIP failure
@@ -376,6 +380,7 @@ struct Replica {
     ~Replica() {
         pool.clear();
         hipSetDevice(device);
+        if (main_ev) hipEventDestroy(main_ev);
         for (void* p : owned) hipFree(p);
     }
 
@@ -1103,10 +1108,30 @@ int queue_search(Library& L, Replica& R, Context& c, const uint8_t* d_raw, const
                                gc + 5, c.d_lslots, c.d_lctr, s, side, c.prep_ev, c.lists_ev)))
         return -4;
     if (timing) HIP_CHECK(hipEventRecord(c.ev[1], s));  // the end of k_prep is the start of the tier-1 phase
-    if (!HIP_CHECK(launch_fast(X, P, c.d_norm, d_off, c.d_qm, d_n, d_k, d_s, c.d_list2, gc + 1, c.d_fb, gc + 2,
-                               c.d_fb2, gc + 4, c.d_heavy, gc + 3, c.d_full, gc + 5, c.d_glist, gc, sd, s, side,
-                               side2, c.join, c.join2, c.lists_ev, all_heavy && !NGS_NO_SKIP_EMPTY)))
-        return -4;
+    // the main tier-1a launches of this replica's calls one after another (NGS_SERIAL_MAIN=0: not):
+    // with two calls in flight the second call's main launch otherwise starts in the first one's and
+    // the two share the GPU (C3, one box, three passes each: 31.3-31.6 against 30.1-30.6 Mq/s,
+    // profiles/r05_s15_ab_serial_main.txt; C5 the same)
+    static const bool serial_main = [] {
+        const char* e = std::getenv("NGS_SERIAL_MAIN");
+        return !e || std::atoi(e) != 0;
+    }();
+    {
+        std::unique_lock<std::mutex> g(R.main_mu, std::defer_lock);
+        hipEvent_t mev = nullptr;
+        bool mwait = false;
+        if (serial_main && !small) {
+            g.lock();
+            if (!R.main_ev && !HIP_CHECK(hipEventCreateWithFlags(&R.main_ev, hipEventDisableTiming))) return -4;
+            mev = R.main_ev;
+            mwait = R.main_rec;
+            R.main_rec = true;
+        }
+        if (!HIP_CHECK(launch_fast(X, P, c.d_norm, d_off, c.d_qm, d_n, d_k, d_s, c.d_list2, gc + 1, c.d_fb, gc + 2,
+                                   c.d_fb2, gc + 4, c.d_heavy, gc + 3, c.d_full, gc + 5, c.d_glist, gc, sd, s, side,
+                                   side2, c.join, c.join2, c.lists_ev, all_heavy && !NGS_NO_SKIP_EMPTY, mev, mwait)))
+            return -4;
+    }
     if (timing) HIP_CHECK(hipEventRecord(c.ev[3], s));
     // the statistics and the path counts in one read-back (the general path adds no statistics)
     if (!small && !HIP_CHECK(hipMemcpyAsync(c.h_stats, c.d_stats, kSioStats, hipMemcpyDeviceToHost, s))) return -4;

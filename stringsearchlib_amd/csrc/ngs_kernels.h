@@ -29,7 +29,7 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
                        const uint32_t* heavy, const uint32_t* hcount, const uint32_t* full,
                        const uint32_t* fcount, uint32_t* glist, uint32_t* gcount, DevStats* stats, hipStream_t s,
                        hipStream_t side, hipStream_t side2, hipEvent_t join, hipEvent_t join2,
-                       hipEvent_t lists_ev, bool all_heavy = false);
+                       hipEvent_t lists_ev, bool all_heavy = false, hipEvent_t main_ev = nullptr, bool main_wait = false);
 
 // The low-latency server (ngsServe): one persistent one-wave workgroup on `s` serving requests
 // from `blk` (coherent pinned host memory, device view) until blk->stop, or until no request

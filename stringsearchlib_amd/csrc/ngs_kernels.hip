@@ -4110,7 +4110,7 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
                        const uint32_t* heavy, const uint32_t* hcount, const uint32_t* full,
                        const uint32_t* fcount, uint32_t* glist, uint32_t* gcount, DevStats* stats, hipStream_t s,
                        hipStream_t side, hipStream_t side2, hipEvent_t join, hipEvent_t join2,
-                       hipEvent_t lists_ev, bool all_heavy) {
+                       hipEvent_t lists_ev, bool all_heavy, hipEvent_t main_ev, bool main_wait) {
     if (!P.n_queries) return hipSuccess;
     hipError_t e = hipSuccess;
     switch (P.waves) {  // SearchParams.waves: 0 = tier 1a + 1b (batches), 1 = tier 1b alone (latency path)
@@ -4136,12 +4136,16 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
                 const char* e = std::getenv("NGS_LEAN_PAD_LDS");
                 return e ? (uint32_t)std::strtoul(e, nullptr, 0) : 0u;
             }();
+            // main_ev (NGS_SERIAL_MAIN): the replica's last main launch, waited for (main_wait) before this
+            // one and recorded after it, so that two calls in flight do not run their main launches at once
             auto main_lean = [&]() {
+                if (main_ev && main_wait) (void)hipStreamWaitEvent(s, main_ev, 0);
                 hipLaunchKernelGGL((k_wave_lean<kDeferEmit, false, false>), dim3(P.n_queries), dim3(64), pad_lds, s, X,
                                    P, qnorm, off, qm,
                                    out_n, out_k, out_s, list2, count2, stats, fb, fbc, (const uint32_t*)nullptr,
                                    (const uint32_t*)nullptr);
                 dbg_check(s, "k_wave_lean");
+                if (main_ev) (void)hipEventRecord(main_ev, s);
             };
             // the main launch is queued first: the GPU idled ~35 us while the host queued the side
             // streams' launches ahead of it
