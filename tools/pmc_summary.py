@@ -19,6 +19,10 @@ import os
 import sys
 from collections import defaultdict
 
+# the main tier-1a launch (one workgroup per query); the heavy list's launch has the same grid since
+# round 5 (one workgroup per item), so it is told apart by its template arguments
+MAIN = "k_wave_lean<true, false, false, false>"
+
 N_CU = 256
 N_SE = 32  # 8 XCDs x 4 shader engines
 N_SIMD = 4 * N_CU
@@ -26,7 +30,7 @@ VALU_ISSUE_CYCLES = 2
 NOMINAL_GHZ = 2.4
 
 
-def main(root, kernel_substr="k_wave_lean"):
+def main(root, kernel_substr=MAIN):
     per = defaultdict(lambda: defaultdict(float))
     grid, span = {}, {}
     for f in sorted(glob.glob(os.path.join(root, "p*", "**", "run_counter_collection.csv"), recursive=True)):
@@ -89,4 +93,4 @@ def main(root, kernel_substr="k_wave_lean"):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "k_wave_lean")
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else MAIN)

@@ -19,10 +19,14 @@ import os
 import sys
 from collections import defaultdict
 
+# the main tier-1a launch (one workgroup per query); the heavy list's launch has the same grid since
+# round 5 (one workgroup per item), so it is told apart by its template arguments
+MAIN = "k_wave_lean<true, false, false, false>"
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def main_kernel_ns(src, kernel="k_wave_lean"):
+def main_kernel_ns(src, kernel=MAIN):
     """Mean duration of the largest-grid dispatches of `kernel` in a --pmc pass (its own timestamps)."""
     span, grid = {}, {}
     for f in glob.glob(os.path.join(src, "**", "run_counter_collection.csv"), recursive=True):
@@ -37,7 +41,7 @@ def main_kernel_ns(src, kernel="k_wave_lean"):
     return sum(d) / len(d) if d else None
 
 
-def main(src, cfg, kernel="k_wave_lean", sq=None, library=None):
+def main(src, cfg, kernel=MAIN, sq=None, library=None):
     """HBM bytes of one search call's tier-1 phase: every k_wave* / k_emit / k_fast dispatch of
     the pass (tier 1a over the batch and over the heavy list, k_emit, tier 1b on the full list
     and on hand-overs, tier 2), divided by the number of main tier-1a dispatches (one per call:
@@ -88,7 +92,7 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("src")
     ap.add_argument("cfg")
-    ap.add_argument("kernel", nargs="?", default="k_wave_lean")
+    ap.add_argument("kernel", nargs="?", default=MAIN)
     ap.add_argument("--sq")
     ap.add_argument("--library")
     a = ap.parse_args()

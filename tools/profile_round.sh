@@ -20,6 +20,6 @@ timeout -s KILL 180 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $OUT/fetch -o r
 timeout -s KILL 180 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS GRBM_GUI_ACTIVE -d $OUT/sq -o run --output-format csv -- \
     python3 bench.py --config $CFG --no-cpu-baseline --no-dropin --steps 5 --warmup 1 > $OUT/sq_bench.json 2> $OUT/sq_bench.err || { echo "sq pass failed"; exit 1; }
 LIBV=$(python3 -c "import json; print(json.load(open('$OUT/fetch_bench.json'))['detail']['library'])") || exit 1
-python3 tools/pmc_traffic.py $OUT/fetch $CFG k_wave_lean --sq $OUT/sq --library "$LIBV" || exit 1
+python3 tools/pmc_traffic.py $OUT/fetch $CFG --sq $OUT/sq --library "$LIBV" || exit 1
 timeout -k 10 400 python3 bench.py --config $CFG > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; exit 1; }
 cat $OUT/bench.json
