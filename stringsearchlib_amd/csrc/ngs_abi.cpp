@@ -256,6 +256,7 @@ struct Context {
     uint32_t* d_at = nullptr;
     uint8_t* d_ac = nullptr;
     uint32_t ablocks = 0, arena_grow = 0;
+    uint32_t heavy_items = 0;      // (query, slice) items of the last call's heavy launch (SearchParams.hgrid)
     size_t eorows = 0;
     uint64_t* d_prec = nullptr;    // sliced tier 1b: top-L records per (query, slice)
     uint32_t* d_pcnt = nullptr;    // ... and their counts
@@ -1025,6 +1026,8 @@ int queue_search(Library& L, Replica& R, Context& c, const uint8_t* d_raw, const
         return e ? std::min<uint32_t>((uint32_t)std::strtoul(e, nullptr, 0), kHeavyMaxSlices) : 0u;
     }();
     P.hslices = hslices;
+    P.hbase = 0;
+    P.hgrid = c.heavy_items ? c.heavy_items + c.heavy_items / 8 + 64 : 0u;  // (a margin: batches change)
     // tier 1: the lean kernel with tier 1b on its hand-overs (batches), or tier 1b alone (the latency path)
     P.waves = small ? 1u : 0u;
     {
@@ -1193,6 +1196,7 @@ int finish_search(Library& L, Replica& R, Context& c, uint32_t B, const SearchPa
     // count as slot_full): later calls get a larger arena, not more slots per query
     // (the queries it ran out for add the blocks they would still need, the next word: the next
     // call's arena is 5/4 of the estimated need, at least 3/2 of this one)
+    if (!small) c.heavy_items = counts3[3] * heavy_slices(P, counts3[3], R.dev);  // the next call's heavy grid
     const uint32_t arena_used = small ? 0u : counts3[kArenaCtrWord];
     const bool arena_out = !small && P.at && arena_used > P.ablocks;
     if (arena_out) {

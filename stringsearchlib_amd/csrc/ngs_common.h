@@ -215,6 +215,7 @@ constexpr uint32_t kHeavyGrid = 4096;           // the heavy list's launches: th
 constexpr uint32_t kHeavyMaxSlices = 8;         // ... over (query, term-id slice) items, up to this many per query
 constexpr uint32_t kHeavyItems = 8 * kHeavyGrid; // ... as many slices as keep about this many items
 constexpr uint32_t kHeavySliceList = 1024;      // ... on indexes of at least this many postings per list
+constexpr uint32_t kHeavyOverflowGrid = 1024;   // ... the overflow launch's grid (items past the hinted grid)
 constexpr uint64_t kHeavySlicePostings = 3840;  // ... a slice per this many of the query's postings (~16 parts)
 constexpr bool kSidePriority = false;           // side streams at the highest priority (NGS_SIDE_PRIO; measured no faster)
 #ifndef NGS_SHRINK2
@@ -317,8 +318,10 @@ struct SearchParams {
     uint32_t waves;      // tier 1: 0 = lean 1a + full 1b (batches), 1 = the full kernel alone (latency path)
     uint32_t lean_all;     // tier 1a also takes heavy queries (its launch over the heavy list)
     // the heavy list's launch: term-id slices per query (0: from the list's length, heavy_slices;
-    // NGS_HEAVY_SLICES); a sliced query's survivors take slots from eovf[q] (heavy_slot)
-    uint32_t hslices;
+    // NGS_HEAVY_SLICES); a sliced query's survivors take slots from eovf[q] (heavy_slot).
+    // hbase: the first (query, slice) item of a heavy launch (its overflow launch starts past the
+    // first launch's grid); hgrid: the first launch's grid from the context's last call (0: none)
+    uint32_t hslices, hbase, hgrid;
     // deferred calcScore (kDeferEmit): per query the survivor count (kNoEmit = none) and
     // kEmitCap survivor slots, terms and hit counts
     uint32_t* esn;
@@ -356,6 +359,27 @@ struct SearchParams {
     // counter (zeroed with the path counts) instead of one workgroup per item; null: grid-stride
     uint32_t* qhead;
 };
+
+// Term-id slices per heavy-list query (the most; lean_query takes fewer for a query of fewer
+// postings), host and device alike (the host sizes the next call's grid with it): hslices, else
+// as many as keep about kHeavyItems (query, slice) items, no more than the longest heavy query is
+// estimated to use (cmin <= 2: at most 2 / thr grams of post_per_row postings each, a slice per
+// kHeavySlicePostings), at most kHeavyMaxSlices and one bucket per slice. None on an index of short
+// lists (C2, 1M rows: ~11 parts per query, where the slices' own set-up cost more than they saved:
+// 40.6 -> 36.0 Mq/s, profiles/r05_s7_ab_heavy_slices_c2.txt)
+__host__ __device__ inline uint32_t heavy_slices(const SearchParams& P, uint32_t cnt, const DevIndex& X) {
+    if (!P.hslices && X.post_per_row < kHeavySliceList) return 1;
+    uint32_t want = P.hslices;
+    if (!want) {
+        const uint32_t nmax = P.thr > 0.0f && 2.0f / P.thr < (float)kWaveMaxGrams ? (uint32_t)(2.0f / P.thr) : kWaveMaxGrams;
+        const uint64_t est = ((uint64_t)nmax * X.post_per_row + kHeavySlicePostings - 1) / kHeavySlicePostings;
+        want = kHeavyItems / (cnt ? cnt : 1u);
+        if (est < want) want = (uint32_t)(est ? est : 1u);
+    }
+    if (want > kHeavyMaxSlices) want = kHeavyMaxSlices;
+    if (want > X.n_buckets) want = X.n_buckets;
+    return want ? want : 1u;
+}
 
 // Tier 1b slices per query (SearchParams.nslices): a full-list or handed-over query is a few
 // hundred to thousands of survivors in one wave; four waves on disjoint term-id ranges each keep

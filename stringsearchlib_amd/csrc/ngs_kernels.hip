@@ -3308,18 +3308,6 @@ __global__ __launch_bounds__(64) void k_serve(DevIndex X, SearchParams P0, Serve
     if (lane == 0) __hip_atomic_store(&blk->alive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// Term-id slices per heavy-list query (the most; lean_query takes fewer for a query of fewer
-// postings): SearchParams.hslices, else as many as keep about kHeavyItems (query, slice) items
-// (C3: ~3,800 heavy queries, up to 8 each; an 8-character one takes 4 by its postings), at most
-// kHeavyMaxSlices and one bucket per slice. None on an index of short lists (C2, 1M rows: ~11
-// parts per query, where the slices' own set-up cost more than they saved: 40.6 -> 36.0 Mq/s,
-// profiles/r05_s7_ab_heavy_slices_c2.txt)
-__device__ __forceinline__ uint32_t heavy_slices(const SearchParams& P, uint32_t cnt, const DevIndex& X) {
-    if (!P.hslices && X.post_per_row < kHeavySliceList) return 1;
-    const uint32_t want = P.hslices ? P.hslices : kHeavyItems / max(cnt, 1u);
-    return max(1u, min(min(want, kHeavyMaxSlices), X.n_buckets));
-}
-
 // Tier 1a: the lean wave kernel over every query (qlist == nullptr), or over the heavy list.
 // DEFER: survivors spill to HBM for k_emit (the heavy launch always; the main one if kDeferEmit).
 // ONES: the heavy list's launch, which also takes cmin-1 queries (part_ones); the main launch
@@ -3327,7 +3315,7 @@ __device__ __forceinline__ uint32_t heavy_slices(const SearchParams& P, uint32_t
 // one workgroup per query (the main launch): either way the part loop is compiled once (with
 // both in one kernel the main launch carried 76 B of scratch spills and 434 lane reloads; the
 // same speed, profiles/r03_s5_ab_lean_one_copy.txt)
-template <bool DEFER, bool ONES = false, bool LISTED = true, bool PACKED = false>
+template <bool DEFER, bool ONES = false, bool LISTED = true, bool PACKED = false, bool LOOPED = false>
 __global__ __launch_bounds__(64, PACKED ? kHeavyLeanWavesPerSimd : kLeanWavesPerSimd) void k_wave_lean(DevIndex X, SearchParams P,
                                                                     const uint8_t* __restrict__ qnorm,
                                                                     const uint64_t* __restrict__ qoff,
@@ -3373,11 +3361,23 @@ __global__ __launch_bounds__(64, PACKED ? kHeavyLeanWavesPerSimd : kLeanWavesPer
         // whose reloads waited for the next part's loads in the counting: an all-heavy batch of 8,192
         // 8-character queries 0.98 -> 0.75 ms per call). (Lane-group staging here measured slower
         // on C2: 32.0-32.8 against 37.1-37.3 Mq/s, profiles/r05_s12_ab_heavy_staging.txt.)
-        const uint32_t nsl = heavy_slices(P, cnt, X), i = blockIdx.x;
-        if (i >= cnt * nsl) return;
-        const uint32_t k = i / nsl;
-        lean_query<ONES>(S, qlist[k], X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats, fb, fbc,
-                         i - k * nsl, nsl);
+        // (LOOPED: the overflow launch, items past the first launch's grid, grid-stride; it spills,
+        // and runs only when a call has more items than its context's last call)
+        const uint32_t nsl = heavy_slices(P, cnt, X);
+        if constexpr (LOOPED) {
+            for (uint32_t i = P.hbase + blockIdx.x; i < cnt * nsl; i += gridDim.x) {
+                const uint32_t k = i / nsl;
+                lean_query<ONES>(S, qlist[k], X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats, fb, fbc,
+                                 i - k * nsl, nsl);
+                wave_sync();
+            }
+        } else {
+            const uint32_t i = P.hbase + blockIdx.x;
+            if (i >= cnt * nsl) return;
+            const uint32_t k = i / nsl;
+            lean_query<ONES>(S, qlist[k], X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats, fb, fbc,
+                             i - k * nsl, nsl);
+        }
         return;
     }
     for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
@@ -4093,10 +4093,12 @@ hipError_t launch_prep(const uint8_t* raw, const uint64_t* off, uint32_t B, cons
     return hipGetLastError();
 }
 
-// Workgroups of the heavy list's lean launch: one per (query, slice) item heavy_slices can make
-// from a list of up to n_queries queries. Automatic slicing keeps cnt x slices within
-// max(kHeavyItems, cnt): on long-list indexes max(kHeavyItems, n_queries) workgroups (C3: 65,536 for
-// ~31k items), else one per query (C2); NGS_HEAVY_SLICES: n_queries x that many.
+// Workgroups for every (query, slice) item heavy_slices can make from a list of up to n_queries
+// queries: automatic slicing keeps cnt x slices within max(kHeavyItems, cnt), so on long-list
+// indexes max(kHeavyItems, n_queries), else one per query (C2); NGS_HEAVY_SLICES: n_queries x that
+// many. The first heavy launch takes the context's last item count instead (P.hgrid; C3: ~19k
+// where this bound is 65,536: the 46k workgroups that only exited cost 2.7 % of a step), and an
+// overflow launch the rest.
 uint32_t heavy_grid(const DevIndex& X, const SearchParams& P) {
     const uint64_t B = std::max<uint32_t>(P.n_queries, 1);
     uint64_t g = P.hslices ? B * std::min<uint32_t>(P.hslices, kHeavyMaxSlices)
@@ -4124,7 +4126,10 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
             const uint32_t g1s = std::min<uint32_t>(P.n_queries * std::max<uint32_t>(P.nslices, 1u),
                                                     std::min<uint32_t>(persistent_slots(kWaveWavesPerSimd), kTier1bGrid));
             const uint32_t gh = std::min<uint32_t>(P.n_queries, kHeavyGrid);  // (the heavy k_emit's grid)
-            const uint32_t ghl = heavy_grid(X, P);                            // the heavy lean launch's
+            // the heavy lean launch: as many workgroups as the context's last call had items (every item
+            // heavy_slices can make otherwise), the rest in an overflow launch
+            const uint32_t ghb = heavy_grid(X, P);
+            const uint32_t ghl = P.hgrid ? std::min(P.hgrid, ghb) : ghb;
             const uint32_t gfull = std::min<uint32_t>(P.n_queries, std::min<uint32_t>(persistent_slots(kWaveWavesPerSimd), kTier1bGrid));
             SearchParams PM = P, PHO = P;  // the main and the heavy hand-over launches
             PM.qhead = gcount + 8;
@@ -4164,6 +4169,7 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
                     // at a threshold the shortest lean query (n_min grams) passes with one hit
                     const uint32_t n_min = (X.n_short ? X.short_query_len : X.full_scan_len + 1) - X.gsz + 1;
                     const bool ones = kLeanOnes && (NGS_HEAVY_ONES_ALWAYS || (!X.rank_post && !(1.0f / (float)n_min < P.thr)));
+                    PH.hbase = 0;
                     if (ones)
                         hipLaunchKernelGGL((k_wave_lean<true, kLeanOnes, true, true>), dim3(ghl), dim3(64), 0, side, X, PH,
                                            qnorm, off, qm, out_n, out_k, out_s, list2, count2, stats, fb2, fbc2, heavy,
@@ -4172,6 +4178,20 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
                         hipLaunchKernelGGL((k_wave_lean<true, false, true, true>), dim3(ghl), dim3(64), 0, side, X, PH, qnorm,
                                            off, qm, out_n, out_k, out_s, list2, count2, stats, fb2, fbc2, heavy, hcount);
                     dbg_check(side, "k_wave_lean (heavy list)");
+                    if (ghl < ghb) {  // items past the first grid, if this call has more than the last
+                        PH.hbase = ghl;
+                        const uint32_t gov = std::min<uint32_t>(ghb - ghl, kHeavyOverflowGrid);
+                        if (ones)
+                            hipLaunchKernelGGL((k_wave_lean<true, kLeanOnes, true, true, true>), dim3(gov), dim3(64), 0,
+                                               side, X, PH, qnorm, off, qm, out_n, out_k, out_s, list2, count2, stats,
+                                               fb2, fbc2, heavy, hcount);
+                        else
+                            hipLaunchKernelGGL((k_wave_lean<true, false, true, true, true>), dim3(gov), dim3(64), 0, side,
+                                               X, PH, qnorm, off, qm, out_n, out_k, out_s, list2, count2, stats, fb2,
+                                               fbc2, heavy, hcount);
+                        dbg_check(side, "k_wave_lean (heavy list overflow)");
+                        PH.hbase = 0;
+                    }
                     hipLaunchKernelGGL(k_emit<true>, dim3((gh + kEmitWaves - 1) / kEmitWaves), dim3(64 * kEmitWaves), 0,
                                        side, X, PH, qnorm, off, qm, out_n, out_k, out_s, stats, heavy, hcount);
                     dbg_check(side, "k_emit (heavy list)");
