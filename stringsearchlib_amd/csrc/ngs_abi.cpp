@@ -301,9 +301,10 @@ struct Context {
         for (hipEvent_t e : piece_ev)
             if (e) hipEventDestroy(e);
         if (stream) hipStreamDestroy(stream);
-        if (side && side != stream) hipStreamDestroy(side);
+        if (side && side != stream && !side_shared) hipStreamDestroy(side);
         if (side2 && side2 != side && side2 != stream) hipStreamDestroy(side2);
     }
+    bool side_shared = false;  // side is the replica's (NGS_SHARED_SIDE)
 };
 
 // The side stream runs tier 1b on the heavy list beside tier 1a. At the highest priority
@@ -322,10 +323,10 @@ hipError_t make_side_stream(hipStream_t* s) {
 }
 
 // The full list's tier 1b (cmin 1, short search) runs on the side stream after the heavy list's
-// chain (NGS_SIDE2=1: on a third stream of its own). Two contexts in flight (ngsSearchDeviceAsync,
-// the pipelined host path) then use four streams, one per hardware queue (HIP's default of
-// four): with three per context, one context's main stream shared a queue with the other's
-// side work and waited behind it (a pipelined scoreBatch measured 2x slower that way).
+// chain (NGS_SIDE2=1: on a third stream of its own). With three streams per context, one context's
+// main stream shared a hardware queue (HIP's default is four, one of them the null stream's) with
+// the other's side work and waited behind it (a pipelined scoreBatch measured 2x slower that way);
+// the side stream is now also shared by the replica's contexts (kSharedSide, queue_search).
 hipError_t make_second_side(hipStream_t side, hipStream_t* s) {
     static const bool own = [] {
         const char* e = std::getenv("NGS_SIDE2");
@@ -353,6 +354,7 @@ struct Replica {
     std::mutex main_mu;
     hipEvent_t main_ev = nullptr;
     bool main_rec = false;
+    hipStream_t shared_side = nullptr;  // NGS_SHARED_SIDE: one side stream for every context (made under main_mu)
 
     // the index as the kernels of a search under `valid` see it (kt_flag for that set); false on a
     // HIP failure
@@ -382,6 +384,7 @@ struct Replica {
         pool.clear();
         hipSetDevice(device);
         if (main_ev) hipEventDestroy(main_ev);
+        if (shared_side) hipStreamDestroy(shared_side);
         for (void* p : owned) hipFree(p);
     }
 
@@ -1095,7 +1098,22 @@ int queue_search(Library& L, Replica& R, Context& c, const uint8_t* d_raw, const
     // main launch, and in order after it a call of 8,192 C3-like queries took 0.23 ms longer)
     const bool all_heavy = !((float)kHeavyCmin / (float)kWaveMaxGrams < thr);
     hipStream_t side = s, side2 = s;
+    // one side stream for all of the replica's contexts (NGS_SHARED_SIDE=0: one per context): two
+    // calls in flight then hold three streams beside the null stream, one per hardware queue at HIP's
+    // default of four; with a side stream per context, one context's main and side streams shared a
+    // queue and its tail waited behind its own heavy chain (C3 +1.0 %, six passes on two boxes;
+    // profiles/r05_s27_ab_hw_queues.txt)
+    static const bool shared_side = [] {
+        const char* e = std::getenv("NGS_SHARED_SIDE");
+        return e ? std::atoi(e) != 0 : kSharedSide;
+    }();
     if (B > one_stream_batch || !all_heavy) {
+        if (!c.side && shared_side) {
+            std::lock_guard<std::mutex> g(R.main_mu);
+            if (!R.shared_side && !HIP_CHECK(make_side_stream(&R.shared_side))) return -4;
+            c.side = c.side2 = R.shared_side;
+            c.side_shared = true;
+        }
         if (!c.side && !HIP_CHECK(make_side_stream(&c.side))) return -4;
         if (!c.side2 && !HIP_CHECK(make_second_side(c.side, &c.side2))) return -4;
         side = c.side;
