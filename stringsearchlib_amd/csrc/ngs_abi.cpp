@@ -224,6 +224,10 @@ struct Context {
     hipEvent_t join = nullptr, join2 = nullptr;
     hipEvent_t prep_ev = nullptr, lists_ev = nullptr;  // k_prep done (s), heavy / full lists merged (side)
     hipEvent_t in_ev = nullptr;   // ngsSearchDeviceAsync: the caller's stream up to the call
+    // d_stats needs no reset before the next call's k_prep (kPrepZero): k_prep zeroes the statistics
+    // and the path counts, k_lists the list counters after reading them; false until a call has
+    // queued both, and after a call that flagged *oflow
+    bool stats_clean = false;
     hipEvent_t ev[6] = {};
     hipEvent_t piece_ev[kBackPieces] = {};  // finish_host_chunk: the read-back's pieces landed
     size_t qcap = 0, bcap = 0, ncap = 0, ocap = 0;
@@ -1119,15 +1123,28 @@ int queue_search(Library& L, Replica& R, Context& c, const uint8_t* d_raw, const
         side = c.side;
         side2 = c.side2;
     }
-    // statistics, path counts and list counters
-    if (!small && !HIP_CHECK(hipMemsetAsync(c.d_stats, 0, sizeof(DevStats) * (kStatSlots + 1 + 2 * kListSlots), s)))
+    // statistics, path counts and list counters: reset by k_prep and k_lists when the context's last
+    // call left them so (the memset's fill kernel waited ~200 us for a workgroup slot behind the
+    // previous call's tail in the pipelined trace; NGS_PREP_ZERO=0: always the memset)
+    static const bool prep_zero = [] {
+        const char* e = std::getenv("NGS_PREP_ZERO");
+        return e ? std::atoi(e) != 0 : kPrepZero;
+    }();
+    const bool zero_in_prep = prep_zero && !small && c.stats_clean && P.waves == 0;
+    c.stats_clean = false;
+    if (zero_in_prep) {
+        P.zero_stats = reinterpret_cast<uint32_t*>(c.d_stats);
+        P.zero_words = (uint32_t)(kStatSlots * sizeof(DevStats) / sizeof(uint32_t));
+    } else if (!small && !HIP_CHECK(hipMemsetAsync(c.d_stats, 0, sizeof(DevStats) * (kStatSlots + 1 + 2 * kListSlots), s))) {
         return -4;
+    }
     if (timing) HIP_CHECK(hipEventRecord(c.ev[0], s));
     DevIndex X;
     if (!R.index_for(P.valid, X)) return -4;
     if (!HIP_CHECK(launch_prep(d_raw, d_off, B, P, c.d_norm, c.d_qm, X.csize, X, c.d_heavy, gc + 3, c.d_full,
                                gc + 5, c.d_lslots, c.d_lctr, s, side, c.prep_ev, c.lists_ev)))
         return -4;
+    c.stats_clean = !small && P.waves == 0;  // k_lists queued: it leaves the list counters zero
     if (timing) HIP_CHECK(hipEventRecord(c.ev[1], s));  // the end of k_prep is the start of the tier-1 phase
     // the main tier-1a launches of this replica's calls one after another (NGS_SERIAL_MAIN=0: not):
     // with two calls in flight the second call's main launch otherwise starts in the first one's and
@@ -1168,7 +1185,10 @@ int finish_search(Library& L, Replica& R, Context& c, uint32_t B, const SearchPa
     st.queries = B;
     // general, tier 2, tier 1a hand-overs, heavy, heavy hand-overs, full
     const uint32_t* counts3 = reinterpret_cast<const uint32_t*>(hst + kStatSlots);
-    if (counts3[6]) return kRetryQcap;  // a query past the normalised-query buffer: nothing is valid
+    if (counts3[6]) {  // (the rerun resets the path counts with the memset)
+        c.stats_clean = false;
+        return kRetryQcap;
+    }  // a query past the normalised-query buffer: nothing is valid
     const uint32_t ngen = counts3[0];
     if (ngen) {
         std::vector<uint32_t> gl(ngen);

@@ -218,6 +218,7 @@ constexpr uint32_t kHeavySliceList = 1024;      // ... on indexes of at least th
 constexpr uint32_t kHeavyOverflowGrid = 1024;   // ... the overflow launch's grid (items past the hinted grid)
 constexpr uint64_t kHeavySlicePostings = 3840;  // ... a slice per this many of the query's postings (~16 parts)
 constexpr bool kSidePriority = false;           // side streams at the highest priority (NGS_SIDE_PRIO; measured no faster)
+constexpr bool kPrepZero = true;               // k_prep / k_lists reset the statistics, not a memset (NGS_PREP_ZERO)
 constexpr bool kSharedSide = true;             // one side stream per replica, not per context (NGS_SHARED_SIDE)
 #ifndef NGS_SHRINK2
 #define NGS_SHRINK2 0

@@ -104,9 +104,11 @@ __global__ __launch_bounds__(64) void k_prep(const uint8_t* __restrict__ raw, co
     const uint32_t lane = threadIdx.x, gl = lane & 15u, sh = lane & 48u;
     const uint32_t q = blockIdx.x * 4 + (lane >> 4);
     const bool live = q < B;
-    if (P.zero_stats) {  // (the host sized qcap for the batch, so no block sets *oflow meanwhile)
+    if (P.zero_stats) {
         for (uint32_t i = blockIdx.x * 64 + lane; i < P.zero_words; i += gridDim.x * 64) P.zero_stats[i] = 0;
-        if (blockIdx.x == 0 && lane < 16) P.zero_stats[kStatSlots * 16 + lane] = 0;  // the path counts
+        // the path counts, but not word 6 (*oflow), which other blocks of this launch may set: the host
+        // resets it (it is zero unless a call reran for the query buffer)
+        if (blockIdx.x == 0 && lane < 16 && lane != 6) P.zero_stats[kStatSlots * 16 + lane] = 0;
     }
     const uint8_t* rq = raw;  // query q: characters of cs bytes from byte offset off[q]
     uint8_t* nq = qnorm;
@@ -4015,7 +4017,7 @@ int phase_stats(unsigned long long* out, int n, bool reset) {
 // One wave: it runs beside the main tier-1a launch, whose one-wave workgroups refill every wave slot
 // as they free up, so a larger workgroup (four free slots on one CU at once) waited ~1.2 ms for
 // room at C3 and held back the heavy list's launch behind it.
-__global__ __launch_bounds__(64) void k_lists(const uint32_t* __restrict__ slots, const uint32_t* __restrict__ ctr,
+__global__ __launch_bounds__(64) void k_lists(const uint32_t* __restrict__ slots, uint32_t* __restrict__ ctr,
                                               uint32_t cap, uint32_t* __restrict__ heavy, uint32_t* __restrict__ hcount,
                                               uint32_t* __restrict__ full, uint32_t* __restrict__ fcount) {
     __shared__ uint32_t base[2 * (kListSlots + 1)];
@@ -4023,6 +4025,7 @@ __global__ __launch_bounds__(64) void k_lists(const uint32_t* __restrict__ slots
 #pragma unroll
     for (uint32_t L = 0; L < 2; ++L) {  // 0: heavy slots, 1: full slots
         const uint32_t c = ctr[16 * (L * kListSlots + lane)];
+        ctr[16 * (L * kListSlots + lane)] = 0;  // zero again for the context's next call (kPrepZero)
         const uint32_t incl = wave_incl_scan(c);
         base[L * (kListSlots + 1) + lane + 1] = incl;
         if (lane == 0) base[L * (kListSlots + 1)] = 0;

@@ -232,7 +232,10 @@ def test_device_api_query_buffer_grows():
 
     small = ssl.synth.gen_queries(words, 1, 50, rng)
     big = ssl.synth.gen_queries(words, 1, 200, rng) * 40 + [b"x" * 70000]  # > the first 64 KB buffer
-    for qs in (small, big, small):
+    bigger = big + [b"y" * 400000]  # past the grown buffer too
+    # (k_prep resets the statistics of a context whose last call left them clean, kPrepZero: a rerun
+    # must leave them clean for the calls after it)
+    for qs in (small, big, small, big, bigger, small):
         got = run(qs)
         host = gi.score_batch(qs, 0.3, limit)
         for i, h in enumerate(host):
