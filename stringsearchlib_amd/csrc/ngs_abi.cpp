@@ -260,6 +260,9 @@ struct Context {
     uint32_t* d_at = nullptr;
     uint8_t* d_ac = nullptr;
     uint32_t ablocks = 0, arena_grow = 0;
+    // arena_calm: calls in a row that used under a quarter of a grown arena (kCalmCalls: halved);
+    // arena_off: calls left to run without an arena after its allocation failed
+    uint32_t arena_calm = 0, arena_off = 0, arena_shrink_to = 0;
     uint32_t heavy_items = 0;      // (query, slice) items of the last call's heavy launch (SearchParams.hgrid)
     size_t eorows = 0;
     uint64_t* d_prec = nullptr;    // sliced tier 1b: top-L records per (query, slice)
@@ -917,20 +920,43 @@ bool ensure_arena(Context& c, size_t B) {
         const char* e = std::getenv("NGS_ARENA_INIT");
         return e ? std::max<uint32_t>(1, (uint32_t)std::strtoul(e, nullptr, 0)) : kArenaInit;
     }();
-    const uint32_t want = std::max<uint32_t>({init, c.ablocks, c.arena_grow});
-    if (!c.d_eovf || B > c.eorows) {
+    if (!c.d_eovf || B > c.eorows) {  // the first-block words (also the heavy slices' words): required
         if (c.d_eovf) { hipFree(c.d_eovf); c.d_eovf = nullptr; }
         const size_t nb = std::max<size_t>(B, 1024);
         if (!dev_alloc(&c.d_eovf, nb)) return false;
         c.eorows = nb;
     }
-    if (!c.d_at || want > c.ablocks) {
+    auto free_arena = [&c] {
         for (void** p : {(void**)&c.d_anext, (void**)&c.d_at, (void**)&c.d_ac})
             if (*p) { hipFree(*p); *p = nullptr; }
         c.ablocks = 0;
-        if (!dev_alloc(&c.d_anext, want) || !dev_alloc(&c.d_at, (size_t)want * kArenaBlock) ||
-            !dev_alloc(&c.d_ac, (size_t)want * kArenaBlock))
-            return false;
+    };
+    if (c.arena_shrink_to && c.arena_shrink_to < c.ablocks) {  // a grown arena left unused (finish_search)
+        free_arena();
+        c.arena_grow = c.arena_shrink_to;
+    }
+    c.arena_shrink_to = 0;
+    // The arena is optional: the kernels run without one (SearchParams.at null; a query past its slots
+    // goes to tier 1b). An allocation that fails leaves the call without it, drops the grown size and
+    // waits kCalmCalls calls before trying again, so one out-of-memory event does not fail every later
+    // call of the context.
+    if (c.arena_off) {
+        --c.arena_off;
+        return true;
+    }
+    const uint32_t want = std::max<uint32_t>({init, c.ablocks, c.arena_grow});
+    if (!c.d_at || want > c.ablocks) {
+        free_arena();
+        // plain hipMalloc, not dev_alloc: a refused arena is not an error of the call
+        if (hipMalloc((void**)&c.d_anext, (size_t)want * sizeof(uint32_t)) != hipSuccess ||
+            hipMalloc((void**)&c.d_at, (size_t)want * kArenaBlock * sizeof(uint32_t)) != hipSuccess ||
+            hipMalloc((void**)&c.d_ac, (size_t)want * kArenaBlock) != hipSuccess) {
+            (void)hipGetLastError();
+            free_arena();
+            c.arena_grow = 0;
+            c.arena_off = kCalmCalls;
+            return true;
+        }
         c.ablocks = want;
     }
     return true;
@@ -1049,9 +1075,9 @@ int queue_search(Library& L, Replica& R, Context& c, const uint8_t* d_raw, const
     if (!small) {  // (the latency path runs tier 1b alone: no tier-1a survivors)
         if (!ensure_arena(c, B)) return -4;
         P.eovf = c.d_eovf;
-        P.anext = c.d_anext;
-        P.at = c.d_at;
-        P.ac = c.d_ac;
+        P.anext = c.ablocks ? c.d_anext : nullptr;
+        P.at = c.ablocks ? c.d_at : nullptr;  // null: no arena this call (ensure_arena)
+        P.ac = c.ablocks ? c.d_ac : nullptr;
         P.ablocks = c.ablocks;
         P.actr = gc + kArenaCtrWord;
     }
@@ -1242,6 +1268,15 @@ int finish_search(Library& L, Replica& R, Context& c, uint32_t B, const SearchPa
         const uint64_t want = std::max<uint64_t>(3ull * P.ablocks / 2, 5ull * need / 4);
         const uint64_t cap = kArenaBudget / ((uint64_t)kArenaBlock * (sizeof(uint32_t) + sizeof(uint8_t)));
         c.arena_grow = (uint32_t)std::min<uint64_t>(want, cap);
+        c.arena_calm = 0;
+    } else if (!small && P.at && P.ablocks > kArenaInit && (uint64_t)arena_used * 4 < P.ablocks) {
+        // a grown arena mostly unused for kCalmCalls calls in a row: halved (as the survivor slots)
+        if (++c.arena_calm >= kCalmCalls) {
+            c.arena_calm = 0;
+            c.arena_shrink_to = std::max<uint32_t>(kArenaInit, P.ablocks / 2);
+        }
+    } else if (!small) {
+        c.arena_calm = 0;
     }
     if (!small && !arena_out) {
         if (slot_full * 64 > B) {
@@ -1666,10 +1701,11 @@ bool host_normalise(const uint32_t* valid, const char* q, uint8_t* out, uint32_t
 // the server routes to tier 2 or the general path, or a server that cannot be reached).
 bool serve_query(Library& L, const char* query, float thr, uint32_t limit, std::vector<uint32_t>& keys,
                  std::vector<float>& sc) {
-    // one request in flight (ngsServe(0) waits for it); a caller that finds the server busy with
-    // another thread's request takes the regular path instead of waiting
-    std::unique_lock<std::mutex> g(L.server_mu, std::try_to_lock);
-    if (!g.owns_lock() || L.batches.load(std::memory_order_acquire) > 0) return false;
+    // one request in flight (ngsServe(0) waits for it). A caller that finds the server busy with
+    // another thread's request waits its turn (~12 us): taking the regular path instead would stop
+    // the server for every contended call, and relaunch it on the next
+    std::unique_lock<std::mutex> g(L.server_mu);
+    if (L.batches.load(std::memory_order_acquire) > 0) return false;
     Server* sv = L.server.get();
     const uint32_t Lm = effective_limit(L, limit);
     Replica& R = *L.reps.front();
@@ -1777,9 +1813,9 @@ uint32_t one_query(uint32_t handle, const CharT* query, CharT*** results, float*
     if (sizeof(CharT) == 1 && !L->serving.load(std::memory_order_acquire)) maybe_auto_serve(*L);
     if (sizeof(CharT) == 1 && L->serving.load(std::memory_order_acquire) && serve_query(*L, reinterpret_cast<const char*>(query), thr, limit, keys, sc))
         return marshal(*L, keys, sc, results, scores);
-    // the regular path's kernels while a server exists (it was busy with another thread's request,
-    // or cannot take this query): stop it first, since its stream may share a hardware queue with
-    // ours and a resident server would hold our launches until its idle exit
+    // the regular path's kernels while a server exists (it cannot take this query: a limit past the
+    // wave search's, tier 2 or the general path): stop it first, since its stream may share a
+    // hardware queue with ours and a resident server would hold our launches until its idle exit
     BatchGuard bg(L->serving.load(std::memory_order_acquire) ? L : nullptr);
     if (!host_search(*L, &query, 1, thr, limit, counts, keys, sc)) return 0;
     return marshal(*L, keys, sc, results, scores);

@@ -31,3 +31,20 @@ def test_arena_holds_survivors_past_the_slots():
     assert s[2]["arena_used"] > 0 and s[2]["arena_used"] <= s[2]["arena_blocks"], s
     assert s[2]["slot_full_queries"] == 0, s
     assert s[3]["arena_used"] > 0 and s[3]["slot_full_queries"] == 0, s
+    assert r["promoted"] == r["exact"], r  # every exact-key query answered with its key promoted to 100
+
+
+def test_arena_allocation_failure_leaves_the_context_working():
+    """An arena too large to allocate (NGS_ARENA_INIT of 2^30 blocks, 5 TB) is not an error of the call
+    (ADVICE r5): the calls run without one, the queries past their slots go to tier 1b, every answer
+    stays exact, and later calls on the same context keep working."""
+    env = dict(os.environ, NGS_ECAP_INIT="256", NGS_ARENA_INIT=str(1 << 30))
+    child = os.path.join(os.path.dirname(os.path.abspath(__file__)), "arena_child.py")
+    p = subprocess.run([sys.executable, child], env=env, capture_output=True, text=True, timeout=400)
+    assert p.returncode == 0, p.stderr[-3000:]
+    r = json.loads(p.stdout.strip().splitlines()[-1])
+    assert not r["fails"], "\n".join(r["fails"])
+    s = r["stats"]
+    assert all(x["arena_blocks"] == 0 for x in s[:3]), s
+    assert s[0]["slot_full_queries"] > 0, s  # the overflowing queries went to tier 1b
+    assert r["promoted"] == r["exact"], r
