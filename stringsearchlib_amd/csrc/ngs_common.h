@@ -164,9 +164,6 @@ constexpr bool kSketchLoose = NGS_SKETCH_LOOSE != 0;
 #ifndef NGS_LEAN_DEFER_SKIP
 #define NGS_LEAN_DEFER_SKIP 0  // 1: tier 1a issues the next skip-table read after the part's loads (1 % slower)
 #endif
-#ifndef NGS_LEAN_PIPE2
-#define NGS_LEAN_PIPE2 0  // 1: tier-1a part loop unrolled by two over swapping buffers (two parts in flight)
-#endif
 #ifndef NGS_LEAN_GROUPS
 #define NGS_LEAN_GROUPS 1  // tier 1a staging by fixed lane groups per list (lean_query_g) in the main launch; 0: packed (lean_stage)
 #endif

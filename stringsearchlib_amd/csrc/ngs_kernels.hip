@@ -2656,7 +2656,9 @@ __device__ __forceinline__ uint32_t lean_sketch_g(WaveSmem<1, true>& S, const ui
             for (uint32_t e = 0; e < 4; ++e) {
                 bool f = __builtin_amdgcn_ubfe(w[e], sketch_sh4<1, true>(t[e]), 4u) >= cmin;
                 if (__ballot(f)) {  // rare: the entry's segment bounds (and chunks not loaded) only here
-                    f = f && 4u * (k0 + r * G) + e - head < len;
+                    uint32_t kk = k0;  // opaque: the round's entry offset is made here, not kept across the part loop
+                    asm volatile("" : "+v"(kk));
+                    f = f && 4u * (kk + r * G) + e - head < len;
                     const unsigned long long b = __ballot(f);
                     const uint32_t pos = nw + rank_below(b);
                     if (f && pos < 64u) S.cbuf[pos] = t[e];
@@ -3100,14 +3102,12 @@ __device__ __forceinline__ void lean_query_g(WaveSmem<1, true>& S, const uint32_
 #ifdef NGS_PHASE_STAMPS
         uint32_t last_nc = 0;  // candidates of the last part counted (phase statistics)
 #endif
-        // on_fail runs first on a path that returns false (PIPE2: the other buffer's loads waited for
-        // inside the loop body, before the loop's exits merge)
-        auto count = [&](const uint4 (&v)[kDmaRounds], const PartGroups& ps, auto&& on_fail) -> bool {
+        auto count = [&](const uint4 (&v)[kDmaRounds], const PartGroups& ps) -> bool {
             if (surv_n + 64 > (uint32_t)kWaveSurv) {
                 if (!__builtin_amdgcn_readfirstlane(spill() ? 1u : 0u)) {  // (uniform: no exec-masked exit)
-                    on_fail();
                     slot_full();
-                    arena_need((uint32_t)wave_sum((uint64_t)(has && k0 == 0 ? cur : 0u)));
+                    // (DPP sum: a shuffle sum's lane-index vectors would be hoisted out of the part loop)
+                    arena_need(wave_sum_u32(has && k0 == 0 ? cur : 0u));
                     return false;
                 }
                 wave_sync();  // the list is read before it is refilled
@@ -3125,150 +3125,8 @@ __device__ __forceinline__ void lean_query_g(WaveSmem<1, true>& S, const uint32_
 #ifdef NGS_PHASE_STAMPS
             last_nc = nc;
 #endif
-            if (__builtin_amdgcn_readfirstlane(nc) > 64) {  // a wrapped counter or too many candidates
-                on_fail();
-                return false;
-            }
-            return true;
+            return __builtin_amdgcn_readfirstlane(nc) <= 64;  // above: a wrapped counter or too many candidates
         };
-#if NGS_LEAN_PIPE2
-        // two register buffers that swap roles (the loop unrolled by two): part i+1's loads are issued
-        // before part i is waited for, so a wave has two parts in flight. Every part issues exactly
-        // kDmaRounds loads and one skip-table read, on every lane and with no branch around them, so
-        // the compiler's wait for part i is vmcnt(loads issued since), not vmcnt(0)
-        // plan with one skip-table read, at its end and on every lane (the next group's end for the
-        // fast path of the next call); the slow paths read the ends they need themselves and wait
-        auto end_at = [&](uint32_t bn) -> uint32_t { return X.skip[has ? skrow + min(Kend, bn + w) : 0u]; };
-        auto plan2 = [&](uint32_t& nch, uint32_t& len) -> bool {
-            bool have_p = false;
-            in_sub = __builtin_amdgcn_readfirstlane(in_sub);
-            bnext = __builtin_amdgcn_readfirstlane(bnext);
-            uint32_t e_cur = e_pre;  // end of the group from bnext (valid while !in_sub)
-            bool fast = false;
-            if (!in_sub && bnext < Kend) {  // common case, straight-line: the next bucket group fits
-                const uint32_t e = has ? e_cur : cur;
-                nch = chunks(cur, e);
-                if (!__ballot(nch > capc) && __ballot(nch != 0)) {
-                    len = e - cur;
-                    bnext = min(Kend, bnext + w);
-                    have_p = fast = true;
-                }
-            }
-            if (!fast) {
-                for (;;) {
-                    guard = __builtin_amdgcn_readfirstlane(guard);
-                    bnext = __builtin_amdgcn_readfirstlane(bnext);
-                    sub_lo = __builtin_amdgcn_readfirstlane(sub_lo);
-                    step = __builtin_amdgcn_readfirstlane(step);
-                    if (++guard > 8u * K + 4096u) {
-                        atomicOr(err, 4u);  // every lane (idempotent)
-                        break;
-                    }
-                    if (!in_sub) {
-                        if (bnext >= Kend) break;
-                        const uint32_t bhi = min(Kend, bnext + w), e = has ? e_cur : cur;
-                        nch = chunks(cur, e);
-                        if (!__ballot(nch > capc)) {
-                            len = e - cur;
-                            bnext = bhi;
-                            if (__ballot(nch != 0)) { have_p = true; break; }
-                            e_cur = end_at(bnext);
-                            asm volatile("" ::"v"(e_cur));  // waited here: the loop header sees no pending read
-                            continue;
-                        }
-                        in_sub = 1;  // the group is over a list's cap: term-id sub-ranges of it
-                        sub_lo = bnext * span;
-                        hi_lim = (uint32_t)min64((uint64_t)bhi * span, n_long);
-                        sub_end = e;
-                        sub_bnext = bhi;
-                        step = (uint32_t)max64(1, min64((uint64_t)(hi_lim - sub_lo) * 192u / fill(nch), kMaxPartSpan));
-                    }
-                    const uint32_t hi = (uint32_t)min64(hi_lim, (uint64_t)sub_lo + step);
-                    uint32_t a = cur, b = has ? sub_end : cur;
-                    while (__ballot(a < b)) {
-                        const bool act = a < b;
-                        const uint32_t mid = (a + b) >> 1;
-                        uint32_t pvv = 0;
-                        if (act) pvv = X.post[((uint64_t)cb << 2) + a0 + mid];  // (the list's base, not kept)
-                        const bool below = pvv < hi;
-                        a = act && below ? mid + 1 : a;
-                        b = act && !below ? mid : b;
-                    }
-                    nch = has ? chunks(cur, a) : 0u;
-                    if (__ballot(nch > capc) && hi - sub_lo > 1) {
-                        step = max(1u, (uint32_t)((uint64_t)(hi - sub_lo) * 192u / fill(nch)));
-                        continue;
-                    }
-                    len = has ? a - cur : 0u;
-                    sub_lo = hi;
-                    if (sub_lo >= hi_lim) {
-                        in_sub = 0;
-                        bnext = sub_bnext;
-                        e_cur = end_at(bnext);
-                        asm volatile("" ::"v"(e_cur));
-                    }
-                    if (__ballot(nch != 0)) { have_p = true; break; }
-                    cur = a;
-                }
-            }
-            e_pre = end_at(__builtin_amdgcn_readfirstlane(bnext));  // the one read the next call's fast path waits for
-            return __builtin_amdgcn_readfirstlane(have_p ? 1u : 0u) != 0;
-        };
-        // a staged part's per-lane state in one register: chunks (8 bits), head (2), entries (12); R in an SGPR
-        struct PartPacked {
-            uint32_t w, R;
-        };
-        auto stage2 = [&](uint4 (&v)[kDmaRounds], PartPacked& ps, uint32_t nch, uint32_t len) {
-            const uint32_t R = 1u + (__ballot(nch > G) ? 1u : 0u) + (__ballot(nch > 2u * G) ? 1u : 0u);
-            const uint32_t head = (a0 + cur) & 3u;
-            const uint32_t first = cb + ((a0 + cur) >> 2);
-#pragma unroll
-            for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) {
-                const uint32_t k = k0 + r * G;
-                v[r] = post4[k < nch ? first + k : first];  // past the segment: a chunk the part reads anyway
-            }
-            ps.w = nch | head << 8 | len << 10;
-            ps.R = R;
-            cur += len;
-        };
-        auto count2 = [&](const uint4 (&v)[kDmaRounds], const PartPacked& pp, auto&& on_fail) -> bool {
-            const PartGroups ps{pp.w & 0xFFu, (pp.w >> 8) & 3u, pp.w >> 10, pp.R};
-            return count(v, ps, on_fail);
-        };
-        uint4 va[kDmaRounds], vb[kDmaRounds];
-        PartPacked pa{}, pb{};
-        // a buffer's loads waited for where the loop ends: no path out of it leaves loads pending in
-        // registers that the code after it (or the structurizer's merge blocks) may reuse
-        auto drain = [](const uint4 (&v)[kDmaRounds]) {
-#pragma unroll
-            for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) asm volatile("" ::"v"(v[r].x), "v"(v[r].y), "v"(v[r].z), "v"(v[r].w));
-        };
-        {
-            uint32_t nch = 0, len = 0;
-            const bool hp = plan2(nch, len);
-            stage2(va, pa, hp ? nch : 0u, hp ? len : 0u);
-            pa.R = hp ? pa.R : 0u;
-        }
-        if (!pa.R) drain(va);
-        while (pa.R) {
-            {
-                uint32_t nch = 0, len = 0;
-                const bool hp = plan2(nch, len);
-                stage2(vb, pb, hp ? nch : 0u, hp ? len : 0u);  // loads even past the last part (no branch)
-                pb.R = hp ? pb.R : 0u;
-                if (!count2(va, pa, [&] { drain(vb); })) { bail(); return; }  // part i while part i+1 is in flight
-            }
-            if (!pb.R) { drain(vb); break; }
-            {
-                uint32_t nch = 0, len = 0;
-                const bool hp = plan2(nch, len);
-                stage2(va, pa, hp ? nch : 0u, hp ? len : 0u);
-                pa.R = hp ? pa.R : 0u;
-                if (!count2(vb, pb, [&] { drain(va); })) { bail(); return; }
-            }
-            if (!pa.R) { drain(va); break; }
-        }
-#else
         // software pipeline in registers: part i+1's loads are in flight while part i is counted
         uint4 pv[kDmaRounds];
         PartGroups ps{};
@@ -3284,7 +3142,7 @@ __device__ __forceinline__ void lean_query_g(WaveSmem<1, true>& S, const uint32_
             WSTAMP(2);
             if (hp) stage(pv, ps, nch, len);
             WSTAMP(4);
-            if (cs.R && !count(cv, cs, [] {})) { bail(); return; }  // count part i while part i+1 is in flight
+            if (cs.R && !count(cv, cs)) { bail(); return; }  // count part i while part i+1 is in flight
             WSTAMP(5);
             WCOUNT(11, cs.R ? 1 : 0);
             WCOUNT(13, cs.R);
@@ -3293,7 +3151,6 @@ __device__ __forceinline__ void lean_query_g(WaveSmem<1, true>& S, const uint32_
             ps.R = hp ? ps.R : 0u;
             if (!hp) break;
         }
-#endif
     }
     if (!spill()) {
         slot_full();
