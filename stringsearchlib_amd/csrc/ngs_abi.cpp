@@ -180,6 +180,76 @@ void parallel_ranges(size_t n, size_t serial_below, F&& body) {
     pool.run(nt, task);
 }
 
+// Persistent host threads for the parts of a batch split over replicas (dllmain.cpp:82-90 callers
+// on an index placed on several devices): part 0 runs on the calling thread, part i on worker i - 1,
+// each on its replica's device and contexts. One split at a time; a call that finds the workers
+// busy (another thread's split) spawns threads of its own for that call.
+class PartWorkers {
+  public:
+    explicit PartWorkers(size_t n) : n_(n), todo_(n, false) {
+        for (size_t i = 0; i < n; ++i) th_.emplace_back([this, i] { loop(i); });
+    }
+    ~PartWorkers() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            quit_ = true;
+        }
+        work_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    size_t size() const { return n_; }
+    // f(i) for i in [0, parts): i = 0 here, the rest on the workers; false if busy (nothing ran)
+    bool try_run(size_t parts, const std::function<void(size_t)>& f) {
+        std::unique_lock<std::mutex> call(call_mu_, std::try_to_lock);
+        if (!call.owns_lock() || parts > n_ + 1) return false;
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            f_ = &f;
+            left_ = parts - 1;
+            for (size_t i = 0; i + 1 < parts; ++i) todo_[i] = true;
+        }
+        work_.notify_all();
+        f(0);
+        std::unique_lock<std::mutex> lk(mu_);
+        done_.wait(lk, [&] { return left_ == 0; });
+        f_ = nullptr;
+        return true;
+    }
+
+  private:
+    void loop(size_t i) {
+        std::unique_lock<std::mutex> lk(mu_);
+        for (;;) {
+            work_.wait(lk, [&] { return quit_ || todo_[i]; });
+            if (quit_) return;
+            todo_[i] = false;
+            const std::function<void(size_t)>* f = f_;
+            lk.unlock();
+            (*f)(i + 1);
+            lk.lock();
+            if (--left_ == 0) done_.notify_all();
+        }
+    }
+    size_t n_;
+    std::vector<char> todo_;
+    std::vector<std::thread> th_;
+    std::mutex mu_, call_mu_;
+    std::condition_variable work_, done_;
+    const std::function<void(size_t)>* f_ = nullptr;
+    size_t left_ = 0;
+    bool quit_ = false;
+};
+
+// f(i) for the parts of a split: on the library's persistent workers, or threads of this call's own
+template <class Workers>
+void run_parts(Workers& w, size_t parts, const std::function<void(size_t)>& f) {
+    if (w && w->try_run(parts, f)) return;
+    std::vector<std::thread> th;
+    for (size_t i = 1; i < parts; ++i) th.emplace_back(f, i);
+    f(0);
+    for (auto& t : th) t.join();
+}
+
 template <class T>
 bool dev_alloc(T** p, size_t n) {
     *p = nullptr;
@@ -513,6 +583,9 @@ struct Library {
     uint32_t w_uniform = 0;
     // DevIndex.kt_off / kt_term (keys with several pairs), built once in upload() for every replica
     std::vector<uint32_t> kt_off, kt_term;
+    // the replicas a batch is split over (upload), and host threads for its parts past the first
+    std::vector<uint32_t> split;
+    std::unique_ptr<PartWorkers> workers;
 
     // ngsSearchDeviceAsync calls in flight: their context stays out of the pool until
     // ngsSearchDeviceWait (the general path and the statistics need the host afterwards)
@@ -533,6 +606,7 @@ struct Library {
     uint64_t next_ticket = 1;
 
     ~Library() {
+        workers.reset();  // (idle: dispose holds the exclusive lock, so no split is running)
         server.reset();  // stops the kernel before the index it reads is freed
         for (auto& kv : pending)  // dispose: nothing may still run on the buffers freed below
             if (kv.second.c) hipStreamSynchronize(kv.second.c->stream);
@@ -820,6 +894,21 @@ bool upload(Library& L, const std::vector<int>& devs) {
         }
     }
     L.device = devs.front();
+    // the replicas a batch is split over: the first one on each device (NGS_SPLIT_SAME_DEVICE=1, a
+    // test hook for one-GPU boxes: every replica). Two replicas on one device add no compute, and
+    // their halves' streams share the device's hardware queues: at C3 a forced split ran 1.34x one
+    // replica's time (profiles/r06_s2_dropin_replicas.txt)
+    static const bool same_dev = [] {
+        const char* e = std::getenv("NGS_SPLIT_SAME_DEVICE");
+        return e && std::atoi(e) != 0;
+    }();
+    L.split.clear();
+    for (size_t i = 0; i < L.reps.size(); ++i) {
+        bool first = true;
+        for (size_t j = 0; j < i && !same_dev; ++j) first &= L.reps[j]->device != L.reps[i]->device;
+        if (first) L.split.push_back((uint32_t)i);
+    }
+    if (L.split.size() > 1) L.workers = std::make_unique<PartWorkers>(L.split.size() - 1);
     free_uploaded(L.host);
     std::vector<uint32_t>().swap(L.kt_off);
     std::vector<uint32_t>().swap(L.kt_term);
@@ -1524,6 +1613,17 @@ bool finish_host_chunk(Library& L, Replica& R, HostChunk& h, uint32_t Lm, std::v
 constexpr uint32_t kPipeChunks = 1;  // measured: 4 chunks 6.1-6.6 ms against 4.4-4.6 for one at C3
 constexpr uint32_t kPipeMinChunk = 8192;
 
+// Queries per chunk of a host batch of nq queries at limit Lm: the outputs within kOutBudget and
+// sliced tier 1b's partial results within kPartBudget
+size_t host_chunk(uint32_t nq, uint32_t Lm) {
+    const size_t stride = std::max<uint32_t>(Lm, 1);
+    size_t max_chunk = std::max<size_t>(1, std::min<size_t>(1 << 20, kOutBudget / (stride * 8)));
+    if (Lm <= kWaveMaxLimit)  // sliced tier 1b's partial results fit the budget
+        max_chunk = std::max<size_t>(1, std::min<size_t>(max_chunk, kPartBudget / (sizeof(uint64_t) * kSlices * stride)));
+    const size_t want = std::max<size_t>(kPipeMinChunk, (nq + kPipeChunks - 1) / kPipeChunks);
+    return std::min(max_chunk, want);
+}
+
 // Scores n queries (characters of the index's width) on one replica; fills counts and hands
 // each chunk's records, in query order, to emit(keys, scores, n).
 template <typename CharT, class Emit>
@@ -1532,16 +1632,7 @@ bool host_search_chunks(Library& L, Replica& R, const CharT* const* queries, uin
     counts.assign(nq, 0);
     if (Lm == 0 || nq == 0) return true;
     if (!HIP_CHECK(hipSetDevice(R.device))) return false;
-    const size_t stride = Lm;
-    size_t max_chunk = std::max<size_t>(1, std::min<size_t>(1 << 20, kOutBudget / (stride * 8)));
-    if (Lm <= kWaveMaxLimit)  // sliced tier 1b's partial results fit the budget
-        max_chunk = std::max<size_t>(1, std::min<size_t>(max_chunk, kPartBudget / (sizeof(uint64_t) * kSlices * Lm)));
-    static const uint32_t pipe_chunks = [] {  // NGS_PIPE_CHUNKS=1: one chunk (no pipelining)
-        const char* e = std::getenv("NGS_PIPE_CHUNKS");
-        return e ? std::max<uint32_t>(1, (uint32_t)std::strtoul(e, nullptr, 0)) : kPipeChunks;
-    }();
-    const size_t want = std::max<size_t>(kPipeMinChunk, (nq + pipe_chunks - 1) / pipe_chunks);
-    const size_t chunk = std::min(max_chunk, want);
+    const size_t chunk = host_chunk(nq, Lm);
     const uint32_t n_chunks = (uint32_t)((nq + chunk - 1) / chunk);
     std::unique_ptr<Context> ctx[2];
     ctx[0] = R.acquire();
@@ -1601,7 +1692,7 @@ template <typename CharT>
 bool host_search(Library& L, const CharT* const* queries, uint32_t nq, float thr, uint32_t limit,
                  std::vector<uint32_t>& counts, std::vector<uint32_t>& keys, std::vector<float>& scores) {
     const uint32_t Lm = effective_limit(L, limit);
-    const size_t nrep = L.reps.size();
+    const size_t nrep = std::max<size_t>(L.split.size(), 1);
     const uint32_t parts = (uint32_t)std::min<uint64_t>(nrep, std::max<uint64_t>(1, nq / split_min()));
     if (parts <= 1) return host_search_one(L, *L.reps.front(), queries, nq, thr, Lm, counts, keys, scores);
     const uint32_t per = (nq + parts - 1) / parts;
@@ -1609,16 +1700,14 @@ bool host_search(Library& L, const CharT* const* queries, uint32_t nq, float thr
     std::vector<std::vector<float>> ps(parts);
     std::vector<char> pok(parts, 0);
     std::vector<int> perr(parts, 0);  // each worker's ngsLastError, handed to the caller's thread
-    std::vector<std::thread> th;
-    for (uint32_t i = 0; i < parts; ++i) {
-        const uint32_t q0 = i * per, n = std::min(per, nq - std::min(nq, q0));
-        th.emplace_back([&, i, q0, n] {
-            t_last_error = 0;
-            pok[i] = host_search_one(L, *L.reps[i], queries + q0, n, thr, Lm, pc[i], pk[i], ps[i]);
-            perr[i] = pok[i] ? 0 : (t_last_error ? t_last_error : kErrInternal);
-        });
-    }
-    for (auto& t : th) t.join();
+    const int err0 = t_last_error;
+    run_parts(L.workers, parts, [&](size_t i) {
+        const uint32_t q0 = (uint32_t)i * per, n = std::min(per, nq - std::min(nq, q0));
+        t_last_error = 0;
+        pok[i] = host_search_one(L, *L.reps[L.split[i]], queries + q0, n, thr, Lm, pc[i], pk[i], ps[i]);
+        perr[i] = pok[i] ? 0 : (t_last_error ? t_last_error : kErrInternal);
+    });
+    t_last_error = err0;
     for (uint32_t i = 0; i < parts; ++i)
         if (perr[i]) t_last_error = perr[i];
     counts.clear();
@@ -1821,6 +1910,90 @@ uint32_t one_query(uint32_t handle, const CharT* query, CharT*** results, float*
     return marshal(*L, keys, sc, results, scores);
 }
 
+// A batch split over the replicas with the one-replica path's pointer mode (dllmain.cpp:82-90 over
+// several devices): each replica's part packs its records on its device as result pointers, the
+// parts publish their record counts, the last one allocates the caller's arrays at the exact total,
+// and every part copies its records into its own slice of them straight from its pinned read-back.
+// kNoDirect: a part would take several chunks (the caller's general path then joins vectors).
+constexpr uint32_t kNoDirect = 0xFFFFFFFFu;
+template <typename CharT>
+uint32_t split_direct(Library& L, const CharT* const* queries, uint32_t nq, float thr, uint32_t Lm, uint32_t* counts,
+                      CharT*** results, float** scores) {
+    const uint32_t parts = (uint32_t)std::min<uint64_t>(L.split.size(), std::max<uint64_t>(1, nq / split_min()));
+    const uint32_t per = (nq + parts - 1) / parts;
+    if (parts < 2 || host_chunk(per, Lm) < per || (uint64_t)nq * Lm > kDirectMax) return kNoDirect;
+    const uint64_t pbase = (uint64_t)(uintptr_t)L.host.key_bytes.data();
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<uint64_t> total(parts, 0), base(parts, 0);
+    uint32_t known = 0;
+    bool failed = false, ready = false;
+    CharT** res = nullptr;
+    float* out_s = nullptr;
+    // part i knows its record count: the last part to know allocates the arrays for everyone
+    auto publish = [&](uint32_t i, uint64_t n, bool fail) {
+        std::unique_lock<std::mutex> lk(mu);
+        total[i] = n;
+        failed |= fail;
+        if (++known == parts) {
+            uint64_t sum = 0;
+            for (uint32_t j = 0; j < parts; ++j) base[j] = sum, sum += total[j];
+            if (!failed) {
+                res = new CharT*[std::max<uint64_t>(sum, 1)];
+                out_s = scores ? new float[std::max<uint64_t>(sum, 1)] : nullptr;
+            }
+            ready = true;
+            cv.notify_all();
+        } else {
+            cv.wait(lk, [&] { return ready; });
+        }
+    };
+    std::vector<std::vector<uint32_t>> pc(parts);
+    std::vector<int> perr(parts, 0);
+    const int err0 = t_last_error;
+    run_parts(L.workers, parts, [&](size_t pi) {
+        const uint32_t i = (uint32_t)pi, q0 = i * per, n = std::min(per, nq - std::min(nq, q0));
+        t_last_error = 0;
+        bool seen = false;
+        size_t off = 0;
+        const bool ok = host_search_chunks(L, *L.reps[L.split[i]], queries + q0, n, thr, Lm, pc[i],
+                                           [&](const void* recs, const float* sc, uint32_t m, bool, uint32_t chunk_total) {
+            if (!seen) {  // (one chunk: its total is the part's)
+                seen = true;
+                publish(i, chunk_total, false);
+            }
+            if (!res) return;  // another part failed
+            const uint64_t* p = static_cast<const uint64_t*>(recs);
+            CharT** dst = res + base[i] + off;
+            float* dsc = out_s ? out_s + base[i] + off : nullptr;
+            parallel_ranges(m, size_t(1) << 16, [&](size_t a, size_t e) {
+                std::memcpy(dst + a, p + a, (e - a) * sizeof(uint64_t));
+                if (dsc) std::memcpy(dsc + a, sc + a, (e - a) * sizeof(float));
+            });
+            off += m;
+        }, pbase);
+        if (!seen) publish(i, 0, true);  // (failed before its records: the others must not wait)
+        if (!ok) perr[i] = t_last_error ? t_last_error : kErrInternal;
+    });
+    t_last_error = err0;
+    bool bad = failed;
+    for (uint32_t i = 0; i < parts; ++i)
+        if (perr[i]) bad = true, t_last_error = perr[i];
+    if (bad) {
+        delete[] res;
+        delete[] out_s;
+        return 0;
+    }
+    uint64_t sum = 0;
+    for (uint32_t i = 0; i < parts; ++i) {
+        std::copy(pc[i].begin(), pc[i].end(), counts + (size_t)i * per);
+        sum += total[i];
+    }
+    *results = res;
+    if (scores) *scores = out_s;
+    return (uint32_t)sum;
+}
+
 template <typename CharT>
 uint32_t batch_query(uint32_t handle, const CharT* const* queries, uint32_t nq, float thr, uint32_t limit,
                      uint32_t* counts, CharT*** results, float** scores) {
@@ -1834,7 +2007,7 @@ uint32_t batch_query(uint32_t handle, const CharT* const* queries, uint32_t nq, 
     std::vector<float> sc;
     HostTimer ht;
     const uint32_t Lm = effective_limit(*L, limit);
-    const bool one_replica = L->reps.size() == 1 || nq / split_min() <= 1;
+    const bool one_replica = L->split.size() <= 1 || nq / split_min() <= 1;
     if (one_replica && Lm && (uint64_t)nq * Lm <= kDirectMax && nq >= kSmallBatch) {
         // marshalled as the chunks finish, straight into the caller's arrays. One chunk (the
         // common case): the arrays at the exact size, filled from the pinned read-back; several
@@ -1876,6 +2049,14 @@ uint32_t batch_query(uint32_t handle, const CharT* const* queries, uint32_t nq, 
         *results = res;
         if (scores) *scores = out_s;
         return (uint32_t)off;
+    }
+    if (Lm && nq >= kSmallBatch && !one_replica) {
+        const uint32_t n = split_direct(*L, queries, nq, thr, Lm, counts, results, scores);
+        if (n != kNoDirect) {
+            ht.mark(kHpCall, "search + marshal (replicas)");
+            g_host_phase[kHpCalls].fetch_add(1, std::memory_order_relaxed);
+            return n;
+        }
     }
     if (!host_search(*L, queries, nq, thr, limit, cnt, keys, sc)) return 0;
     std::copy(cnt.begin(), cnt.end(), counts);

@@ -10,6 +10,10 @@ try:  # one HIP runtime per process: torch's bundled runtime must be loaded befo
 except ImportError:  # pragma: no cover
     torch = None
 
+# a box here has one GPU: the multi-replica tests place several replicas on device 0, and the library
+# splits a batch only over replicas on distinct devices unless told to split over every replica
+os.environ.setdefault("NGS_SPLIT_SAME_DEVICE", "1")
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
