@@ -381,38 +381,16 @@ struct Context {
         if (side && side != stream && !side_shared) hipStreamDestroy(side);
         if (side2 && side2 != side && side2 != stream) hipStreamDestroy(side2);
     }
-    bool side_shared = false;  // side is the replica's (NGS_SHARED_SIDE)
+    bool side_shared = false;  // side is the replica's (shared by its contexts)
 };
 
-// The side stream runs tier 1b on the heavy list beside tier 1a. At the highest priority
-// (NGS_SIDE_PRIO=1) its workgroups are dispatched first, so the few long heavy queries start
-// at once instead of queueing behind tier 1a's.
-hipError_t make_side_stream(hipStream_t* s) {
-    static const bool prio = [] {
-        const char* e = std::getenv("NGS_SIDE_PRIO");
-        return e ? std::atoi(e) != 0 : kSidePriority;
-    }();
-    if (!prio) return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
-    int lo = 0, hi = 0;
-    hipError_t e = hipDeviceGetStreamPriorityRange(&lo, &hi);
-    if (e != hipSuccess) return e;
-    return hipStreamCreateWithPriority(s, hipStreamNonBlocking, hi);
-}
-
-// The full list's tier 1b (cmin 1, short search) runs on the side stream after the heavy list's
-// chain (NGS_SIDE2=1: on a third stream of its own). With three streams per context, one context's
-// main stream shared a hardware queue (HIP's default is four, one of them the null stream's) with
-// the other's side work and waited behind it (a pipelined scoreBatch measured 2x slower that way);
-// the side stream is now also shared by the replica's contexts (kSharedSide, queue_search).
-hipError_t make_second_side(hipStream_t side, hipStream_t* s) {
-    static const bool own = [] {
-        const char* e = std::getenv("NGS_SIDE2");
-        return e && std::atoi(e) != 0;
-    }();
-    if (own) return make_side_stream(s);
-    *s = side;
-    return hipSuccess;
-}
+// The side stream runs the heavy list's chain and then the full list's tier 1b (cmin 1, short
+// search) beside tier 1a, at normal priority (at the highest one the main launches' streams starved:
+// rejected in round 1 and again in round 5). A third stream per context for the full list made one
+// context's main stream share a hardware queue (HIP's default is four, one of them the null
+// stream's) with the other's side work (a pipelined scoreBatch measured 2x slower that way); the
+// side stream is also shared by the replica's contexts (queue_search).
+hipError_t make_side_stream(hipStream_t* s) { return hipStreamCreateWithFlags(s, hipStreamNonBlocking); }
 
 // One copy of the index in one device's HBM, with its pool of per-call contexts. An index built
 // after ngsSetDevices has one replica per listed device; batches are split across them.
@@ -427,11 +405,11 @@ struct Replica {
     // until dispose (a launch in flight may still read an older set's)
     std::mutex kflag_mu;
     std::vector<std::pair<std::array<uint32_t, 8>, uint8_t*>> kflags;
-    // NGS_SERIAL_MAIN: the last main tier-1a launch of any call on this replica (launch_fast)
+    // the last main tier-1a launch of any call on this replica (launch_fast orders the next after it)
     std::mutex main_mu;
     hipEvent_t main_ev = nullptr;
     bool main_rec = false;
-    hipStream_t shared_side = nullptr;  // NGS_SHARED_SIDE: one side stream for every context (made under main_mu)
+    hipStream_t shared_side = nullptr;  // one side stream for every context (made under main_mu)
 
     // the index as the kernels of a search under `valid` see it (kt_flag for that set); false on a
     // HIP failure
@@ -926,16 +904,7 @@ bool upload(Library& L, const std::vector<int>& devs) {
 // slots they go to tier 1b, and the slots grow when that is frequent (finish_search). Sizing the
 // cap by threshold (wide only at thr <= 1/8) handed 26,594 C4 and 7,871 C5 queries per batch to
 // tier 1b before the arena (profiles/r03_s4_ab_ecap.txt).
-uint32_t emit_cap_forced() {  // NGS_ECAP: fixed slots per query, no growth (experiments)
-    static const uint32_t forced = [] {
-        const char* e = std::getenv("NGS_ECAP");  // (at least the rank-list tail, kRankInfo, plus 64)
-        return e ? std::max<uint32_t>(kRankInfo + 64, (uint32_t)std::strtoul(e, nullptr, 0)) : 0u;
-    }();
-    return forced;
-}
-
 uint32_t emit_cap(size_t B) {
-    if (const uint32_t forced = emit_cap_forced()) return forced;
     static const uint32_t init = [] {  // NGS_ECAP_INIT: the slots a context starts with (tests)
         const char* e = std::getenv("NGS_ECAP_INIT");
         return e ? std::max<uint32_t>(kRankInfo + 64, (uint32_t)std::strtoul(e, nullptr, 0)) : 0u;
@@ -973,12 +942,12 @@ bool ensure_queries(Context& c, size_t B, size_t bytes) {
     // rows actually allocated: a context that once ran a large batch must not grow a small
     // batch's cap into rows x cap bytes past the budget.
     uint32_t want = emit_cap(B);
-    if (c.ecap_grow > want && !emit_cap_forced()) want = std::min(c.ecap_grow, std::max(want, emit_cap_max(B)));
+    if (c.ecap_grow > want) want = std::min(c.ecap_grow, std::max(want, emit_cap_max(B)));
     const bool give_back = c.shrink && c.d_est && want < c.ecap;
     c.shrink = false;
     if (!c.d_est || B > c.ebcap || want > c.ecap || give_back) {
         const size_t nb = (want == c.ecap && c.d_est) ? std::max<size_t>({B, 1024, c.ebcap}) : std::max<size_t>(B, 1024);
-        if (!emit_cap_forced()) want = std::max(emit_cap(B), std::min(want, emit_cap_max(nb)));
+        want = std::max(emit_cap(B), std::min(want, emit_cap_max(nb)));
         for (void** p : {(void**)&c.d_est, (void**)&c.d_esc})
             if (*p) { hipFree(*p); *p = nullptr; }
         c.ebcap = 0;
@@ -1170,16 +1139,8 @@ int queue_search(Library& L, Replica& R, Context& c, const uint8_t* d_raw, const
         P.ablocks = c.ablocks;
         P.actr = gc + kArenaCtrWord;
     }
-    static const uint32_t list_slices = [] {  // term-id slices of the hand-over / full lists' tier 1b
-        const char* e = std::getenv("NGS_SLICES");
-        const uint32_t v = e ? (uint32_t)std::strtoul(e, nullptr, 0) : kSlices;
-        return std::max<uint32_t>(1, std::min<uint32_t>(v, 16));
-    }();
-    static const uint32_t small_slices = [] {  // ... and of every query of the latency path
-        const char* e = std::getenv("NGS_SMALL_SLICES");
-        const uint32_t v = e ? (uint32_t)std::strtoul(e, nullptr, 0) : kSmallSlices;
-        return std::max<uint32_t>(1, std::min<uint32_t>(v, 64));
-    }();
+    constexpr uint32_t list_slices = kSlices;        // term-id slices of the hand-over / full lists' tier 1b
+    constexpr uint32_t small_slices = kSmallSlices;  // ... and of every query of the latency path
     if (small) {
         // one query's postings over several CUs: a wave per (query, slice of at least 8 skip
         // buckets), then k_merge; a small library stays on one wave per query
@@ -1206,46 +1167,31 @@ int queue_search(Library& L, Replica& R, Context& c, const uint8_t* d_raw, const
     // of one call overlapping: its side work goes on the call's own stream, in order, and a context
     // that only ever runs such batches never makes its side streams. Three pipelined calls then hold
     // three hardware queues (HIP maps streams to its four queues round-robin as they are made) instead
-    // of six streams sharing four (C2 28.6 -> 34.8 Mq/s at three in flight; NGS_ONE_STREAM_BATCH sets
-    // the size, 0 turns it off)
-    static const uint32_t one_stream_batch = [] {
-        const char* e = std::getenv("NGS_ONE_STREAM_BATCH");
-        return e ? (uint32_t)std::strtoul(e, nullptr, 0) : kOneStreamBatch;
-    }();
+    // of six streams sharing four (C2 28.6 -> 34.8 Mq/s at three in flight)
+    constexpr uint32_t one_stream_batch = kOneStreamBatch;
     // (only where every lean query is on the heavy list, cmin <= kHeavyCmin for any gram count up to
     // kWaveMaxGrams, as at threshold 0: with a mix, the heavy chain on its own stream overlaps the
     // main launch, and in order after it a call of 8,192 C3-like queries took 0.23 ms longer)
     const bool all_heavy = !((float)kHeavyCmin / (float)kWaveMaxGrams < thr);
     hipStream_t side = s, side2 = s;
-    // one side stream for all of the replica's contexts (NGS_SHARED_SIDE=0: one per context): two
-    // calls in flight then hold three streams beside the null stream, one per hardware queue at HIP's
-    // default of four; with a side stream per context, one context's main and side streams shared a
-    // queue and its tail waited behind its own heavy chain (C3 +1.0 %, six passes on two boxes;
-    // profiles/r05_s27_ab_hw_queues.txt)
-    static const bool shared_side = [] {
-        const char* e = std::getenv("NGS_SHARED_SIDE");
-        return e ? std::atoi(e) != 0 : kSharedSide;
-    }();
+    // one side stream for all of the replica's contexts: two calls in flight then hold three streams
+    // beside the null stream, one per hardware queue at HIP's default of four; with a side stream per
+    // context, one context's main and side streams shared a queue and its tail waited behind its own
+    // heavy chain (C3 +1.0 %, six passes on two boxes; profiles/r05_s27_ab_hw_queues.txt)
     if (B > one_stream_batch || !all_heavy) {
-        if (!c.side && shared_side) {
+        if (!c.side) {
             std::lock_guard<std::mutex> g(R.main_mu);
             if (!R.shared_side && !HIP_CHECK(make_side_stream(&R.shared_side))) return -4;
             c.side = c.side2 = R.shared_side;
             c.side_shared = true;
         }
-        if (!c.side && !HIP_CHECK(make_side_stream(&c.side))) return -4;
-        if (!c.side2 && !HIP_CHECK(make_second_side(c.side, &c.side2))) return -4;
         side = c.side;
         side2 = c.side2;
     }
     // statistics, path counts and list counters: reset by k_prep and k_lists when the context's last
     // call left them so (the memset's fill kernel waited ~200 us for a workgroup slot behind the
-    // previous call's tail in the pipelined trace; NGS_PREP_ZERO=0: always the memset)
-    static const bool prep_zero = [] {
-        const char* e = std::getenv("NGS_PREP_ZERO");
-        return e ? std::atoi(e) != 0 : kPrepZero;
-    }();
-    const bool zero_in_prep = prep_zero && !small && c.stats_clean && P.waves == 0;
+    // previous call's tail in the pipelined trace)
+    const bool zero_in_prep = !small && c.stats_clean && P.waves == 0;
     c.stats_clean = false;
     if (zero_in_prep) {
         P.zero_stats = reinterpret_cast<uint32_t*>(c.d_stats);
@@ -1261,19 +1207,15 @@ int queue_search(Library& L, Replica& R, Context& c, const uint8_t* d_raw, const
         return -4;
     c.stats_clean = !small && P.waves == 0;  // k_lists queued: it leaves the list counters zero
     if (timing) HIP_CHECK(hipEventRecord(c.ev[1], s));  // the end of k_prep is the start of the tier-1 phase
-    // the main tier-1a launches of this replica's calls one after another (NGS_SERIAL_MAIN=0: not):
-    // with two calls in flight the second call's main launch otherwise starts in the first one's and
-    // the two share the GPU (C3, one box, three passes each: 31.3-31.6 against 30.1-30.6 Mq/s,
+    // the main tier-1a launches of this replica's calls one after another: with two calls in flight
+    // the second call's main launch otherwise starts in the first one's and the two share the GPU
+    // (C3, one box, three passes each: 31.3-31.6 against 30.1-30.6 Mq/s,
     // profiles/r05_s15_ab_serial_main.txt; C5 the same)
-    static const bool serial_main = [] {
-        const char* e = std::getenv("NGS_SERIAL_MAIN");
-        return !e || std::atoi(e) != 0;
-    }();
     {
         std::unique_lock<std::mutex> g(R.main_mu, std::defer_lock);
         hipEvent_t mev = nullptr;
         bool mwait = false;
-        if (serial_main && !small) {
+        if (!small) {
             g.lock();
             if (!R.main_ev && !HIP_CHECK(hipEventCreateWithFlags(&R.main_ev, hipEventDisableTiming))) return -4;
             mev = R.main_ev;
@@ -1282,7 +1224,7 @@ int queue_search(Library& L, Replica& R, Context& c, const uint8_t* d_raw, const
         }
         if (!HIP_CHECK(launch_fast(X, P, c.d_norm, d_off, c.d_qm, d_n, d_k, d_s, c.d_list2, gc + 1, c.d_fb, gc + 2,
                                    c.d_fb2, gc + 4, c.d_heavy, gc + 3, c.d_full, gc + 5, c.d_glist, gc, sd, s, side,
-                                   side2, c.join, c.join2, c.lists_ev, all_heavy && !NGS_NO_SKIP_EMPTY, mev, mwait)))
+                                   side2, c.join, c.join2, c.lists_ev, all_heavy, mev, mwait)))
             return -4;
     }
     if (timing) HIP_CHECK(hipEventRecord(c.ev[3], s));
@@ -1605,8 +1547,8 @@ bool finish_host_chunk(Library& L, Replica& R, HostChunk& h, uint32_t Lm, std::v
     return true;
 }
 
-// A large host batch can run as about kPipeChunks chunks (of at least kPipeMinChunk queries; env
-// NGS_PIPE_CHUNKS) over two contexts, one queued ahead, so that chunk k's copies and read-back
+// A large host batch can run as about kPipeChunks chunks (of at least kPipeMinChunk queries) over
+// two contexts, one queued ahead, so that chunk k's copies and read-back
 // overlap chunk k + 1's kernels. Measured slower than one chunk at C3 (the chunks' read-backs
 // waited behind the other chunk's kernels), so one chunk is the default; the batch is still cut
 // into chunks where its outputs would exceed kOutBudget / kPartBudget.

@@ -48,10 +48,7 @@ constexpr uint32_t kFastMaxGrams = 255;  // u8 counts in the table slot
 constexpr uint32_t kMaxPartSpan = (1u << 24) - 2;  // 24-bit relative term id in the slot
 
 // bucket skip table: K <= kMaxBuckets term-id buckets of >= kMinBucketTerms terms each
-#ifndef NGS_MAX_BUCKETS
-#define NGS_MAX_BUCKETS 256
-#endif
-constexpr uint32_t kMaxBuckets = NGS_MAX_BUCKETS;
+constexpr uint32_t kMaxBuckets = 256;
 constexpr uint32_t kMinBucketTerms = 4096;
 constexpr uint64_t kDenseBucketLen = 16;          // dense lists: postings of the longest list per bucket
 constexpr uint64_t kSkipBudget = 512ull << 20;    // ... within this many bytes of skip table
@@ -78,31 +75,19 @@ inline void skip_buckets(uint32_t n_long, uint32_t rows, uint64_t max_len, uint3
 #define NGS_SKETCH_CAP 768
 #endif
 constexpr int kWaveSlotBits = NGS_SLOT_BITS;     // tier 1a table: 2^10 words = 4 KB
-#ifndef NGS_FULL_SLOT_BITS
-#define NGS_FULL_SLOT_BITS 11
-#endif
-constexpr int kFullSlotBits = NGS_FULL_SLOT_BITS;  // tier 1b (full kernel) table: 8 KB
+constexpr int kFullSlotBits = 11;  // tier 1b (full kernel) table: 8 KB
 constexpr int kWaveSlots = 1 << kWaveSlotBits;  // wave-private LDS table (u32 words)
 constexpr int kWaveCap = kWaveSlots / 2;        // entries per exact-count pass (<= 50 % table load)
 constexpr int kSketchCellBits = 4;              // sketch counters: u4, 8 per table word
 constexpr uint32_t kSketchMax = (1u << kSketchCellBits) - 1u;
 constexpr int kSketchCap = NGS_SKETCH_CAP;      // entries per sketch part (<= 1/8 of the cells)
 static_assert(kSketchCap * 8 <= kWaveSlots * (32 / kSketchCellBits), "sketch load");
-#ifndef NGS_WAVE_CAND
-#define NGS_WAVE_CAND 256
-#endif
-constexpr int kWaveCand = NGS_WAVE_CAND;        // candidate buffer per query
+constexpr int kWaveCand = 256;        // candidate buffer per query
 constexpr uint32_t kWaveMaxLimit = 128;         // tier 1 limits (<= kWaveCand / 2)
 static_assert(kWaveMaxLimit * 2 <= (uint32_t)kWaveCand, "a flush keeps at most half the buffer");
 constexpr int kWaveChunks = kSketchCap / 4;     // 16-byte chunks per part and wave (sketch parts)
 constexpr int kExactChunks = (kWaveCap < kSketchCap ? kWaveCap : kSketchCap) / 4;  // ... parts counted exactly (cmin <= 2)
 constexpr int kDmaRounds = kWaveChunks / 64;    // dwordx4 loads per lane for one part
-#ifndef NGS_CAND_BALLOT
-#define NGS_CAND_BALLOT 1  // one-wave sketch: candidates written per entry slot through a ballot
-#endif
-#ifndef NGS_LEAN_CELL_XOR
-#define NGS_LEAN_CELL_XOR 0  // tier-1a sketch cell: 1 = (t ^ t >> 13) & mask, 0 = t & mask
-#endif
 #ifndef NGS_WPS
 #define NGS_WPS 3
 #endif
@@ -115,58 +100,9 @@ constexpr int kLeanWavesPerSimd = NGS_LEAN_WPS; // tier 1a: 6 -> <= 80 VGPRs (LD
 #define NGS_HEAVY_LEAN_WPS NGS_LEAN_WPS  // (5: 95 VGPRs and no scratch, measured no faster: profiles/r04_s2_ab_heavy_wps_sort64.txt)
 #endif
 constexpr int kHeavyLeanWavesPerSimd = NGS_HEAVY_LEAN_WPS;  // ... the heavy list's launch (packed staging)
-#ifndef NGS_LEAN_CAND_IN_TABLE
-#define NGS_LEAN_CAND_IN_TABLE 1
-#endif
-// Only without kDeferEmit (NGS_DEFER_EMIT=0, tier 1a scoring its own survivors): tier 1a keeps
-// its candidate buffer over the sketch table (no calcScore until the part loop ends; a query
-// with more survivors than the survivor list holds goes to tier 1b), or in its own 2 KB
-// (calcScore mid-loop like tier 1b, 8 KB of LDS)
-constexpr bool kLeanCandInTable = NGS_LEAN_CAND_IN_TABLE != 0;
-#ifndef NGS_DEFER_EMIT
-#define NGS_DEFER_EMIT 1
-#endif
-// tier 1a writes its survivor list (term, count) to HBM and k_emit runs calcScore and the top-L
-// per query afterwards: the dependent term -> key loads and the sorts leave the occupancy-bound
-// counting kernel (SearchParams.esn / est / esc)
-constexpr bool kDeferEmit = NGS_DEFER_EMIT != 0;
-#ifndef NGS_MAIN_FIRST
-#define NGS_MAIN_FIRST 1
-#endif
-constexpr bool kMainFirst = NGS_MAIN_FIRST != 0;  // queue the main tier-1a launch before the side streams'
-#ifndef NGS_SKIP_COLD
-#define NGS_SKIP_COLD 1
-#endif
-constexpr bool kSkipCold = NGS_SKIP_COLD != 0;  // skip the sketch candidate pass when no cell reached cmin
-#ifndef NGS_SKETCH_LOOSE
-#define NGS_SKETCH_LOOSE 1
-#endif
-// one-wave sketch add pass without per-entry mask bits (segment-edge entries counted too)
-constexpr bool kSketchLoose = NGS_SKETCH_LOOSE != 0;
-#ifndef NGS_ADD_BATCH
-#define NGS_ADD_BATCH 1  // a round's four sketch adds issued before their results are read
-#endif
-#ifndef NGS_LEAN_G4
-#define NGS_LEAN_G4 0  // 1: tier-1a staging reads each list's chunk base from LDS (measured 1.5 % slower)
-#endif
-#ifndef NGS_EMIT_DEPTH
-#define NGS_EMIT_DEPTH 1  // batches of survivor pairs in flight in the heavy list's k_emit
-#endif
-#ifndef NGS_SORT64
-#define NGS_SORT64 1  // final flushes of <= 64 distinct records sorted in registers (wave_sort64)
-#endif
-#ifndef NGS_RADIX_SELECT
-#define NGS_RADIX_SELECT 1  // top-L buffer refills by radix select (wave_select); 0: bitonic sort
-#endif
-#ifndef NGS_LEAN_STAGE_BATCH
-#define NGS_LEAN_STAGE_BATCH 0  // 1: tier-1a staging reads every round's lookups before its loads
-#endif
-#ifndef NGS_LEAN_DEFER_SKIP
-#define NGS_LEAN_DEFER_SKIP 0  // 1: tier 1a issues the next skip-table read after the part's loads (1 % slower)
-#endif
-#ifndef NGS_LEAN_GROUPS
-#define NGS_LEAN_GROUPS 1  // tier 1a staging by fixed lane groups per list (lean_query_g) in the main launch; 0: packed (lean_stage)
-#endif
+// Tier 1a writes its survivor list (term, count) to HBM and k_emit runs calcScore and the top-L per
+// query afterwards: the dependent term -> key loads and the sorts leave the occupancy-bound counting
+// kernel (SearchParams.esn / est / esc).
 constexpr uint32_t kListSlots = 64;             // slot lists per routing list in k_prep
 constexpr uint32_t kNoEmit = 0xFFFFFFFFu;       // esn[q]: query not finished by tier 1a
 constexpr uint32_t kEmitHeavy = 0x80000000u;    // esn[q] flag: finished by the heavy-list launch
@@ -175,41 +111,14 @@ constexpr uint32_t kEmitHeavy = 0x80000000u;    // esn[q] flag: finished by the 
 constexpr uint32_t kHeavySlotMask = 0xFFFFFFu;
 constexpr uint32_t kHeavyDone = 1u << 24;
 constexpr uint32_t kHeavyBailed = 0x80000000u;
-#ifndef NGS_HEAVY_CMIN
-#define NGS_HEAVY_CMIN 2
-#endif
-constexpr uint32_t kHeavyCmin = NGS_HEAVY_CMIN; // queries with cmin <= this go to the heavy list from the start
-#ifndef NGS_HEAVY_LEAN
-#define NGS_HEAVY_LEAN 1
-#endif
-// the heavy list runs through the lean kernel (its survivors spill to k_emit; cmin-1 and
-// short-search queries hand over to tier 1b), else through tier 1b directly
-constexpr bool kHeavyLean = NGS_HEAVY_LEAN != 0;
-#ifndef NGS_LEAN_SHRINK2
-#define NGS_LEAN_SHRINK2 1
-#endif
-constexpr uint32_t kLeanShrink2 = NGS_LEAN_SHRINK2;  // tier 1a cmin-2 sketch parts: cap and target >> this
-#ifndef NGS_RANK_SHRINK
-#define NGS_RANK_SHRINK NGS_LEAN_SHRINK2
-#endif
-constexpr uint32_t kRankShrink = NGS_RANK_SHRINK;    // ... of threshold-0 queries on rank lists
-#ifndef NGS_LEAN_ONES
-#define NGS_LEAN_ONES 1
-#endif
-// tier 1a also takes cmin-1 queries (threshold 0) on the heavy list: part_ones
-constexpr bool kLeanOnes = NGS_LEAN_ONES != 0;
-#ifndef NGS_HEAVY_ONES_ALWAYS
-#define NGS_HEAVY_ONES_ALWAYS 0  // experiment: the heavy launch compiled with part_ones at every threshold
-#endif
-#ifndef NGS_ONES_SHRINK
-#define NGS_ONES_SHRINK 2
-#endif
-constexpr uint32_t kOnesShrink = NGS_ONES_SHRINK;  // ... in parts of a quarter of the sketch cap
+constexpr uint32_t kHeavyCmin = 2; // queries with cmin <= this go to the heavy list from the start
+// the heavy list runs through the lean kernel (its survivors spill to k_emit; short-search queries
+// and cmin-1 queries without part_ones hand over to tier 1b)
+constexpr uint32_t kLeanShrink2 = 1;  // tier 1a cmin-2 sketch parts: cap and target >> this
+// the heavy list's launch also takes cmin-1 queries (threshold 0): part_ones
+constexpr uint32_t kOnesShrink = 2;  // ... in parts of a quarter of the sketch cap
 constexpr uint32_t kBackPieces = 4;              // host batches: records read back in up to this many pieces
 constexpr uint32_t kBackPieceMin = 131072;        // ... of at least this many records
-#ifndef NGS_NO_SKIP_EMPTY
-#define NGS_NO_SKIP_EMPTY 0  // 1: launch the main k_emit and hand-over tier 1b even when all queries are heavy
-#endif
 constexpr uint32_t kOneStreamBatch = 16384;     // batches up to this size run on one stream per call
 constexpr uint32_t kHeavyGrid = 4096;           // the heavy list's launches: this many workgroups (grid-stride)
 constexpr uint32_t kHeavyMaxSlices = 8;         // ... over (query, term-id slice) items, up to this many per query
@@ -217,28 +126,15 @@ constexpr uint32_t kHeavyItems = 8 * kHeavyGrid; // ... as many slices as keep a
 constexpr uint32_t kHeavySliceList = 1024;      // ... on indexes of at least this many postings per list
 constexpr uint32_t kHeavyOverflowGrid = 1024;   // ... the overflow launch's grid (items past the hinted grid)
 constexpr uint64_t kHeavySlicePostings = 3840;  // ... a slice per this many of the query's postings (~16 parts)
-constexpr bool kSidePriority = false;           // side streams at the highest priority (NGS_SIDE_PRIO; measured no faster)
-constexpr bool kPrepZero = true;               // k_prep / k_lists reset the statistics, not a memset (NGS_PREP_ZERO)
-constexpr bool kSharedSide = true;             // one side stream per replica, not per context (NGS_SHARED_SIDE)
-#ifndef NGS_SHRINK2
-#define NGS_SHRINK2 0
-#endif
-constexpr uint32_t kShrink2 = NGS_SHRINK2;      // cmin 2 sketch parts: cap and target >> this
 constexpr int kWaveTarget = kWaveCap * 5 / 8;   // postings per exact part the bucket grouping aims at
 #ifndef NGS_TGT8
 #define NGS_TGT8 5
 #endif
 constexpr int kSketchTarget = kSketchCap * NGS_TGT8 / 8;  // ... per sketch part (bucket groups aim at NGS_TGT8/8 of the cap)
-#ifndef NGS_GTGT8
-#define NGS_GTGT8 NGS_TGT8
-#endif
-constexpr int kGroupTarget = kSketchCap * NGS_GTGT8 / 8;  // ... the same for tier 1a's lane-group staging (lean_query_g)
+constexpr int kGroupTarget = kSketchCap * NGS_TGT8 / 8;  // ... the same for tier 1a's lane-group staging (lean_query_g)
 constexpr uint32_t kStray = 0xFFFFFFFFu;        // staged entry outside its list segment
 constexpr int kWaveSurv = 128;                  // survivor list (term, count) before calcScore
-#ifndef NGS_EMIT_CAP
-#define NGS_EMIT_CAP 1024
-#endif
-constexpr uint32_t kEmitCap = NGS_EMIT_CAP;
+constexpr uint32_t kEmitCap = 1024;
 // threshold-0 queries on rank lists (DevIndex.rank_post): tier 1a leaves the query's lists for k_emit
 // in the last slots of its survivor slots, per list lane the posting offset (2 x u32) and the length
 constexpr uint32_t kRankInfo = 3 * 64;
@@ -247,9 +143,6 @@ constexpr uint32_t kRankInfo = 3 * 64;
 constexpr uint32_t kEmitCapWide = 4096;
 constexpr uint64_t kEmitWideBytes = 1ull << 30;       // ... halved until the batch's slots fit this
 constexpr uint32_t kEmitCapMax = 32768;              // ... grown up to this many per query
-#ifndef NGS_ARENA
-#define NGS_ARENA 1  // 0 (A/B only): no survivor arena, a query past its slots goes to tier 1b
-#endif
 constexpr uint32_t kArenaBlock = 1024;               // survivor arena block (entries; a multiple of 128)
 constexpr uint32_t kArenaChain = 128;                // blocks one query may chain (k_emit lists them in LDS)
 constexpr uint32_t kArenaCtrWord = 12;               // SearchParams.actr: this word of the path-count line
@@ -257,10 +150,7 @@ constexpr uint32_t kArenaCtrWord = 12;               // SearchParams.actr: this 
 constexpr uint64_t kEmitBudget = 16ull << 30;         // ... within this many bytes per context
 constexpr size_t kEmitWideBatch = 262144;             // tier 1a survivors per query spilled to HBM for k_emit
 constexpr uint32_t kWaveMaxGrams = 63;          // counts <= 63: one lane per count value
-#ifndef NGS_SK2
-#define NGS_SK2 2     // smallest cmin counted by the sketch (below: exact hash counting)
-#endif
-constexpr uint32_t kSketchMinCmin = NGS_SK2;
+constexpr uint32_t kSketchMinCmin = 2;     // smallest cmin counted by the sketch (below: exact hash counting)
 
 struct DevIndex {  // passed by value to kernels; all pointers are device pointers
     const uint64_t* gram_off;   // [kGramSpace + 1] -> post
@@ -387,14 +277,8 @@ __host__ __device__ inline uint32_t heavy_slices(const SearchParams& P, uint32_t
 // hundred to thousands of survivors in one wave; four waves on disjoint term-id ranges each keep
 // their own top-L, and k_merge joins them. The key-max merge is exact: a key among the global
 // top L is among the top L of the slice holding its best record.
-#ifndef NGS_SLICES
-#define NGS_SLICES 4
-#endif
-constexpr uint32_t kSlices = NGS_SLICES;
-#ifndef NGS_T1B_GRID
-#define NGS_T1B_GRID 65536
-#endif
-constexpr uint32_t kTier1bGrid = NGS_T1B_GRID;  // cap on the persistent tier-1b grids (else one per wave slot)
+constexpr uint32_t kSlices = 4;
+constexpr uint32_t kTier1bGrid = 65536;  // cap on the persistent tier-1b grids (else one per wave slot)
 constexpr uint32_t kNoPart = 0xFFFFFFFFu;  // pcnt[q * nslices]: the query was answered unsliced
 
 // ---- low-latency score() (ngsServe, opt-in): a persistent one-wave server kernel polls a

@@ -73,11 +73,9 @@ __device__ __forceinline__ uint32_t char_at(const uint8_t* base, uint64_t i, uin
 
 // Queries tier 1a leaves to a launch of their own, known from the normalised length alone:
 // 1 (heavy list) match-count threshold cmin == 2, where every term sharing a (g+1)-gram with the
-//   query survives: hundreds of survivors, which the heavy list's lean launch spills to k_emit
-//   (kHeavyLean);
-//   The same list takes cmin 1 (kLeanOnes: part_ones, every term sharing a gram survives);
-// 2 (full list, tier 1b) a short search over shortLib (m < 3g, hpp:381); without kHeavyLean
-//   also cmin 1 and 2.
+//   query survives: hundreds of survivors, which the heavy list's lean launch spills to k_emit;
+//   the same list takes cmin 1 (part_ones, every term sharing a gram survives);
+// 2 (full list, tier 1b) a short search over shortLib (m < 3g, hpp:381).
 // Both run beside tier 1a. cmin is computed exactly as the wave kernel does: the first c with
 // !((float)c / n < thr).
 __device__ __forceinline__ uint32_t heavy_class(const DevIndex& X, const SearchParams& P, uint32_t m) {
@@ -90,7 +88,7 @@ __device__ __forceinline__ uint32_t heavy_class(const DevIndex& X, const SearchP
     for (uint32_t c = n; c >= 1; --c)
         if (!((float)c / fn < P.thr)) cmin = c;
     if (cmin > kHeavyCmin) return 0;
-    return kHeavyLean && (cmin >= kSketchMinCmin || kLeanOnes) ? 1 : 2;
+    return 1;
 }
 
 // ---------------------------------------------------------------- normalisation ------
@@ -217,37 +215,14 @@ __device__ __forceinline__ void term_pairs(const DevIndex& X, uint32_t t, float 
     }
 }
 
-// stringMatch (nGramSearch.hpp:182-222): min over source substrings of the edit distance to
-// q (m <= 8); returns m - distance. Column DP over the query held in registers.
-template <typename TT>
-__device__ __forceinline__ uint32_t string_match_t(const uint32_t (&qc)[8], uint32_t m, const TT* s, uint32_t L) {
-    uint32_t col[9];
-#pragma unroll
-    for (int i = 0; i <= 8; ++i) col[i] = (uint32_t)i;
-    uint32_t best = m;
-    for (uint32_t j = 0; j < L; ++j) {
-        const uint32_t c = s[j];
-        uint32_t diag = 0, cur = 0;  // D[0][j] = 0: free start in the source
-#pragma unroll
-        for (int i = 1; i <= 8; ++i) {
-            const uint32_t up = col[i];
-            const uint32_t v = min(diag + (qc[i - 1] != c ? 1u : 0u), min(up, cur) + 1u);
-            diag = up;
-            col[i] = v;
-            cur = v;
-            if ((uint32_t)i == m) best = min(best, v);  // free end: min over the last row
-        }
-    }
-    return m - best;
-}
-
-// The same value by Myers' bit-vector algorithm (J. ACM 46(3), 1999) in its approximate-matching
-// form: bit i of the vertical deltas is row i + 1 of the DP column; a free start in the source is
+// stringMatch (nGramSearch.hpp:182-222): min over source substrings of the edit distance to q
+// (m <= 8), returned as m - distance, by Myers' bit-vector algorithm (J. ACM 46(3), 1999) in its
+// approximate-matching form: bit i of the vertical deltas is row i + 1 of the DP column; a free start in the source is
 // a zero carried into the horizontal deltas, the score tracks the last row (the query's end), and
 // its minimum over the columns is the free end. peq[c] holds the query positions holding
 // character c (c < 256; others are compared with qc); ~16 operations per source character
-// against ~50 for the column DP. Tested against the DP above and the reference's through the
-// oracle (tests/test_gpu_parity.py short corpora, test_oracle_golden.py).
+// against ~50 for a column DP. Tested against a column DP (200k random pairs, round 2) and the
+// reference's through the oracle (tests/test_gpu_parity.py short corpora, test_oracle_golden.py).
 template <typename TT>
 __device__ __forceinline__ uint32_t myers_match_t(const uint8_t* peq, const uint32_t (&qc)[8], uint32_t m,
                                                   const TT* s, uint32_t L) {
@@ -312,19 +287,16 @@ __device__ __forceinline__ void build_peq(uint8_t* peq, QF q, uint32_t m, uint32
     }
 }
 
-#ifndef NGS_MYERS
-#define NGS_MYERS 1  // 0: the column DP (A/B)
-#endif
 // term t of the index against the query (m <= 8 characters in qc; peq its match masks)
 __device__ __forceinline__ uint32_t string_match(const uint8_t* peq, const uint32_t (&qc)[8], uint32_t m,
                                                  const DevIndex& X, uint32_t t) {
     const uint64_t a = X.term_off[t], b = X.term_off[t + 1];
     if (X.csize == 4) {
         const uint32_t* s = reinterpret_cast<const uint32_t*>(X.term_bytes) + a;
-        return NGS_MYERS ? myers_match_t(peq, qc, m, s, (uint32_t)(b - a)) : string_match_t(qc, m, s, (uint32_t)(b - a));
+        return myers_match_t(peq, qc, m, s, (uint32_t)(b - a));
     }
     const uint8_t* s = X.term_bytes + a;
-    return NGS_MYERS ? myers_match_t(peq, qc, m, s, (uint32_t)(b - a)) : string_match_t(qc, m, s, (uint32_t)(b - a));
+    return myers_match_t(peq, qc, m, s, (uint32_t)(b - a));
 }
 
 // Gram of the query characters at position i (accessor qf), as a row of the gram space:
@@ -880,10 +852,10 @@ struct TableGeom {
 template <int W, bool LEAN = false>
 struct alignas(16) WaveSmem {
     uint32_t table[TableGeom<LEAN>::kSlots * W];  // exact: (term - lo + 1) << 8 | count; sketch: 8 x u4 counters
-    uint64_t cand_own[LEAN && kLeanCandInTable ? 1 : kWaveCand];  // (~enc) << 32 | key
+    uint64_t cand_own[LEAN ? 1 : kWaveCand];  // (~enc) << 32 | key
     // the candidate buffer; tier 1a (LEAN) fills it only after the part loop, over the dead table
     __device__ __forceinline__ uint64_t* cand() {
-        if constexpr (LEAN && kLeanCandInTable) return reinterpret_cast<uint64_t*>(table);
+        if constexpr (LEAN) return reinterpret_cast<uint64_t*>(table);
         else return cand_own;
     }
     uint2 segtab[W][64];             // staging, per wave: per list {first chunk - position, first | end entry << 16}
@@ -1101,8 +1073,8 @@ __device__ __forceinline__ void wave_sort64(SM& S, uint32_t n) {
 template <bool RADIX = false, class SM>
 __device__ void wave_flush(SM& S, uint32_t& cand_n, uint64_t& tau, uint32_t L, bool unique = false) {
     const uint32_t lane = lane_id();
-    if (RADIX && NGS_RADIX_SELECT && unique && cand_n > L && L) wave_select(S, cand_n, tau, L);
-    if (NGS_SORT64 && unique && cand_n <= 64) {  // distinct records: sorted in registers
+    if (RADIX && unique && cand_n > L && L) wave_select(S, cand_n, tau, L);
+    if (unique && cand_n <= 64) {  // distinct records: sorted in registers
         const uint32_t n = cand_n;
         wave_sort64(S, n);
         cand_n = min(n, L);
@@ -1158,7 +1130,7 @@ __device__ void wave_flush(SM& S, uint32_t& cand_n, uint64_t& tau, uint32_t L, b
 // and tau are needed, not their order, so distinct-key buffers take the radix select alone.
 template <bool RADIX = false, class SM>
 __device__ __forceinline__ void wave_trim(SM& S, uint32_t& cand_n, uint64_t& tau, uint32_t L, bool unique) {
-    if (RADIX && NGS_RADIX_SELECT && unique && cand_n >= L && L)
+    if (RADIX && unique && cand_n >= L && L)
         wave_select(S, cand_n, tau, L);
     else
         wave_flush(S, cand_n, tau, L, unique);
@@ -1269,12 +1241,12 @@ __device__ __forceinline__ uint32_t wave_insert_slot(uint32_t* T, uint32_t rel, 
 
 // sketch cell of a term: full-rate shift/xor (v_mul_lo_u32 is quarter rate). Term ids of a part
 // are spread over a range much wider than the table, and consecutive ids get distinct cells.
-// Tier 1a (NGS_LEAN_CELL_XOR=0) takes the low bits alone: its parts are contiguous term-id ranges
+// Tier 1a takes the low bits alone (the xor fold measured 10 % slower there): its parts are contiguous term-id ranges
 // whose few hundred entries are spread over an id span far wider than the table.
 template <int W, bool LEAN>
 __device__ __forceinline__ uint32_t sketch_cell(uint32_t t) {  // u4 counter index: 8 per table word
     constexpr uint32_t kBits = TableGeom<LEAN>::kBits + 3 + (W == 4 ? 2 : W == 2 ? 1 : 0);
-    if constexpr (LEAN && !NGS_LEAN_CELL_XOR) return t & ((1u << kBits) - 1u);
+    if constexpr (LEAN) return t & ((1u << kBits) - 1u);
     return (t ^ (t >> kBits)) & ((1u << kBits) - 1u);
 }
 // the table word holding t's cell; tier 1a's low-bit cells address it as the byte offset
@@ -1282,7 +1254,7 @@ __device__ __forceinline__ uint32_t sketch_cell(uint32_t t) {  // u4 counter ind
 template <int W, bool LEAN>
 __device__ __forceinline__ uint32_t* sketch_word(uint32_t* table, uint32_t t) {
     constexpr uint32_t kBits = TableGeom<LEAN>::kBits + 3 + (W == 4 ? 2 : W == 2 ? 1 : 0);
-    if constexpr (LEAN && !NGS_LEAN_CELL_XOR)
+    if constexpr (LEAN)
         return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(table) + ((t >> 1) & (((1u << kBits) - 1u) >> 1 & ~3u)));
     return table + (sketch_cell<W, LEAN>(t) >> 3);
 }
@@ -1292,7 +1264,7 @@ __device__ __forceinline__ uint32_t* sketch_word(uint32_t* table, uint32_t t) {
 template <int W, bool LEAN>
 __device__ __forceinline__ uint32_t sketch_sh4(uint32_t t) {
     constexpr uint32_t kBits = TableGeom<LEAN>::kBits + 3 + (W == 4 ? 2 : W == 2 ? 1 : 0);
-    if constexpr (LEAN && !NGS_LEAN_CELL_XOR) return t << 2;
+    if constexpr (LEAN) return t << 2;
     return (t ^ (t >> kBits)) << 2;
 }
 
@@ -1374,15 +1346,15 @@ __device__ __forceinline__ uint32_t stage_part(WaveSmem<W, LEAN>& S, const uint4
 // of them): shared LDS hash table term -> count. Each such entry's register is replaced by
 // its slot, tagged with the pass number (bit 31 | pass << 16 | slot; term ids stay below 2^31),
 // so later passes over other term ranges skip it; the extraction exchanges the slot with 0,
-// so the first holder of a term owns its count (no table scan; the table ends empty). With
-// W > 1 the waves extract in turns, handing wave 0's survivor / top-L state round in LDS.
+// so the first holder of a term owns its count (no table scan; the table ends empty). One wave
+// (W = 1: the multi-wave variants were slower and are gone).
 template <int W, bool LEAN>
 __device__ __forceinline__ void part_exact(WaveSmem<W, LEAN>& S, uint4 (&v)[kDmaRounds], uint32_t vmask, uint32_t mt,
                                            uint32_t ta, uint32_t tb, uint32_t pass, const DevIndex& X,
                                            const SearchParams& P, uint32_t m, uint32_t L, uint32_t cmin,
                                            float sc_long, float sc_short, uint32_t& surv_n, uint32_t& cand_n,
                                            uint64_t& tau, unsigned* err) {
-    const uint32_t lane = lane_id(), wid = W == 1 ? 0u : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    static_assert(W == 1, "one wave per query");
     mt = __builtin_amdgcn_readfirstlane(mt);
     const uint32_t tag = 0x80000000u | (pass << 16);
 #pragma unroll
@@ -1396,19 +1368,11 @@ __device__ __forceinline__ void part_exact(WaveSmem<W, LEAN>& S, uint4 (&v)[kDma
             }
         }
     }
-    grp_sync<W>();
-    if constexpr (W > 1) {
-        if (wid == 0 && lane == 0) {
-            S.x_surv_n = surv_n;
-            S.x_cand_n = cand_n;
-            S.x_tau = tau;
-        }
-        grp_sync<W>();
-    }
-    for (uint32_t turn = 0; turn < (uint32_t)W; ++turn) {
-        if (wid == turn) {
-            uint32_t sn = W == 1 ? surv_n : S.x_surv_n, cn = W == 1 ? cand_n : S.x_cand_n;
-            uint64_t ta2 = W == 1 ? tau : S.x_tau;
+    wave_sync();
+    {
+        {
+            uint32_t sn = surv_n, cn = cand_n;
+            uint64_t ta2 = tau;
             // one element slot per step (a single wave_emit call site keeps the registers out of scratch)
             for (uint32_t k = 0; k < 4 * (uint32_t)kDmaRounds && 64 * (k >> 2) < mt; ++k) {
                 if (sn + 64 > (uint32_t)kWaveSurv) {
@@ -1434,186 +1398,90 @@ __device__ __forceinline__ void part_exact(WaveSmem<W, LEAN>& S, uint4 (&v)[kDma
                 const uint32_t cnt = c & 255u;  // s = cnt / n; s >= thr <=> cnt >= cmin (nGramSearch.hpp:300,315)
                 surv_append(S, c != 0 && cnt >= cmin, min(X.n_short + ta + (c >> 8) - 1u, X.n_terms - 1u), cnt, sn);
             }
-            if constexpr (W == 1) {
-                surv_n = sn;
-                cand_n = cn;
-                tau = ta2;
-            } else {
-                wave_sync();
-                if (lane == 0) {
-                    S.x_surv_n = sn;
-                    S.x_cand_n = cn;
-                    S.x_tau = ta2;
-                }
-            }
+            surv_n = sn;
+            cand_n = cn;
+            tau = ta2;
         }
-        grp_sync<W>();
-    }
-    if constexpr (W > 1) {
-        if (wid == 0) {  // only wave 0 keeps survivor / top-L state
-            surv_n = S.x_surv_n;
-            cand_n = S.x_cand_n;
-            tau = S.x_tau;
-        }
-        grp_sync<W>();
+        wave_sync();
     }
 }
 
-// Sketch count of a part held in registers (3 <= cmin <= 15; all waves): 8 x u4 counters per shared
-// table word, never an undercount (an increment that wraps a counter past 15 is seen in the
-// value the atomic returns and sends the part to exact counting). Entries whose cell reaches cmin
-// are candidates; wave 0 gets their exact counts by comparing the <= 64 candidates with each
-// other. Returns the number of candidate entries; above 64 the caller counts the part exactly
+// Sketch count of a part held in registers (2 <= cmin <= 15): 8 x u4 counters per table word,
+// never an undercount (an increment that wraps a counter past 15 is seen in the value the atomic
+// returns and sends the part to exact counting). Entries whose cell reaches cmin are candidates;
+// the wave gets their exact counts by comparing the <= 64 candidates with each other. Returns the number of candidate entries; above 64 the caller counts the part exactly
 // (the table is clean again). (u16 counters with no-return adds were measured: the 4x fewer
 // cells per KB cost more in false candidates than the returns cost in waits.)
 template <int W, bool LEAN, int NR = kDmaRounds>
 __device__ __forceinline__ uint32_t part_sketch(WaveSmem<W, LEAN>& S, const uint4 (&v)[NR], uint32_t vmask,
                                                 uint32_t mt, uint32_t cmin, uint32_t n_short, uint32_t n_terms,
                                                 uint32_t& surv_n, uint32_t dbg) {
-    const uint32_t lane = lane_id(), wid = W == 1 ? 0u : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    static_assert(W == 1, "one wave per query");
+    const uint32_t lane = lane_id();
     mt = __builtin_amdgcn_readfirstlane(mt);
-    // ovf: a counter wrapped; hot: an add took a cell from cmin - 1 to cmin (every cell that ends
-    // at >= cmin had exactly one such add in this part: the table starts clear and adds are 0/1)
-    bool ovf = false, hot = false;
     const uint32_t cm1 = __builtin_amdgcn_readfirstlane(cmin - 1u);
-    if constexpr (kSketchLoose && W == 1) {
-        // the add pass also counts the <= 3 entries of neighbouring lists at each segment edge
-        // (never an undercount; the candidate pass below masks them out), so an add needs no
-        // per-entry mask bit, and one running max of the counters it saw stands for both tests:
-        // >= cmin - 1 (an add reached cmin: candidates) and == 15 (a counter wrapped)
-        uint32_t seen = 0;
+    // the add pass also counts the <= 3 entries of neighbouring lists at each segment edge (never an
+    // undercount; the candidate pass below masks them out), so an add needs no per-entry mask bit,
+    // and one running max of the counters it saw stands for both tests: >= cmin - 1 (an add took a
+    // cell to cmin: candidates; every cell that ends at >= cmin had exactly one such add in this part,
+    // the table starting clear and the adds being 0/1) and == 15 (a counter wrapped)
+    uint32_t seen = 0;
 #pragma unroll
-        for (uint32_t r = 0; r < (uint32_t)NR; ++r) {
-            if (64 * r < mt && 64 * r + lane < mt) {
-                const uint32_t t[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
-#if NGS_ADD_BATCH
-                // the round's four returning adds issued together, then their values read (one LDS
-                // wait per round: +3 % once the VALU diet left latency to hide, 31.5 -> 32.4 Mq/s)
-                uint32_t old[4];
+    for (uint32_t r = 0; r < (uint32_t)NR; ++r) {
+        if (64 * r < mt && 64 * r + lane < mt) {
+            const uint32_t t[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
+            // the round's four returning adds issued together, then their values read (one LDS wait
+            // per round: +3 % once the VALU diet left latency to hide, 31.5 -> 32.4 Mq/s)
+            uint32_t old[4];
 #pragma unroll
-                for (uint32_t e = 0; e < 4; ++e)
-                    old[e] = atomicAdd(sketch_word<W, LEAN>(S.table, t[e]), 1u << (sketch_sh4<W, LEAN>(t[e]) & 31u));
+            for (uint32_t e = 0; e < 4; ++e)
+                old[e] = atomicAdd(sketch_word<W, LEAN>(S.table, t[e]), 1u << (sketch_sh4<W, LEAN>(t[e]) & 31u));
 #pragma unroll
-                for (uint32_t e = 0; e < 4; ++e) seen = max(seen, __builtin_amdgcn_ubfe(old[e], sketch_sh4<W, LEAN>(t[e]), 4u));
-#else
-#pragma unroll
-                for (uint32_t e = 0; e < 4; ++e) {
-                    const uint32_t sh4 = sketch_sh4<W, LEAN>(t[e]);
-                    const uint32_t old = atomicAdd(sketch_word<W, LEAN>(S.table, t[e]), 1u << (sh4 & 31u));
-                    seen = max(seen, __builtin_amdgcn_ubfe(old, sh4, 4u));
-                }
-#endif
-            }
-        }
-        ovf = seen == kSketchMax;
-        hot = seen >= cm1;
-    } else {
-#pragma unroll
-        for (uint32_t r = 0; r < (uint32_t)NR; ++r) {
-            if (64 * r < mt) {
-                const uint32_t t[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
-                // (issuing the four returning adds together, one wait, was measured no faster: the
-                // other waves of the SIMD already cover the LDS latency)
-#pragma unroll
-                for (uint32_t e = 0; e < 4; ++e) {
-                    const uint32_t sh4 = sketch_sh4<W, LEAN>(t[e]);
-                    const uint32_t old = atomicAdd(sketch_word<W, LEAN>(S.table, t[e]), ((vmask >> (4 * r + e)) & 1u) << (sh4 & 31u));
-                    const uint32_t on = __builtin_amdgcn_ubfe(old, sh4, 4u);
-                    ovf |= on == kSketchMax;
-                    if constexpr (kSkipCold && W == 1) hot |= on == cm1;
-                }
-            }
+            for (uint32_t e = 0; e < 4; ++e) seen = max(seen, __builtin_amdgcn_ubfe(old[e], sketch_sh4<W, LEAN>(t[e]), 4u));
         }
     }
-    grp_sync<W>();
-    bool cold = false;  // no cell reached cmin: no candidates, skip the candidate pass
-    if constexpr (kSkipCold && W == 1) cold = !__ballot(hot || ovf);
-    if ((dbg & 2u) || cold) {  // (dbg 2, ablation: add pass only)
-        uint4* T4 = reinterpret_cast<uint4*>(S.table) + wid * (TableGeom<LEAN>::kSlots / 4);
+    const bool ovf = seen == kSketchMax, hot = seen >= cm1;
+    wave_sync();
+    if ((dbg & 2u) || !__ballot(hot || ovf)) {  // no cell reached cmin (or dbg 2, ablation: add pass only)
+        uint4* T4 = reinterpret_cast<uint4*>(S.table);
         for (uint32_t i = lane; i < (uint32_t)TableGeom<LEAN>::kSlots / 4; i += 64) T4[i] = make_uint4(0, 0, 0, 0);
-        grp_sync<W>();
+        wave_sync();
         return 0;
     }
     const uint32_t ov = __ballot(ovf) ? 65u : 0u;  // a wrapped counter forces exact counting
-    uint32_t wnc = 0;
-    if constexpr (W == 1 && NGS_CAND_BALLOT) {
-        // one wave: candidates are rare (~3.5 of ~410 entries), so each entry slot is a compare
-        // into a ballot and a uniform branch, taken by the few slots holding one, which write
-        // their terms in place (no per-lane mask, prefix sum or register select)
-        uint32_t nw = 0;
+    // candidates are rare (~3.5 of ~410 entries), so each entry slot is a compare into a ballot and a
+    // uniform branch, taken by the few slots holding one, which write their terms in place (no
+    // per-lane mask, prefix sum or register select)
+    uint32_t nw = 0;
 #pragma unroll
-        for (uint32_t r = 0; r < (uint32_t)NR; ++r) {
-            if (64 * r < mt) {
-                const uint32_t t[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
-                uint32_t w[4];
+    for (uint32_t r = 0; r < (uint32_t)NR; ++r) {
+        if (64 * r < mt) {
+            const uint32_t t[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
+            uint32_t w[4];
 #pragma unroll
-                for (uint32_t e = 0; e < 4; ++e) w[e] = *sketch_word<W, LEAN>(S.table, t[e]);
+            for (uint32_t e = 0; e < 4; ++e) w[e] = *sketch_word<W, LEAN>(S.table, t[e]);
 #pragma unroll
-                for (uint32_t e = 0; e < 4; ++e) {
-                    // the entry's mask bit is tested only in the (rare) branch taken when some
-                    // cell of the slot reached cmin
-                    bool f = __builtin_amdgcn_ubfe(w[e], sketch_sh4<W, LEAN>(t[e]), 4u) >= cmin;
-                    if (__ballot(f)) {
-                        f = f && ((vmask >> (4 * r + e)) & 1u);
-                        const unsigned long long b = __ballot(f);
-                        const uint32_t pos = nw + rank_below(b);
-                        if (f && pos < 64u) S.cbuf[pos] = t[e];
-                        nw += (uint32_t)__popcll(b);
-                    }
+            for (uint32_t e = 0; e < 4; ++e) {
+                // the entry's mask bit is tested only in the (rare) branch taken when some cell of the
+                // slot reached cmin
+                bool f = __builtin_amdgcn_ubfe(w[e], sketch_sh4<W, LEAN>(t[e]), 4u) >= cmin;
+                if (__ballot(f)) {
+                    f = f && ((vmask >> (4 * r + e)) & 1u);
+                    const unsigned long long b = __ballot(f);
+                    const uint32_t pos = nw + rank_below(b);
+                    if (f && pos < 64u) S.cbuf[pos] = t[e];
+                    nw += (uint32_t)__popcll(b);
                 }
             }
-        }
-        wnc = nw + ov;
-    } else {
-        // candidates are rare (~10 of ~600 entries): flag them in a per-lane mask, then write them
-        // at offsets from one prefix sum instead of compacting every entry slot by ballot
-        uint32_t cm = 0;
-#pragma unroll
-        for (uint32_t r = 0; r < (uint32_t)NR; ++r) {
-            if (64 * r < mt) {
-                const uint32_t t[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
-                uint32_t w[4];
-#pragma unroll
-                for (uint32_t e = 0; e < 4; ++e) w[e] = *sketch_word<W, LEAN>(S.table, t[e]);
-#pragma unroll
-                for (uint32_t e = 0; e < 4; ++e) {
-                    cm |= (__builtin_amdgcn_ubfe(w[e], sketch_sh4<W, LEAN>(t[e]), 4u) >= cmin ? 1u : 0u) << (4 * r + e);
-                }
-            }
-        }
-        cm &= vmask;
-        const uint32_t mine = __popc(cm);
-        const uint32_t incl = wave_incl_scan(mine);
-        wnc = __builtin_amdgcn_readlane(incl, 63) + ov;
-        uint32_t base = 0;
-        if constexpr (W > 1) {
-            uint32_t b0 = 0;
-            if (lane == 0 && wnc) b0 = atomicAdd(&S.ncand, wnc);
-            base = __builtin_amdgcn_readlane(b0, 0);
-        }
-        if (base + wnc <= 64 && cm) {  // the few lanes holding candidates walk their set bits
-            uint32_t pos = base + incl - mine;
-            uint32_t bits = cm;
-            do {
-                const uint32_t k = __ffs(bits) - 1u;
-                bits &= bits - 1u;
-                uint32_t t = 0;
-#pragma unroll
-                for (uint32_t j = 0; j < 4 * (uint32_t)NR; ++j) {
-                    const uint32_t x = (j & 3) == 0 ? v[j >> 2].x : (j & 3) == 1 ? v[j >> 2].y : (j & 3) == 2 ? v[j >> 2].z : v[j >> 2].w;
-                    t = j == k ? x : t;
-                }
-                S.cbuf[pos++] = t;
-            } while (bits);
         }
     }
-    grp_sync<W>();
-    uint32_t nc = __builtin_amdgcn_readfirstlane(W == 1 ? wnc : S.ncand);
+    wave_sync();
+    const uint32_t nc = __builtin_amdgcn_readfirstlane(nw + ov);
     {
-        uint4* T4 = reinterpret_cast<uint4*>(S.table) + wid * (TableGeom<LEAN>::kSlots / 4);
+        uint4* T4 = reinterpret_cast<uint4*>(S.table);
         for (uint32_t i = lane; i < (uint32_t)TableGeom<LEAN>::kSlots / 4; i += 64) T4[i] = make_uint4(0, 0, 0, 0);
     }
-    if (wid == 0 && nc && nc <= 64 && !(dbg & 4u)) {
+    if (nc && nc <= 64 && !(dbg & 4u)) {
         // lane l < nc holds candidate l; its term's exact count is the number of candidates with
         // that term (every entry of a term lands in the same cell), owned by the first of them
         uint32_t lc = lane;  // opaque: the slot address is made here, not kept across the part loop (spilled)
@@ -1629,10 +1497,7 @@ __device__ __forceinline__ uint32_t part_sketch(WaveSmem<W, LEAN>& S, const uint
         }
         surv_append(S, lane < nc && first && cnt >= cmin, min(n_short + t, n_terms - 1u), cnt, surv_n);
     }
-    grp_sync<W>();
-    if constexpr (W > 1) {
-        if (wid == 0 && lane == 0) S.ncand = 0;  // every wave has read it; the next writes come after a barrier
-    }
+    wave_sync();
     return nc;
 }
 
@@ -1725,11 +1590,9 @@ __device__ __forceinline__ uint32_t part_ones(WaveSmem<1, true>& S, const uint4 
     return nw;
 }
 
-// One query on W waves. LEAN (tier 1a, W = 1): the common case only, sketch counting with no
-// exact-count pass, no mid-loop calcScore and no short search, which keeps the kernel within 96
-// VGPRs (5 waves per SIMD); a query that needs any of those is appended to fb[] untouched and
-// rerun from scratch by the full kernel (tier 1b).
-template <int W, bool LEAN, bool DEFER = false>
+// One query on W waves: tier 1b (the full wave kernel, k_wave) and the server kernel. Tier 1a's
+// lean kernel has part loops of its own (lean_query, lean_query_g).
+template <int W, bool LEAN = false>
 __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t q, const DevIndex& X, const SearchParams& P,
                                            const uint8_t* __restrict__ qnorm, const uint64_t* __restrict__ qoff,
                                            const uint32_t* __restrict__ qm, uint32_t* __restrict__ out_n,
@@ -1741,7 +1604,8 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
     const uint32_t lane = lane_id(), tid = threadIdx.x;
     // sliced tier 1b: this wave takes the term ids of skip-table buckets [K * slice / nsl,
     // K * (slice + 1) / nsl) and leaves its top-L records for k_merge (SearchParams.prec)
-    const bool sliced = !LEAN && W == 1 && nsl > 1;
+    static_assert(!LEAN, "tier 1a runs lean_query / lean_query_g");
+    const bool sliced = W == 1 && nsl > 1;
     if (sliced) {  // queries answered without the long search: slice 0 answers, k_merge skips them
         const uint32_t m0 = qm[q];
         const bool direct = m0 == kQueryWildcard || m0 == 0 || m0 <= X.full_scan_len ||
@@ -1751,11 +1615,8 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
             if (tid == 0) P.pcnt[(size_t)q * nsl] = kNoPart;
         }
     }
-    // tier 1a hands the query over (all lanes leave together; nothing of it was written yet)
-    auto bail = [&]() {
-        if (lane == 0) fb[atomicAdd(fbc, 1u)] = q;
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    };
+    (void)fb;
+    (void)fbc;
     const uint32_t wid = W == 1 ? 0u : __builtin_amdgcn_readfirstlane(tid >> 6);
     // m_in_lds: the caller (k_serve) put the normalised query in S.q already
     const uint32_t m = m_in_lds != kQueryInGlobal ? m_in_lds : qm[q];
@@ -1800,21 +1661,6 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
     grp_sync<W>();
     uint32_t cand_n = 0, surv_n = 0;
     uint64_t tau = kNoCand;
-    // tier 1a with DEFER: the survivor list goes to this query's kEmitCap slots in HBM
-    // (spilled of them written so far); false if they are full (the query is handed over)
-    uint32_t spilled = 0;
-    auto spill = [&]() -> bool {
-        if (spilled + surv_n > P.ecap) return false;
-        uint32_t* et = P.est + (size_t)q * P.ecap + spilled;
-        uint8_t* ec = P.esc + (size_t)q * P.ecap + spilled;
-        for (uint32_t i = lane; i < surv_n; i += 64) {
-            et[i] = S.surv_t[i];
-            ec[i] = S.surv_c[i];
-        }
-        spilled += surv_n;
-        surv_n = 0;
-        return true;
-    };
     unsigned* err = &stats->errors;
     // lane c holds the fp32 score of c hits: (float)c / n (hpp:300) and (float)c / m (hpp:244)
     const float sc_long = lane <= n ? (float)lane / (float)n : 0.0f;
@@ -1822,28 +1668,21 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
     // the smallest hit count whose score passes the threshold (hpp:300,315)
     const unsigned long long pm = __ballot(lane <= n && lane > 0 && !(sc_long < P.thr));
     const uint32_t cmin = pm ? (uint32_t)(__ffsll((long long)pm) - 1) : 1000u;
-    // the queries heavy_class() lists in k_prep run in launches of their own (same test, same cmin)
-    if (LEAN && !P.lean_all && (cmin <= kHeavyCmin || (m < X.short_query_len && X.n_short))) return;
 
     // ---- searchShort over shortLib (nGramSearch.hpp:262-270), 4 <= m < 9, wave 0 ----
-    if constexpr (LEAN) {
-        if (m < X.short_query_len && X.n_short) { bail(); return; }
-    } else if (wid == 0 && slice == 0 && m < X.short_query_len && X.n_short) {
+    if (wid == 0 && slice == 0 && m < X.short_query_len && X.n_short) {
         uint32_t qc[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) qc[i] = (uint32_t)i < m ? S.q[i] : 0;
         const unsigned long long okm = __ballot(lane <= m && !(sc_short < P.thr));  // hpp:315
         const uint32_t cmin_s = okm ? (uint32_t)(__ffsll((long long)okm) - 1) : 64u;
-        if constexpr (!LEAN) {
-            build_peq(S.peq, [&](uint32_t i) { return S.q[i]; }, m, lane, 64u);
-            wave_sync();
-        }
+        build_peq(S.peq, [&](uint32_t i) { return S.q[i]; }, m, lane, 64u);
+        wave_sync();
         for (uint32_t t0 = 0; t0 < X.n_short; t0 += 64) {
             if (surv_n + 64 > (uint32_t)kWaveSurv) wave_emit(S, X, P, m, L, sc_long, sc_short, surv_n, cand_n, tau);
             const uint32_t t = t0 + lane;
             uint32_t match = 0;
-            if constexpr (!LEAN)
-                if (t < X.n_short) match = string_match(S.peq, qc, m, X, t);
+            if (t < X.n_short) match = string_match(S.peq, qc, m, X, t);
             surv_append(S, t < X.n_short && match >= cmin_s, t, match | 0x80u, surv_n);
         }
     }
@@ -1885,11 +1724,10 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
     // sketch counting for 2 <= cmin <= 15; at cmin 2 two colliding entries already make a false
     // candidate, so those parts are cut at half the size
     const bool sketch = cmin >= kSketchMinCmin && cmin <= kSketchMax;
-    const uint32_t shrink = cmin == 2 ? (LEAN ? kLeanShrink2 : kShrink2) : 0u;
+    const uint32_t shrink = 0;  // (tier 1b counts cmin-2 parts in full: half-size parts measured no faster)
     // part cap: a sketch part holds twice the entries of an exact pass (u8 vs u32 cells)
     const uint32_t kChunks = ((sketch ? (uint32_t)kWaveChunks : (uint32_t)kExactChunks) * W) >> shrink;
     WSTAMP(1);
-    if (LEAN && p_total && cmin <= n && !sketch) { bail(); return; }
     if (p_total && cmin <= n) {
         const uint32_t K = X.n_buckets, span = X.bucket_span;
         const uint32_t wmax = (uint32_t)max64(1, min64(K, kMaxPartSpan / max(span, 1u)));
@@ -2033,17 +1871,12 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
             WSTAMP(4);
             // ---- count part i while part i+1 is in flight ----
             if (have_c && !(P.dbg & 1u)) {  // dbg 1: load only, no counting
-                if (wid == 0 && surv_n + 64 > (uint32_t)kWaveSurv) {
-                    if constexpr (LEAN && DEFER) {
-                        if (!spill()) { bail(); return; }
-                        wave_sync();  // the list is read before it is refilled
-                    } else if constexpr (LEAN && kLeanCandInTable) { bail(); return; }
-                    else wave_emit(S, X, P, m, L, sc_long, sc_short, surv_n, cand_n, tau);
-                }
+                if (wid == 0 && surv_n + 64 > (uint32_t)kWaveSurv)
+                    wave_emit(S, X, P, m, L, sc_long, sc_short, surv_n, cand_n, tau);
                 // the count this part must reach: cmin, raised once the running top-L is full and
                 // a term of fewer hits could not enter it (tier 1b, one wave)
                 uint32_t ceff = cmin;
-                if constexpr (!LEAN && W == 1) {
+                if constexpr (W == 1) {
                     if (!(P.dbg & 128u)) ceff = raised_cmin(S, X, P, m, n, L, cmin, sc_long, sc_short, surv_n, cand_n, tau);
                 }
                 // (survivors must pass the threshold exactly: no sketch past its u4 range)
@@ -2055,8 +1888,7 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
                 WCOUNT(13, sketch ? nc : 0);
                 WCOUNT(14, c_mt);
                 WSTAMP(5);
-                if (LEAN && !done) { bail(); return; }
-                if (!LEAN && !done) {
+                if (!done) {
                     // exact count in term-id ranges of <= kWaveCap entries per wave (one range unless a
                     // sketch part overflowed)
                     const uint32_t mtu = __builtin_amdgcn_readfirstlane(c_mt);
@@ -2097,22 +1929,6 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
     }
     WSTAMP(7);
     if (wid != 0) return;
-    if constexpr (LEAN && DEFER) {  // calcScore + top-L in k_emit
-        if (!spill()) { bail(); return; }
-        if (lane == 0) P.esn[q] = spilled | (P.lean_all ? kEmitHeavy : 0u);
-        if (lane == 0 && !(P.dbg & 32u)) {
-            DevStats* sl = stats + (q & (kStatSlots - 1));
-            atomicAdd(&sl->postings, (unsigned long long)p_total);
-            atomicAdd(&sl->lists, (unsigned long long)ng);
-            atomicAdd(&sl->fast, 1ull);
-            atomicAdd(&sl->survivors, (unsigned long long)spilled);
-        }
-#ifdef NGS_PHASE_STAMPS
-        if (lane == 0)
-            for (int i = 0; i < 16; ++i) atomicAdd(&g_phase[16 + i], wacc_[i]);
-#endif
-        return;
-    }
     if (surv_n) wave_emit(S, X, P, m, L, sc_long, sc_short, surv_n, cand_n, tau);
     WSTAMP(8);
     wave_flush(S, cand_n, tau, L, X.keys_unique != 0);
@@ -2164,7 +1980,7 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
 // map's bits below lane l in word c / 64 (v_mbcnt_lo/hi) plus those of the earlier words; the
 // non-empty lists' {first chunk - pre, entry bounds} sit in segtab by ordinal. (stage_part, the
 // full kernel's staging, spends a marker array and a max-scan per round on the same lookup.)
-template <bool G4 = (NGS_LEAN_G4 != 0)>
+template <bool G4>
 __device__ __forceinline__ void lean_stage(WaveSmem<1, true>& S, gptr<uint4> post4, uint64_t gbase,
                                            uint32_t a0, uint32_t cur, uint32_t len, uint32_t nch, uint32_t incl,
                                            uint32_t mt, uint4 (&v)[kDmaRounds], uint32_t& vmask) {
@@ -2203,38 +2019,6 @@ __device__ __forceinline__ void lean_stage(WaveSmem<1, true>& S, gptr<uint4> pos
     vmask = 0;
     uint32_t lo = lane;  // opaque: chunk positions are made per round, not hoisted (and spilled)
     asm volatile("" : "+v"(lo));
-#if NGS_LEAN_STAGE_BATCH
-    // every round's list-start word, then every round's segtab entry, read before the first load
-    // goes out: two dependent LDS round trips per part instead of two per round (the words of
-    // rounds past mt are clear, their lookups harmless)
-    uint32_t idx[kDmaRounds];
-#pragma unroll
-    for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) {
-        const unsigned long long wd = S.lstart[r];
-        const uint32_t wlo = __builtin_amdgcn_readfirstlane((uint32_t)wd);
-        const uint32_t whi = __builtin_amdgcn_readfirstlane((uint32_t)(wd >> 32));
-        idx[r] = __builtin_amdgcn_mbcnt_hi(whi, __builtin_amdgcn_mbcnt_lo(wlo, below)) & 63u;
-        below += (uint32_t)__popc(wlo) + (uint32_t)__popc(whi);
-    }
-    uint2 segs[kDmaRounds];
-#pragma unroll
-    for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) segs[r] = S.segtab[0][idx[r]];
-#pragma unroll
-    for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) {
-        if (64 * r < mt) {
-            const uint32_t c = 64 * r + lo;
-            const bool ok = c < mt;
-            const uint2 seg = segs[r];
-            if (ok) v[r] = post4[seg.x + c];
-            const int y = (int)(seg.y & 0xFFFFu), z = (int)(seg.y >> 16);
-            const uint32_t lo_e = (uint32_t)min(max(y - (int)(4 * c), 0), 4);
-            const uint32_t hi_e = (uint32_t)min(max(z - (int)(4 * c), 0), 4);
-            const uint32_t bits = ((1u << hi_e) - 1u) & ~((1u << lo_e) - 1u);
-            vmask |= (ok ? bits : 0u) << (4 * r);
-        }
-    }
-    return;
-#endif
 #pragma unroll
     for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) {
         if (64 * r < mt) {
@@ -2375,7 +2159,7 @@ __device__ __forceinline__ void lean_query(WaveSmem<1, true>& S, const uint32_t 
     WSTAMP(0);
     const bool sketch = cmin >= kSketchMinCmin && cmin <= kSketchMax;
     const bool ones = ONES && cmin == 1;  // part_ones (the heavy list's launch only)
-    constexpr bool kG4 = NGS_LEAN_G4 || ONES;  // list chunk bases in LDS (lean_stage)
+    constexpr bool kG4 = ONES;  // list chunk bases in LDS (lean_stage; for every query: 1.5 % slower)
     if (p_total && cmin <= n && !sketch && !ones) {  // exact counting: tier 1b
         if (!slc) bail();
         return;
@@ -2422,7 +2206,7 @@ __device__ __forceinline__ void lean_query(WaveSmem<1, true>& S, const uint32_t 
         // cmin 2: every colliding pair is a false candidate, so those parts are cut at half the size;
         // a gram the query repeats makes every term of its list a candidate, so a list held by mu
         // lanes cuts them further (the part's candidates stay within the 64 a part resolves)
-        uint32_t shrink = ones ? kOnesShrink : cmin == 2 ? (rank ? kRankShrink : kLeanShrink2) : 0u;
+        uint32_t shrink = ones ? kOnesShrink : cmin == 2 ? kLeanShrink2 : 0u;
         if (cmin == 2) {
             uint32_t mu = 0;
             for (uint32_t k = 0; k < ng; ++k)
@@ -2479,7 +2263,7 @@ __device__ __forceinline__ void lean_query(WaveSmem<1, true>& S, const uint32_t 
                 if (tot && tot <= kChunks) {
                     len = e - cur;
                     bnext = min(Kend, bnext + w);
-                    if (!NGS_LEAN_DEFER_SKIP && lane < ng) e_pre = next_end(bnext);
+                    if (lane < ng) e_pre = next_end(bnext);
                     have_p = true;
                     fast = true;  // e_pre of the next group loads after this part's loads (below)
                 }
@@ -2554,9 +2338,6 @@ __device__ __forceinline__ void lean_query(WaveSmem<1, true>& S, const uint32_t 
                 p_mt = tot;
                 cur += len;
             }
-            // the fast path's skip-table read for the group after: issued behind the part's loads,
-            // so that nothing in staging waits for it (it is read at the next part's planning)
-            if (NGS_LEAN_DEFER_SKIP && fast && lane < ng) e_pre = next_end(bnext);
             WSTAMP(4);
             // ---- count part i while part i+1 is in flight ----
             if (have_c) {
@@ -2605,7 +2386,7 @@ __device__ __forceinline__ void lean_query(WaveSmem<1, true>& S, const uint32_t 
     }
 }
 
-// Tier 1a with lane groups (NGS_LEAN_GROUPS): each of the query's lists owns a fixed group of lanes
+// Tier 1a with lane groups (the main launch): each of the query's lists owns a fixed group of lanes
 // for the whole query, sized in proportion to its length (quota_j = 1 + (64 - ng) * len_j / P lanes).
 // Lane `slot` of list j's group loads chunks slot, slot + G, slot + 2G of that list's segment in
 // each part, so a chunk never has to find its list: no per-part prefix sum, list-start map or
@@ -2689,90 +2470,6 @@ __device__ __forceinline__ uint32_t lean_sketch_g(WaveSmem<1, true>& S, const ui
     }
     wave_sync();
     return nc;
-}
-
-// part_ones (cmin 1) over a part staged by lane groups
-__device__ __forceinline__ uint32_t lean_ones_g(WaveSmem<1, true>& S, const uint4 (&v)[kDmaRounds], uint32_t R,
-                                                uint32_t k0, uint32_t G, uint32_t nch, uint32_t head, uint32_t len,
-                                                uint32_t n_short, uint32_t n_terms, uint32_t& surv_n,
-                                                uint32_t* __restrict__ et, uint8_t* __restrict__ ec, uint32_t& spilled,
-                                                uint32_t ecap) {
-    const uint32_t lane = lane_id();
-    R = __builtin_amdgcn_readfirstlane(R);
-    uint32_t seen = 0;
-#pragma unroll
-    for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) {
-        if (r < R && k0 + r * G < nch) {
-            const uint32_t t[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
-            uint32_t old[4];
-#pragma unroll
-            for (uint32_t e = 0; e < 4; ++e)
-                old[e] = atomicAdd(sketch_word<1, true>(S.table, t[e]), 1u << (sketch_sh4<1, true>(t[e]) & 31u));
-#pragma unroll
-            for (uint32_t e = 0; e < 4; ++e) seen = max(seen, __builtin_amdgcn_ubfe(old[e], sketch_sh4<1, true>(t[e]), 4u));
-        }
-    }
-    const bool ovf = __ballot(seen == kSketchMax) != 0;
-    wave_sync();
-    uint32_t nw = 0;
-    if (!ovf) {
-#pragma unroll
-        for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) {
-            if (r < R) {
-                const uint32_t t[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
-                uint32_t w[4];
-#pragma unroll
-                for (uint32_t e = 0; e < 4; ++e) w[e] = *sketch_word<1, true>(S.table, t[e]);
-#pragma unroll
-                for (uint32_t e = 0; e < 4; ++e) {
-                    const bool in = 4u * (k0 + r * G) + e - head < len;
-                    const uint32_t c = in ? __builtin_amdgcn_ubfe(w[e], sketch_sh4<1, true>(t[e]), 4u) : 0u;
-                    const bool one = c == 1, two = c >= 2;
-                    const unsigned long long b1 = __ballot(one);
-                    if (b1) {
-                        const uint32_t pos = spilled + rank_below(b1);
-                        if (one && pos < ecap) {
-                            et[pos] = min(n_short + t[e], n_terms - 1u);
-                            ec[pos] = 1;
-                        }
-                        spilled += (uint32_t)__popcll(b1);
-                    }
-                    const unsigned long long b2 = __ballot(two);
-                    if (b2) {
-                        const uint32_t pos = nw + rank_below(b2);
-                        if (two && pos < 64u) S.cbuf[pos] = t[e];
-                        nw += (uint32_t)__popcll(b2);
-                    }
-                }
-            }
-        }
-    }
-    wave_sync();
-    {
-        uint4* T4 = reinterpret_cast<uint4*>(S.table);
-#pragma unroll
-        for (uint32_t i = 0; i < (uint32_t)kWaveSlots / 256; ++i) T4[lane + 64 * i] = make_uint4(0, 0, 0, 0);
-    }
-    if (ovf || nw > 64 || spilled + surv_n > ecap) {
-        wave_sync();
-        return 65;
-    }
-    if (nw) {  // exact counts of the candidates (as part_sketch), every one of them a survivor
-        uint32_t lc = lane;
-        asm volatile("" : "+v"(lc));
-        const uint32_t t = lc < nw ? S.cbuf[lc] : kStray;
-        uint32_t cnt = 0;
-        bool first = true;
-        for (uint32_t j = 0; j < nw; ++j) {
-            const uint32_t tj = __builtin_amdgcn_readlane(t, j);
-            const bool eq = t == tj;
-            cnt += eq;
-            first &= !(eq && j < lane);
-        }
-        surv_append(S, lane < nw && first, min(n_short + t, n_terms - 1u), cnt, surv_n);
-    }
-    wave_sync();
-    return nw;
 }
 
 // a staged part of lean_query_g: its chunks per lane's list, first entry in the first chunk, entries,
@@ -2871,8 +2568,8 @@ __device__ __forceinline__ void lean_query_g(WaveSmem<1, true>& S, const uint32_
     const uint64_t p_total = wave_sum((uint64_t)glen);
     WSTAMP(0);
     const bool sketch = cmin >= kSketchMinCmin && cmin <= kSketchMax;
-    const bool ones = ONES && cmin == 1;  // part_ones (the heavy list's launch only)
-    if (p_total && cmin <= n && !sketch && !ones) { bail(); return; }  // exact counting: tier 1b
+    static_assert(!ONES, "part_ones runs in lean_query (the heavy list's launch)");
+    if (p_total && cmin <= n && !sketch) { bail(); return; }  // exact counting: tier 1b
     uint32_t surv_n = 0, spilled = 0;
     // rank lists: the query's lists for k_emit (emit_rank_prefix) in its last kRankInfo slots
     const uint32_t ecap_q = P.ecap - (rank ? kRankInfo : 0u);
@@ -2933,7 +2630,7 @@ __device__ __forceinline__ void lean_query_g(WaveSmem<1, true>& S, const uint32_
         return true;
     };
     auto spill = [&]() -> bool {
-        if (spilled + surv_n > ecap_q) return NGS_ARENA && P.at && spill_arena();
+        if (spilled + surv_n > ecap_q) return P.at && spill_arena();
         uint32_t qs = q, l0 = lane;  // opaque: the slot pointers are made here, not kept (and spilled)
         asm volatile("" : "+s"(qs), "+v"(l0));
         uint32_t* et = P.est + (size_t)qs * P.ecap + spilled;
@@ -2972,22 +2669,15 @@ __device__ __forceinline__ void lean_query_g(WaveSmem<1, true>& S, const uint32_
         const uint64_t lbase = __shfl(gbase, js);
         const uint32_t lrow = (uint32_t)__shfl(grow, js);
         // cmin 2: every colliding pair is a false candidate, so those parts are cut at half the size
-        const uint32_t shrink = ones ? kOnesShrink : cmin == 2 ? kLeanShrink2 : 0u;
+        const uint32_t shrink = cmin == 2 ? kLeanShrink2 : 0u;
         // chunks a part may hold of this lane's list: its lanes' three rounds (cut as the sketch part is)
         const uint32_t capc = has ? min(3u * G, max(2u, (3u * G) >> shrink)) : 0u;
         const uint32_t K = X.n_buckets, span = X.bucket_span;
         const uint32_t wmax = (uint32_t)max64(1, min64(K, kMaxPartSpan / max(span, 1u)));
         const uint32_t w = (uint32_t)max64(1, min64(wmax, (uint64_t)K * (kGroupTarget >> shrink) / p_total));
         const uint32_t skrow = lrow * (K + 1);
-#ifdef NGS_SLICE_PROBE
-        // diagnostic build (timing only, answers partial): every query counts term-id slice 0 of
-        // NGS_SLICE_PROBE (NGS_DEBUG & 0x100: slice q mod NGS_SLICE_PROBE), to time list locality
-        const uint32_t nsl = NGS_SLICE_PROBE, slc = (P.dbg & 0x100u) ? q % nsl : 0u;
-        const uint32_t b0 = K * slc / nsl, Kend = K * (slc + 1) / nsl;
-#else
         constexpr uint32_t b0 = 0;
         const uint32_t Kend = K;
-#endif
         WSTAMP(1);
         gptr<uint4> post4 = (gptr<uint4>)reinterpret_cast<const uint4*>(X.post);
         asm volatile("" : "+s"(post4));
@@ -3112,16 +2802,7 @@ __device__ __forceinline__ void lean_query_g(WaveSmem<1, true>& S, const uint32_
                 }
                 wave_sync();  // the list is read before it is refilled
             }
-            uint32_t nc;
-            if constexpr (ONES) {
-                uint32_t qs = q;
-                asm volatile("" : "+s"(qs));
-                nc = ones ? lean_ones_g(S, v, ps.R, k0, G, ps.nch, ps.head, ps.len, X.n_short, X.n_terms, surv_n,
-                                        P.est + (size_t)qs * P.ecap, P.esc + (size_t)qs * P.ecap, spilled, P.ecap)
-                          : lean_sketch_g(S, v, ps.R, k0, G, ps.nch, ps.head, ps.len, cmin, X.n_short, X.n_terms, surv_n);
-            } else {
-                nc = lean_sketch_g(S, v, ps.R, k0, G, ps.nch, ps.head, ps.len, cmin, X.n_short, X.n_terms, surv_n);
-            }
+            const uint32_t nc = lean_sketch_g(S, v, ps.R, k0, G, ps.nch, ps.head, ps.len, cmin, X.n_short, X.n_terms, surv_n);
 #ifdef NGS_PHASE_STAMPS
             last_nc = nc;
 #endif
@@ -3314,7 +2995,7 @@ __global__ __launch_bounds__(64) void k_serve(DevIndex X, SearchParams P0, Serve
 }
 
 // Tier 1a: the lean wave kernel over every query (qlist == nullptr), or over the heavy list.
-// DEFER: survivors spill to HBM for k_emit (the heavy launch always; the main one if kDeferEmit).
+// DEFER (both launches): survivors spill to HBM for k_emit.
 // ONES: the heavy list's launch, which also takes cmin-1 queries (part_ones); the main launch
 // is compiled without that path. LISTED: the launch walks a query list (the heavy list), else
 // one workgroup per query (the main launch): either way the part loop is compiled once (with
@@ -3336,29 +3017,21 @@ __global__ __launch_bounds__(64, PACKED ? kHeavyLeanWavesPerSimd : kLeanWavesPer
                                                                     const uint32_t* __restrict__ qcount) {
     __shared__ WaveSmem<1, true> S;
     // lane-group staging (lean_query_g) for the main launch; the heavy list's launch keeps the packed
-    // staging for its threshold-0 queries (part_ones: quarter-size parts of ~3 chunks per list, where a
-    // per-list cap splits most parts), NGS_LEAN_GROUPS 2: for all of them, 3: for its cmin >= 2 ones
+    // staging (lean_query): its threshold-0 queries' part_ones parts are ~3 chunks per list, where a
+    // per-list cap splits most parts (lane groups there measured slower, C2 32.0-32.8 against
+    // 37.1-37.3 Mq/s)
     auto one = [&](uint32_t q) {
-        if constexpr (NGS_LEAN_GROUPS == 0 || (PACKED && NGS_LEAN_GROUPS != 2)) {
+        if constexpr (PACKED || ONES)
             lean_query<ONES>(S, q, X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats, fb, fbc);
-        } else if constexpr (!ONES || NGS_LEAN_GROUPS == 2) {
+        else
             lean_query_g<ONES>(S, q, X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats, fb, fbc);
-        } else if constexpr (NGS_LEAN_GROUPS == 3) {
-            // cmin 1 iff (float)1 / n >= thr, the test lean_query makes (same fp32 division)
-            const uint32_t m = qm[q];
-            const bool c1 = m != kQueryWildcard && m >= X.gsz && !(1.0f / (float)(m - X.gsz + 1) < P.thr);
-            if (c1) lean_query<ONES>(S, q, X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats, fb, fbc);
-            else lean_query_g<ONES>(S, q, X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats, fb, fbc);
-        } else {
-            lean_query<ONES>(S, q, X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats, fb, fbc);
-        }
     };
     if constexpr (!LISTED) {
         one(blockIdx.x);
         return;
     }
     const uint32_t cnt = *qcount;  // the heavy list, grid-stride
-    if constexpr (PACKED && NGS_LEAN_GROUPS != 2) {
+    if constexpr (PACKED) {
         // (query, term-id slice) items, one per workgroup (heavy_grid sizes the launch for every
         // item; the rest exit), a query's slices on neighbouring workgroups: enough slices that a
         // short list fills the GPU and no query's wave outlasts the rest by much. No item loop: in one
@@ -3548,8 +3221,8 @@ __device__ __forceinline__ void emit_query(EmitSmem& S, const uint32_t q, const 
     // one pair per term (DevIndex.tk_identity): a software pipeline over the batches of 64: while
     // batch b is scored, the pairs of batches b + 1 .. b + D and the survivors of batches up to
     // b + 2D + 1 are in flight (a threshold-0 query has thousands of survivors, and a batch is
-    // otherwise two dependent round trips). D = 1 in the main launch; the heavy launch, whose
-    // queries are few per SIMD and long, keeps more in flight (NGS_EMIT_DEPTH)
+    // otherwise two dependent round trips). D = 1 in both launches (2 and 4 for the heavy launch's
+    // long queries measured within noise on C2)
     uint32_t base0 = 0;
     if (X.tk_identity && sn > 64) {
         uint32_t T[2 * D + 1], Cc[2 * D + 1];  // survivors of batches b .. b + 2D
@@ -3647,7 +3320,7 @@ __device__ __forceinline__ void emit_query(EmitSmem& S, const uint32_t q, const 
     // survivors past the slots (rare: a query that outgrew them): its arena blocks in order, 64 at a
     // time, without prefetch (lane 0 walks the chain first: a few dependent loads; the block list goes
     // to rstage, free until emit_rank_prefix)
-    if (NGS_ARENA && sn_all > sn) {
+    if (sn_all > sn) {
         const uint32_t na = sn_all - sn;
         if (lane == 0) {
             uint32_t bnx = P.eovf[q];
@@ -3727,7 +3400,7 @@ __global__ __launch_bounds__(64 * kEmitWaves) void k_emit(DevIndex X, SearchPara
     }
     const uint32_t cnt = *qcount;
     for (uint32_t j = j0; j < cnt; j += gridDim.x * kEmitWaves) {
-        emit_query<RADIX, RADIX ? NGS_EMIT_DEPTH : 1>(S, qlist[j], true, X, P, qnorm, qoff, qm, out_n, out_k, out_s,
+        emit_query<RADIX>(S, qlist[j], true, X, P, qnorm, qoff, qm, out_n, out_k, out_s,
                                                       stats);
         wave_sync();
     }
@@ -4141,17 +3814,11 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
             PM.qhead = gcount + 8;
             PHO.qhead = gcount + 9;
             // (esn[] was reset by k_prep)
-            // NGS_LEAN_PAD_LDS (diagnostic): dynamic LDS bytes per workgroup of the main launch, to run
-            // the same code at fewer waves per CU (occupancy sensitivity)
-            static const uint32_t pad_lds = [] {
-                const char* e = std::getenv("NGS_LEAN_PAD_LDS");
-                return e ? (uint32_t)std::strtoul(e, nullptr, 0) : 0u;
-            }();
             // main_ev (NGS_SERIAL_MAIN): the replica's last main launch, waited for (main_wait) before this
             // one and recorded after it, so that two calls in flight do not run their main launches at once
             auto main_lean = [&]() {
                 if (main_ev && main_wait) (void)hipStreamWaitEvent(s, main_ev, 0);
-                hipLaunchKernelGGL((k_wave_lean<kDeferEmit, false, false>), dim3(P.n_queries), dim3(64), pad_lds, s, X,
+                hipLaunchKernelGGL((k_wave_lean<true, false, false>), dim3(P.n_queries), dim3(64), 0, s, X,
                                    P, qnorm, off, qm,
                                    out_n, out_k, out_s, list2, count2, stats, fb, fbc, (const uint32_t*)nullptr,
                                    (const uint32_t*)nullptr);
@@ -4160,24 +3827,24 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
             };
             // the main launch is queued first: the GPU idled ~35 us while the host queued the side
             // streams' launches ahead of it
-            if (kMainFirst) main_lean();
+            main_lean();
             // then the heavy list's chain on side, which is already ordered after k_prep with k_lists
             // queued on it (launch_prep): queued second, so that it starts soon after k_lists (the
             // host queues ~15 operations per call; at C2 this launch carries every query)
             // (the heavy chain deferred until the main launch ends measured slower at C3, 35.5-35.7
             // against 36.5-36.6 Mq/s; fused with its k_emit into one kernel slower too, C2 18 against
             // 33-35: profiles/r04_s2_ab_defer_heavy.txt, r04_s2_ab_heavy_fuse.txt)
-            if (kHeavyLean) {
+            {
                 SearchParams PH = P;
                 PH.lean_all = 1;
                 {
                     // part_ones is compiled in only where a lean query can have cmin 1: without rank lists,
                     // at a threshold the shortest lean query (n_min grams) passes with one hit
                     const uint32_t n_min = (X.n_short ? X.short_query_len : X.full_scan_len + 1) - X.gsz + 1;
-                    const bool ones = kLeanOnes && (NGS_HEAVY_ONES_ALWAYS || (!X.rank_post && !(1.0f / (float)n_min < P.thr)));
+                    const bool ones = !X.rank_post && !(1.0f / (float)n_min < P.thr);
                     PH.hbase = 0;
                     if (ones)
-                        hipLaunchKernelGGL((k_wave_lean<true, kLeanOnes, true, true>), dim3(ghl), dim3(64), 0, side, X, PH,
+                        hipLaunchKernelGGL((k_wave_lean<true, true, true, true>), dim3(ghl), dim3(64), 0, side, X, PH,
                                            qnorm, off, qm, out_n, out_k, out_s, list2, count2, stats, fb2, fbc2, heavy,
                                            hcount);
                     else
@@ -4188,7 +3855,7 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
                         PH.hbase = ghl;
                         const uint32_t gov = std::min<uint32_t>(ghb - ghl, kHeavyOverflowGrid);
                         if (ones)
-                            hipLaunchKernelGGL((k_wave_lean<true, kLeanOnes, true, true, true>), dim3(gov), dim3(64), 0,
+                            hipLaunchKernelGGL((k_wave_lean<true, true, true, true, true>), dim3(gov), dim3(64), 0,
                                                side, X, PH, qnorm, off, qm, out_n, out_k, out_s, list2, count2, stats,
                                                fb2, fbc2, heavy, hcount);
                         else
@@ -4225,11 +3892,10 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
                 dbg_check(side2, "k_wave<1> (full list)");
             }
             if (side2 != s && (e = hipEventRecord(join2, side2)) != hipSuccess) return e;
-            if (!kMainFirst) main_lean();
             // all_heavy (every lean query on the heavy list, e.g. threshold 0): the main launch finishes
             // no query and hands none over (it returns before either for a heavy or full one), so its
             // k_emit and hand-over launches would find nothing
-            if (kDeferEmit && !all_heavy) {
+            if (!all_heavy) {
                 hipLaunchKernelGGL(k_emit<false>, dim3((P.n_queries + kEmitWaves - 1) / kEmitWaves), dim3(64 * kEmitWaves), 0,
                                    s, X, P, qnorm, off, qm, out_n, out_k, out_s, stats, (const uint32_t*)nullptr,
                                    (const uint32_t*)nullptr);
