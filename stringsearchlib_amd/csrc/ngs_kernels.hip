@@ -3708,12 +3708,27 @@ __global__ __launch_bounds__(64) void k_lists(const uint32_t* __restrict__ slots
         if (lane == 63) *(L ? fcount : hcount) = incl;
     }
     __syncthreads();
-    for (uint32_t sl = 0; sl < 2 * kListSlots; ++sl) {
-        const uint32_t L = sl / kListSlots, k = sl % kListSlots;
-        const uint32_t b0 = base[L * (kListSlots + 1) + k], n = base[L * (kListSlots + 1) + k + 1] - b0;
-        const uint32_t* src = slots + (size_t)sl * cap;
-        uint32_t* dst = (L ? full : heavy) + b0;
-        for (uint32_t i = lane; i < n; i += 64) dst[i] = src[i];
+    // eight slots' copies at once: their loads in flight together (slot by slot, each copy waited for
+    // its load: 36 us for C2's 4,096 heavy queries, on the heavy chain's critical path)
+    constexpr uint32_t kGroup = 8;
+    static_assert((2 * kListSlots) % kGroup == 0, "slot groups");
+    for (uint32_t s0 = 0; s0 < 2 * kListSlots; s0 += kGroup) {
+        uint32_t b0[kGroup], n[kGroup], nmax = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < kGroup; ++j) {
+            const uint32_t sl = s0 + j, L = sl / kListSlots, k = sl % kListSlots;
+            b0[j] = base[L * (kListSlots + 1) + k];
+            n[j] = base[L * (kListSlots + 1) + k + 1] - b0[j];
+            nmax = max(nmax, n[j]);
+        }
+        for (uint32_t i = lane; i < nmax; i += 64) {
+            uint32_t v[kGroup];
+#pragma unroll
+            for (uint32_t j = 0; j < kGroup; ++j) v[j] = i < n[j] ? slots[(size_t)(s0 + j) * cap + i] : 0u;
+#pragma unroll
+            for (uint32_t j = 0; j < kGroup; ++j)
+                if (i < n[j]) ((s0 + j) / kListSlots ? full : heavy)[b0[j] + i] = v[j];
+        }
     }
 }
 
@@ -3932,7 +3947,10 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
         default:
             return hipErrorInvalidValue;
     }
-    const uint32_t grid2 = std::min<uint32_t>(P.n_queries, 1024);
+    // tier 2 takes every query at a limit past the wave kernels' (1,024 blocks), else only the rare
+    // long ones (> 63 grams) and those bound for the general path: 128 blocks, grid-stride (1,024
+    // blocks that mostly exit cost ~20 us at C2 and ~50 us at C3 per call)
+    const uint32_t grid2 = std::min<uint32_t>(P.n_queries, P.limit > kWaveMaxLimit ? 1024u : 128u);
     hipLaunchKernelGGL(k_fast, dim3(grid2), dim3(kFastThreads), 0, s, X, P, qnorm, off, qm, out_n, out_k, out_s,
                        (const uint32_t*)list2, (const uint32_t*)count2, glist, gcount, stats);
     dbg_check(s, "k_fast");
