@@ -632,7 +632,7 @@ bool upload_replica(Library& L, Replica& R, bool keys_unique, bool first) {
     float *wild_w, *wild_score;
     // from here on the replica's destructor frees what was allocated
     PhaseTimer pt;
-    bool ok = dev_upload(&term_off, H.term_off, R.owned) && dev_upload(&term_bytes, H.term_bytes, R.owned, 4) /* whole dwords */ &&
+    bool ok = dev_upload(&term_off, H.term_off, R.owned) && dev_upload(&term_bytes, H.term_bytes, R.owned, 8) /* whole dwords, and a short term's second dword (myers_short) */ &&
               dev_upload(&tk_off, H.tk_off, R.owned) && dev_upload(&tk, H.tk, R.owned) &&
               dev_upload(&key_off, H.key_off, R.owned) && dev_upload(&key_bytes, kb, R.owned) &&
               dev_upload(&wild_w, H.wild_w, R.owned);

@@ -83,6 +83,8 @@ constexpr uint32_t kSketchMax = (1u << kSketchCellBits) - 1u;
 constexpr int kSketchCap = NGS_SKETCH_CAP;      // entries per sketch part (<= 1/8 of the cells)
 static_assert(kSketchCap * 8 <= kWaveSlots * (32 / kSketchCellBits), "sketch load");
 constexpr int kWaveCand = 256;        // candidate buffer per query
+constexpr uint32_t kGenSelThreads = 1024;       // general path: k_gen_select's workgroup (one per query)
+constexpr uint32_t kGenSelCap = 1024;           // ... and the limits it takes (larger: sort per query)
 constexpr uint32_t kWaveMaxLimit = 128;         // tier 1 limits (<= kWaveCand / 2)
 static_assert(kWaveMaxLimit * 2 <= (uint32_t)kWaveCand, "a flush keeps at most half the buffer");
 constexpr int kWaveChunks = kSketchCap / 4;     // 16-byte chunks per part and wave (sketch parts)

@@ -276,6 +276,35 @@ __device__ __forceinline__ uint32_t myers_match_t(const uint8_t* peq, const uint
     return m - best;
 }
 
+// myers_match_t over a short narrow term (L <= 5 bytes: shortLib holds terms shorter than 2g <= 6)
+// held in two dwords (x1:x0) from byte sk: its match masks read from peq all at once (five LDS reads
+// in flight instead of one per character), then the recurrence; steps past L do not move `best`
+__device__ __forceinline__ uint32_t myers_short(const uint8_t* peq, uint32_t m, uint32_t x0, uint32_t x1, uint32_t sk,
+                                                uint32_t L) {
+    const uint64_t x = (((uint64_t)x1 << 32) | x0) >> (8u * sk);
+    uint32_t eq[kShortTermLen - 1];
+#pragma unroll
+    for (uint32_t j = 0; j + 1 < kShortTermLen; ++j) eq[j] = peq[(uint32_t)(x >> (8u * j)) & 255u];
+    const uint32_t top = 1u << (m - 1u);
+    uint32_t pv = ~0u, mv = 0u, score = m, best = m;
+#pragma unroll
+    for (uint32_t j = 0; j + 1 < kShortTermLen; ++j) {
+        const uint32_t e = eq[j];
+        const uint32_t xv = e | mv;
+        const uint32_t xh = (((e & pv) + pv) ^ pv) | e;
+        uint32_t ph = mv | ~(xh | pv);
+        uint32_t mh = pv & xh;
+        score += (ph & top) ? 1u : 0u;
+        score -= (mh & top) ? 1u : 0u;
+        ph <<= 1;
+        mh <<= 1;
+        pv = mh | ~(xv | ph);
+        mv = ph & xv;
+        best = j < L ? min(best, score) : best;
+    }
+    return m - best;
+}
+
 // the match-mask table of Myers' algorithm for characters < 256: peq[c] bit i = (q[i] == c);
 // threads [tid0, tid0 + nthreads) of the caller fill it (the caller orders it before use)
 template <class QF>
@@ -1678,12 +1707,50 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
         const uint32_t cmin_s = okm ? (uint32_t)(__ffsll((long long)okm) - 1) : 64u;
         build_peq(S.peq, [&](uint32_t i) { return S.q[i]; }, m, lane, 64u);
         wave_sync();
-        for (uint32_t t0 = 0; t0 < X.n_short; t0 += 64) {
+        const uint32_t ns = X.n_short;
+        // narrow corpora: rounds of 64 terms (lane: term 64 r + lane) in a software pipeline; while
+        // round r is matched, the bytes of round r + 1 and the offsets of round r + 2 are in flight
+        // (a term is two dependent loads, offsets then bytes; one round at a time left both
+        // exposed). Wide corpora match through string_match. One loop, so wave_emit keeps a
+        // single call site here (a second one stops it inlining and puts X and P in scratch).
+        const bool narrow = X.csize == 1;
+        const uint64_t* to = X.term_off;
+        const uint8_t* tbase = X.term_bytes;  // (padded by two dwords: the second dword is always readable)
+        auto offs = [&](uint32_t t, uint64_t& a, uint64_t& b) {
+            const uint32_t u = min(t, ns - 1u);
+            a = to[u];
+            b = to[u + 1];
+        };
+        auto bytes = [&](uint64_t a, uint64_t b, uint32_t& y0, uint32_t& y1, uint32_t& sk, uint32_t& len) {
+            const uint32_t* w = reinterpret_cast<const uint32_t*>(tbase + (a & ~3ull));
+            y0 = w[0];
+            y1 = w[1];
+            sk = (uint32_t)a & 3u;
+            len = (uint32_t)(b - a);
+        };
+        uint64_t a1 = 0, b1 = 0;
+        uint32_t x0 = 0, x1 = 0, xs = 0, xl = 0;
+        if (narrow) {
+            uint64_t a0, b0;
+            offs(lane, a0, b0);
+            offs(64u + lane, a1, b1);
+            bytes(a0, b0, x0, x1, xs, xl);
+        }
+        for (uint32_t t0 = 0; t0 < ns; t0 += 64) {
+            uint32_t y0 = 0, y1 = 0, ys = 0, yl = 0;
+            uint64_t a2 = 0, b2 = 0;
+            if (narrow) {
+                bytes(a1, b1, y0, y1, ys, yl);   // round r + 1
+                offs(t0 + 128u + lane, a2, b2);  // round r + 2
+            }
             if (surv_n + 64 > (uint32_t)kWaveSurv) wave_emit(S, X, P, m, L, sc_long, sc_short, surv_n, cand_n, tau);
             const uint32_t t = t0 + lane;
             uint32_t match = 0;
-            if (t < X.n_short) match = string_match(S.peq, qc, m, X, t);
-            surv_append(S, t < X.n_short && match >= cmin_s, t, match | 0x80u, surv_n);
+            if (narrow) match = myers_short(S.peq, m, x0, x1, xs, xl);
+            else if (t < ns) match = string_match(S.peq, qc, m, X, t);
+            surv_append(S, t < ns && match >= cmin_s, t, match | 0x80u, surv_n);
+            x0 = y0, x1 = y1, xs = ys, xl = yl;
+            a1 = a2, b1 = b2;
         }
     }
     WSTAMP(0);
@@ -3517,11 +3584,19 @@ __global__ __launch_bounds__(256) void k_gen_compact(uint32_t n_keys, uint32_t* 
     const uint32_t gi = blockIdx.y;
     uint32_t* K = kenc + (size_t)gi * n_keys;
     uint64_t* Lst = list + (size_t)gi * n_keys;
-    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n_keys; k += gridDim.x * blockDim.x) {
-        const uint32_t e = K[k];
+    // (one counter per query: a wave appends its records with one atomic; a full-library scan
+    // leaves most keys set, and per-lane atomics on G counters took ~2 ms per group)
+    const uint32_t n_it = (n_keys + gridDim.x * blockDim.x - 1) / (gridDim.x * blockDim.x);
+    for (uint32_t it = 0, k = blockIdx.x * blockDim.x + threadIdx.x; it < n_it; ++it, k += gridDim.x * blockDim.x) {
+        const uint32_t e = k < n_keys ? K[k] : 0u;
+        const unsigned long long b = __ballot(e != 0);
+        if (!b) continue;
+        uint32_t base = 0;
+        if (lane_id() == (uint32_t)(__ffsll((long long)b) - 1)) base = atomicAdd(&lcount[gi], (uint32_t)__popcll(b));
+        base = __shfl(base, __ffsll((long long)b) - 1);
         if (e) {
             K[k] = 0;
-            Lst[atomicAdd(&lcount[gi], 1u)] = ((uint64_t)(~e) << 32) | k;
+            Lst[base + rank_below(b)] = ((uint64_t)(~e) << 32) | k;
         }
     }
 }
@@ -3538,6 +3613,130 @@ __global__ __launch_bounds__(256) void k_gen_write(const uint64_t* __restrict__ 
         out_s[ob + i] = __uint_as_float(enc - 1u);
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) out_n[q] = cnt;
+}
+
+// The general path's top-L for limits up to kGenSelCap, one workgroup per query of the group, in
+// place of a compaction, a device-wide radix sort per query and k_gen_write (~60 us a query: a
+// full-library scan of an m <= 3 query scores most keys). Order as there: score encoding
+// descending, key id ascending (hpp:397-401 with the canonical tie order).
+// A radix select over the row's encodings (11 + 11 + 10 bits) finds the L-th largest one, T;
+// a last pass in key order takes every key above T and the first keys at T, and clears the row;
+// the <= L records are sorted in LDS.
+__global__ __launch_bounds__(kGenSelThreads) void k_gen_select(uint32_t n_keys, uint32_t* __restrict__ kenc,
+                                                              const uint32_t* __restrict__ group, SearchParams P,
+                                                              uint32_t* __restrict__ out_n,
+                                                              uint32_t* __restrict__ out_k, float* __restrict__ out_s) {
+    constexpr uint32_t kBins = 2048, kWaves = kGenSelThreads / 64;
+    __shared__ uint32_t hist[kBins];
+    __shared__ uint64_t rec[kGenSelCap];
+    __shared__ uint32_t wcnt[kWaves];
+    __shared__ uint32_t s_pick[3];  // bin, count above it, records taken
+    const uint32_t tid = threadIdx.x, lane = lane_id(), wid = tid >> 6;
+    const uint32_t gi = blockIdx.x, q = group[gi];
+    uint32_t* K = kenc + (size_t)gi * n_keys;
+    const uint32_t L = min(P.limit, kGenSelCap);
+    const uint32_t n_it = (n_keys + kGenSelThreads - 1) / kGenSelThreads;
+    uint32_t prefix = 0, mask = 0, need = L;  // need: rank of T among the keys matching prefix
+    bool all = false;                          // fewer than L keys scored: take every one
+    for (int pass = 0; pass < 3 && L; ++pass) {
+        const uint32_t shift = pass == 0 ? 21u : pass == 1 ? 10u : 0u;
+        const uint32_t bmask = pass == 2 ? 0x3FFu : 0x7FFu;
+        for (uint32_t i = tid; i < kBins; i += kGenSelThreads) hist[i] = 0;
+        __syncthreads();
+        for (uint32_t it = 0, k = tid; it < n_it; ++it, k += kGenSelThreads) {
+            const uint32_t e = k < n_keys ? K[k] : 0u;
+            const bool in = e != 0 && (e & mask) == prefix;
+            const uint32_t bin = (e >> shift) & bmask;
+            // equal scores are the rule (m <= 3: a handful of distinct scores): a wave whose
+            // counted keys share one bin adds them with one LDS atomic
+            const unsigned long long b = __ballot(in);
+            if (!b) continue;
+            const uint32_t b0 = __shfl(bin, __ffsll((long long)b) - 1);
+            if (__ballot(in && bin == b0) == b) {
+                if (lane == (uint32_t)(__ffsll((long long)b) - 1)) atomicAdd(&hist[b0], (uint32_t)__popcll(b));
+            } else if (in) {
+                atomicAdd(&hist[bin], 1u);
+            }
+        }
+        __syncthreads();
+        if (wid == 0) {  // the bin holding rank `need`, from the top: lane l owns bins kBins-32(l+1) .. kBins-1-32l
+            constexpr uint32_t per = kBins / 64;
+            uint32_t sum = 0;
+            for (uint32_t j = 0; j < per; ++j) sum += hist[kBins - 1 - lane * per - j];
+            uint32_t incl = sum;  // inclusive prefix over lanes (lane 0 = the top bins)
+            for (uint32_t d = 1; d < 64; d <<= 1) {
+                const uint32_t o = __shfl_up(incl, d);
+                if (lane >= d) incl += o;
+            }
+            const uint32_t total = __shfl(incl, 63);
+            const uint32_t excl = incl - sum;
+            if (pass == 0 && lane == 0 && total < need) s_pick[0] = 0xFFFFFFFFu;  // fewer than L keys
+            if (!(pass == 0 && total < need) && excl < need && need <= incl) {
+                uint32_t above = excl, bin = 0;
+                for (uint32_t j = 0; j < per; ++j) {
+                    const uint32_t bb = kBins - 1 - lane * per - j, c = hist[bb];
+                    if (above + c >= need) { bin = bb; break; }
+                    above += c;
+                }
+                s_pick[0] = bin;
+                s_pick[1] = above;
+            }
+        }
+        __syncthreads();
+        if (s_pick[0] == 0xFFFFFFFFu) { all = true; break; }
+        prefix |= s_pick[0] << shift;
+        mask |= bmask << shift;
+        need -= s_pick[1];
+        __syncthreads();  // (s_pick is rewritten by the next pass)
+    }
+    // T: the L-th largest encoding; take every key above it and the first `need` at it, in key order
+    const uint32_t T = all || !L ? 0u : prefix;
+    if (tid == 0) s_pick[2] = 0;
+    uint32_t eq_base = 0;
+    __syncthreads();
+    for (uint32_t it = 0, k = tid; it < n_it; ++it, k += kGenSelThreads) {
+        const uint32_t e = k < n_keys ? K[k] : 0u;
+        if (e) K[k] = 0;
+        const bool gt = L && e != 0 && (all || e > T);
+        const bool eq = !all && T != 0 && e == T;
+        const unsigned long long be = __ballot(eq);
+        if (lane == 0) wcnt[wid] = (uint32_t)__popcll(be);
+        __syncthreads();
+        uint32_t before = eq_base, chunk = 0;
+        for (uint32_t w = 0; w < kWaves; ++w) {
+            const uint32_t c = wcnt[w];
+            before += w < wid ? c : 0u;
+            chunk += c;
+        }
+        before += rank_below(be);
+        eq_base += chunk;
+        if (gt || (eq && before < need)) {
+            const uint32_t at = atomicAdd(&s_pick[2], 1u);
+            if (at < kGenSelCap) rec[at] = ((uint64_t)(~e) << 32) | k;
+        }
+        __syncthreads();  // (wcnt is rewritten by the next chunk)
+    }
+    const uint32_t n = min(s_pick[2], L);
+    const uint32_t P2 = n <= 1 ? 1u : 1u << (32 - __clz(n - 1));
+    for (uint32_t i = n + tid; i < P2; i += kGenSelThreads) rec[i] = ~0ull;
+    __syncthreads();
+    for (uint32_t k2 = 2; k2 <= P2; k2 <<= 1) {
+        for (uint32_t j = k2 >> 1; j > 0; j >>= 1) {
+            for (uint32_t p = tid; p < P2 / 2; p += kGenSelThreads) {
+                const uint32_t i = ((p & ~(j - 1u)) << 1) | (p & (j - 1u)), l = i + j;
+                const uint64_t x = rec[i], y = rec[l];
+                if ((x > y) == ((i & k2) == 0)) { rec[i] = y; rec[l] = x; }
+            }
+            __syncthreads();
+        }
+    }
+    const size_t ob = (size_t)q * P.out_stride;
+    for (uint32_t i = tid; i < n; i += kGenSelThreads) {
+        const uint64_t r = rec[i];
+        out_k[ob + i] = (uint32_t)r;
+        out_s[ob + i] = __uint_as_float(~(uint32_t)(r >> 32) - 1u);
+    }
+    if (tid == 0) out_n[q] = n;
 }
 
 // DevIndex.kt_flag under one validChar set: key k (several pairs) can be promoted by a long term
@@ -4049,6 +4248,11 @@ hipError_t run_general(const DevIndex& X, const SearchParams& P, const uint8_t* 
     if (X.n_terms) {
         const uint32_t gx = std::min<uint32_t>((X.n_terms + 255) / 256, 2048);
         hipLaunchKernelGGL(k_gen_short, dim3(gx, G), dim3(256), 0, s, X, P, qnorm, off, qm, d_group, W.kenc);
+    }
+    if (P.limit <= kGenSelCap) {  // top-L in one kernel, no host round trip
+        hipLaunchKernelGGL(k_gen_select, dim3(G), dim3(kGenSelThreads), 0, s, X.n_keys, W.kenc, d_group, P, out_n,
+                           out_k, out_s);
+        return hipGetLastError();
     }
     if (X.n_keys) {
         const uint32_t gx = std::min<uint32_t>((X.n_keys + 255) / 256, 2048);

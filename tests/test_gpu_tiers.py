@@ -200,3 +200,29 @@ def test_device_api_general_path_without_device_sync(bench20k):
             ref = oi.score(q, 0.0, 0)
             got = [(gi.key(key[i * stride + j]), sc[i * stride + j]) for j in range(cnt[i])]
             assert_exact(got, ref, f"device q={q!r} rep={rep}")
+
+
+@pytest.mark.parametrize("kind", ["bench", "rows", "short"])
+def test_general_select_limits(bench20k, kind):
+    """The general path's top-L (k_gen_select: radix select over the row of key encodings, the
+    first keys at the L-th score in key order, an LDS sort) at limits that cut through long runs
+    of equal scores, limits above the number of scored keys, and 1025 (the per-query sort) —
+    exact against the oracle, with more queries than one group holds."""
+    if kind == "bench":
+        words, gi, oi = bench20k
+        own = False
+    else:
+        words, rs, wts = _corpus(kind, random.Random(13))
+        gi, oi = ssl.StringIndex(words, rs, wts), OracleIndex(words, rs, wts)
+        own = True
+    rng = random.Random(zlib.crc32(kind.encode()) + 1)
+    live = [w for w in words if w]
+    base = [w[:rng.randint(1, 3)] for w in rng.sample(live, 24)] + [b"E", b"ZZ", b"Q9X"]
+    for thr, limit in [(0.0, 1), (0.0, 2), (0.3, 37), (0.5, 100), (0.0, 1024), (1.0, 1024), (0.3, 1025)]:
+        st = _check(gi, oi, base, thr, limit, f"general-select-{kind}")
+        assert st["general_queries"] == len(base), st
+    many = [w[:rng.randint(2, 3)] for w in rng.sample(live, 150)]
+    st = _check(gi, oi, many, 0.3, 100, f"general-groups-{kind}")
+    assert st["general_queries"] == len(many), st
+    if own:
+        gi.dispose()

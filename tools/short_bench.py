@@ -25,10 +25,15 @@ def main():
     h = L.indexN(arr, rows, 1, None)
     short = [w for w in words if len(w) < 6]
     out = {"rows": rows, "short_terms": L.getSize(h) and len(set(short)), "version": L.ngsVersion().decode()}
-    for name, lo, hi, n in [("m4-8 (shortLib scan)", 4, 8, B), ("m1-3 (whole-library scan)", 2, 3, 256)]:
+    # m4-8: 4-8 characters (shortLib scan in tier 1b); mixed: the same draw before round 6, where a
+    # 3-character source word gives a 3-character query (~1/8 of them) and so a whole-library scan
+    cases = [("m4-8 (shortLib scan)", 4, 8, B, 4), ("m3-8 mixed (1/8 whole-library)", 4, 8, B, 0),
+             ("m1-3 (whole-library scan)", 2, 3, 1024, 0)]
+    for name, lo, hi, n, min_src in cases:
+        pool = [w for w in words if len(w) >= min_src]
         qs = []
         for _ in range(n):
-            src = rng.choice(words)
+            src = rng.choice(pool)
             k = min(len(src), rng.randint(lo, hi))
             o = rng.randrange(len(src) - k + 1)
             qs.append(src[o:o + k])
