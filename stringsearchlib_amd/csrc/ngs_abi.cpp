@@ -466,7 +466,7 @@ struct Replica {
             if (!HIP_CHECK(hipEventCreate(&e))) return nullptr;
         for (hipEvent_t& e : c->piece_ev)
             if (!HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming))) return nullptr;
-        if (!dev_alloc(&c->d_group, 64) || !dev_alloc(&c->d_stats, kStatSlots + 1 + 2 * kListSlots) ||
+        if (!dev_alloc(&c->d_group, kGeneralMaxGroup) || !dev_alloc(&c->d_stats, kStatSlots + 1 + 2 * kListSlots) ||
             !dev_alloc(&c->d_sio, kSioBytes) ||
             !HIP_CHECK(hipMemsetAsync(c->d_sio, 0, kSioStats, c->stream)) ||
             !HIP_CHECK(hipStreamSynchronize(c->stream)) ||
@@ -1072,11 +1072,12 @@ bool ensure_general(const Replica& R, Context& c, hipStream_t s) {
     if (c.gen.G) return true;
     const DevIndex& X = R.dev;
     const uint64_t n_long = X.n_terms - X.n_short;
-    const uint64_t per = n_long * 4 + (uint64_t)X.n_keys * 12 + 64;
-    uint32_t G = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(64, kGeneralBudget / per));
-    if ((uint64_t)G * std::max<uint32_t>(X.n_keys, 1) > (uint64_t)kInt32Max) G = 1;
+    const uint64_t kst = gen_kstride(X.n_keys);
+    const uint64_t per = n_long * 4 + kst * 4 + (uint64_t)X.n_keys * 8 + 64;
+    uint32_t G = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(kGeneralMaxGroup, kGeneralBudget / per));
+    if ((uint64_t)G * std::max<uint64_t>(kst, 1) > (uint64_t)kInt32Max) G = 1;
     GeneralBuffers& W = c.gen;
-    if (!dev_alloc(&W.cnt, (size_t)G * n_long) || !dev_alloc(&W.kenc, (size_t)G * X.n_keys) ||
+    if (!dev_alloc(&W.cnt, (size_t)G * n_long) || !dev_alloc(&W.kenc, (size_t)G * kst) ||
         !dev_alloc(&W.list, (size_t)G * X.n_keys) || !dev_alloc(&W.sorted, X.n_keys) || !dev_alloc(&W.lcount, G))
         return false;
     W.temp_bytes = general_sort_temp_bytes(X.n_keys);
@@ -1084,7 +1085,7 @@ bool ensure_general(const Replica& R, Context& c, hipStream_t s) {
     // on the call's stream: a plain hipMemset runs on the null stream, which the context's
     // non-blocking streams do not wait for (the first group's counts raced with it)
     if (!HIP_CHECK(hipMemsetAsync(W.cnt, 0, sizeof(uint32_t) * std::max<size_t>((size_t)G * n_long, 1), s)) ||
-        !HIP_CHECK(hipMemsetAsync(W.kenc, 0, sizeof(uint32_t) * std::max<size_t>((size_t)G * X.n_keys, 1), s)))
+        !HIP_CHECK(hipMemsetAsync(W.kenc, 0, sizeof(uint32_t) * std::max<size_t>((size_t)G * kst, 1), s)))
         return false;
     W.G = G;
     return true;

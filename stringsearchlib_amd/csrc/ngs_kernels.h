@@ -69,7 +69,7 @@ hipError_t build_rank_post(const uint64_t* gram_off, uint32_t n_seg, const uint3
 struct GeneralBuffers {
     uint32_t G = 0;             // queries per group
     uint32_t* cnt = nullptr;    // [G][n_long] posting counts (self-clearing)
-    uint32_t* kenc = nullptr;   // [G][n_keys] per-key score encoding (self-clearing)
+    uint32_t* kenc = nullptr;   // [G][gen_kstride(n_keys)] per-key score encoding (self-clearing)
     uint64_t* list = nullptr;   // [G][n_keys] compacted candidate records
     uint64_t* sorted = nullptr; // [n_keys] radix-sort output
     uint32_t* lcount = nullptr; // [G] candidates per query
@@ -77,6 +77,9 @@ struct GeneralBuffers {
     size_t temp_bytes = 0;
 };
 size_t general_sort_temp_bytes(uint32_t n_keys);
+constexpr uint32_t kGeneralMaxGroup = 256;  // queries per group (one k_gen_select workgroup each)
+// kenc's row stride: n_keys rounded up to whole 16-byte loads (the padding stays zero)
+__host__ __device__ inline uint32_t gen_kstride(uint32_t n_keys) { return (n_keys + 3u) & ~3u; }
 
 // Diagnostic build (make prof, -DNGS_PHASE_STAMPS): accumulated block-time per k_fast phase in
 // 100 MHz ticks. Returns the number of phases, or -1 in the regular build.

@@ -3536,7 +3536,7 @@ __global__ __launch_bounds__(256) void k_gen_long(DevIndex X, SearchParams P, co
     const uint32_t n = m - X.gsz + 1, n_long = X.n_terms - X.n_short;
     const uint8_t* qs = qnorm + qoff[q];
     uint32_t* C = cnt + (size_t)gi * n_long;
-    uint32_t* K = kenc + (size_t)gi * X.n_keys;
+    uint32_t* K = kenc + (size_t)gi * gen_kstride(X.n_keys);
     const uint64_t me = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (uint64_t)gridDim.x * blockDim.x;
     const float fn = (float)n;
     for (uint32_t i = 0; i < n; ++i) {
@@ -3571,7 +3571,7 @@ __global__ __launch_bounds__(256) void k_gen_short(DevIndex X, SearchParams P, c
     __shared__ uint8_t peq[256];
     build_peq(peq, [&](uint32_t i) { return char_at(qs, i, X.csize); }, m, threadIdx.x, blockDim.x);
     __syncthreads();
-    uint32_t* K = kenc + (size_t)gi * X.n_keys;
+    uint32_t* K = kenc + (size_t)gi * gen_kstride(X.n_keys);
     const float fm = (float)m;
     for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < end; t += gridDim.x * blockDim.x) {
         const float s = (float)string_match(peq, qc, m, X, t) / fm;
@@ -3582,7 +3582,7 @@ __global__ __launch_bounds__(256) void k_gen_short(DevIndex X, SearchParams P, c
 __global__ __launch_bounds__(256) void k_gen_compact(uint32_t n_keys, uint32_t* __restrict__ kenc,
                                                      uint64_t* __restrict__ list, uint32_t* __restrict__ lcount) {
     const uint32_t gi = blockIdx.y;
-    uint32_t* K = kenc + (size_t)gi * n_keys;
+    uint32_t* K = kenc + (size_t)gi * gen_kstride(n_keys);
     uint64_t* Lst = list + (size_t)gi * n_keys;
     // (one counter per query: a wave appends its records with one atomic; a full-library scan
     // leaves most keys set, and per-lane atomics on G counters took ~2 ms per group)
@@ -3621,7 +3621,8 @@ __global__ __launch_bounds__(256) void k_gen_write(const uint64_t* __restrict__ 
 // descending, key id ascending (hpp:397-401 with the canonical tie order).
 // A radix select over the row's encodings (11 + 11 + 10 bits) finds the L-th largest one, T;
 // a last pass in key order takes every key above T and the first keys at T, and clears the row;
-// the <= L records are sorted in LDS.
+// the <= L records are sorted in LDS. A thread reads four keys a load (rows are gen_kstride
+// apart) with the next load in flight: the passes are latency-bound at one load per round.
 __global__ __launch_bounds__(kGenSelThreads) void k_gen_select(uint32_t n_keys, uint32_t* __restrict__ kenc,
                                                               const uint32_t* __restrict__ group, SearchParams P,
                                                               uint32_t* __restrict__ out_n,
@@ -3633,9 +3634,14 @@ __global__ __launch_bounds__(kGenSelThreads) void k_gen_select(uint32_t n_keys, 
     __shared__ uint32_t s_pick[3];  // bin, count above it, records taken
     const uint32_t tid = threadIdx.x, lane = lane_id(), wid = tid >> 6;
     const uint32_t gi = blockIdx.x, q = group[gi];
-    uint32_t* K = kenc + (size_t)gi * n_keys;
+    const uint32_t n4 = gen_kstride(n_keys) / 4;
+    uint4* K4 = reinterpret_cast<uint4*>(kenc + (size_t)gi * gen_kstride(n_keys));
     const uint32_t L = min(P.limit, kGenSelCap);
-    const uint32_t n_it = (n_keys + kGenSelThreads - 1) / kGenSelThreads;
+    const uint32_t n_it = (n4 + kGenSelThreads - 1) / kGenSelThreads;
+    auto ld = [&](uint32_t it) {
+        const uint32_t i = it * kGenSelThreads + tid;
+        return i < n4 ? K4[i] : make_uint4(0, 0, 0, 0);
+    };
     uint32_t prefix = 0, mask = 0, need = L;  // need: rank of T among the keys matching prefix
     bool all = false;                          // fewer than L keys scored: take every one
     for (int pass = 0; pass < 3 && L; ++pass) {
@@ -3643,19 +3649,26 @@ __global__ __launch_bounds__(kGenSelThreads) void k_gen_select(uint32_t n_keys, 
         const uint32_t bmask = pass == 2 ? 0x3FFu : 0x7FFu;
         for (uint32_t i = tid; i < kBins; i += kGenSelThreads) hist[i] = 0;
         __syncthreads();
-        for (uint32_t it = 0, k = tid; it < n_it; ++it, k += kGenSelThreads) {
-            const uint32_t e = k < n_keys ? K[k] : 0u;
-            const bool in = e != 0 && (e & mask) == prefix;
-            const uint32_t bin = (e >> shift) & bmask;
-            // equal scores are the rule (m <= 3: a handful of distinct scores): a wave whose
-            // counted keys share one bin adds them with one LDS atomic
-            const unsigned long long b = __ballot(in);
-            if (!b) continue;
-            const uint32_t b0 = __shfl(bin, __ffsll((long long)b) - 1);
-            if (__ballot(in && bin == b0) == b) {
-                if (lane == (uint32_t)(__ffsll((long long)b) - 1)) atomicAdd(&hist[b0], (uint32_t)__popcll(b));
-            } else if (in) {
-                atomicAdd(&hist[bin], 1u);
+        uint4 nx = ld(0);
+        for (uint32_t it = 0; it < n_it; ++it) {
+            const uint4 v = nx;
+            if (it + 1 < n_it) nx = ld(it + 1);
+            const uint32_t ev[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t e = ev[j];
+                const bool in = e != 0 && (e & mask) == prefix;
+                const uint32_t bin = (e >> shift) & bmask;
+                // equal scores are the rule (m <= 3: a handful of distinct scores): a wave whose
+                // counted keys share one bin adds them with one LDS atomic
+                const unsigned long long b = __ballot(in);
+                if (!b) continue;
+                const uint32_t b0 = __shfl(bin, __ffsll((long long)b) - 1);
+                if (__ballot(in && bin == b0) == b) {
+                    if (lane == (uint32_t)(__ffsll((long long)b) - 1)) atomicAdd(&hist[b0], (uint32_t)__popcll(b));
+                } else if (in) {
+                    atomicAdd(&hist[bin], 1u);
+                }
             }
         }
         __syncthreads();
@@ -3694,25 +3707,41 @@ __global__ __launch_bounds__(kGenSelThreads) void k_gen_select(uint32_t n_keys, 
     if (tid == 0) s_pick[2] = 0;
     uint32_t eq_base = 0;
     __syncthreads();
-    for (uint32_t it = 0, k = tid; it < n_it; ++it, k += kGenSelThreads) {
-        const uint32_t e = k < n_keys ? K[k] : 0u;
-        if (e) K[k] = 0;
-        const bool gt = L && e != 0 && (all || e > T);
-        const bool eq = !all && T != 0 && e == T;
-        const unsigned long long be = __ballot(eq);
-        if (lane == 0) wcnt[wid] = (uint32_t)__popcll(be);
-        __syncthreads();
-        uint32_t before = eq_base, chunk = 0;
-        for (uint32_t w = 0; w < kWaves; ++w) {
-            const uint32_t c = wcnt[w];
-            before += w < wid ? c : 0u;
-            chunk += c;
+    uint4 nx = ld(0);
+    for (uint32_t it = 0; it < n_it; ++it) {
+        const uint4 v = nx;
+        if (it + 1 < n_it) nx = ld(it + 1);
+        const uint32_t i4 = it * kGenSelThreads + tid;
+        if (v.x | v.y | v.z | v.w) K4[i4] = make_uint4(0, 0, 0, 0);
+        const uint32_t ev[4] = {v.x, v.y, v.z, v.w};
+        uint32_t c = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) c += (!all && T != 0 && ev[j] == T) ? 1u : 0u;
+        uint32_t incl = c;  // keys at T in this thread and the wave's lanes below it
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+            const uint32_t o = __shfl_up(incl, d);
+            if (lane >= d) incl += o;
         }
-        before += rank_below(be);
+        if (lane == 63) wcnt[wid] = incl;
+        __syncthreads();
+        uint32_t before = eq_base + incl - c, chunk = 0;
+        for (uint32_t w = 0; w < kWaves; ++w) {
+            const uint32_t cw = wcnt[w];
+            before += w < wid ? cw : 0u;
+            chunk += cw;
+        }
         eq_base += chunk;
-        if (gt || (eq && before < need)) {
-            const uint32_t at = atomicAdd(&s_pick[2], 1u);
-            if (at < kGenSelCap) rec[at] = ((uint64_t)(~e) << 32) | k;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t e = ev[j];
+            const bool gt = L && e != 0 && (all || e > T);
+            const bool eq = !all && T != 0 && e == T;
+            const bool take = gt || (eq && before < need);
+            before += eq ? 1u : 0u;
+            if (take) {
+                const uint32_t at = atomicAdd(&s_pick[2], 1u);
+                if (at < kGenSelCap) rec[at] = ((uint64_t)(~e) << 32) | (i4 * 4 + j);
+            }
         }
         __syncthreads();  // (wcnt is rewritten by the next chunk)
     }
@@ -4259,8 +4288,8 @@ hipError_t run_general(const DevIndex& X, const SearchParams& P, const uint8_t* 
         hipLaunchKernelGGL(k_gen_compact, dim3(gx, G), dim3(256), 0, s, X.n_keys, W.kenc, W.list, W.lcount);
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    uint32_t counts[64];
-    if (G > 64) return hipErrorInvalidValue;
+    uint32_t counts[kGeneralMaxGroup];
+    if (G > kGeneralMaxGroup) return hipErrorInvalidValue;
     if ((e = hipMemcpyAsync(counts, W.lcount, sizeof(uint32_t) * G, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
     if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
     for (uint32_t gi = 0; gi < G; ++gi) {
