@@ -38,10 +38,18 @@ __device__ unsigned long long g_phase[48];  // [16, 32) the packed lean kernel, 
         wt_ = t_;                                                         \
     }
 #define WCOUNT(i, v) wacc_[i] += (v)
+#define WPHASE_BEGIN                                       \
+    unsigned long long wt_ = __builtin_amdgcn_s_memtime(); \
+    unsigned long long wacc_[16] = {};
+#define WPHASE_END(base) \
+    if (lane_id() == 0)  \
+        for (int i_ = 0; i_ < 16; ++i_) atomicAdd(&g_phase[(base) + i_], wacc_[i_]);
 #else
 #define WCOUNT(i, v)
 #define STAMP(i)
 #define WSTAMP(i)
+#define WPHASE_BEGIN
+#define WPHASE_END(base)
 #endif
 
 // a global (address space 1) pointer: keeps global_load addressing where a pointer passes through
@@ -368,6 +376,53 @@ __device__ __forceinline__ uint32_t pair_enc(uint2 kw, float s, bool promo_possi
     return enc;
 }
 
+// the wildcard query's answer (nGramSearch.hpp:356-369), precomputed at index time; threads
+// [tid, ...) of nthreads write it
+__device__ __forceinline__ void wild_answer(const DevIndex& X, const SearchParams& P, uint32_t q, uint32_t tid,
+                                            uint32_t nthreads, uint32_t* out_n, uint32_t* out_k, float* out_s) {
+    const uint32_t n = min(P.limit, X.n_keys);
+    const size_t ob = (size_t)q * P.out_stride;
+    for (uint32_t i = tid; i < n; i += nthreads) {
+        out_k[ob + i] = X.wild_key[i];
+        out_s[ob + i] = X.wild_score[i];
+    }
+    if (tid == 0) out_n[q] = n;
+}
+
+// searchLong's lists (nGramSearch.hpp:278-301): the query's gram occurrences with postings,
+// compacted to lanes 0..ng-1 (a gram repeated k times owns k lanes: counts with multiplicity), each
+// with its posting range and skip-table row. Every wave that calls it computes the same plan.
+template <class QF>
+__device__ __forceinline__ uint32_t gram_lists(const DevIndex& X, QF qch, uint32_t n, uint32_t lane, uint64_t& gbase,
+                                               uint32_t& glen, uint32_t& grow) {
+    gbase = 0;
+    glen = grow = 0;
+    bool have = false;
+    if (lane < n) {
+        const uint32_t code = gram_at(X, qch, lane);
+        if (code != UINT32_MAX) {
+            gbase = X.gram_off[code];
+            glen = (uint32_t)(X.gram_off[code + 1] - gbase);
+            grow = X.gram_row[code];
+            have = glen != 0;
+        }
+    }
+    const unsigned long long hb = __ballot(have);
+    const uint32_t ng = __popcll(hb);
+    uint32_t src = 0;
+    unsigned long long rest = hb;
+    for (uint32_t k = 0; k <= lane && rest; ++k) {  // lane k takes the k-th set bit
+        src = __ffsll((long long)rest) - 1;
+        rest &= rest - 1;
+    }
+    const uint64_t b2 = __shfl(gbase, (int)src);
+    const uint32_t l2 = __shfl(glen, (int)src), r2 = __shfl(grow, (int)src);
+    gbase = lane < ng ? b2 : 0;
+    glen = lane < ng ? l2 : 0;
+    grow = lane < ng ? r2 : 0;
+    return ng;
+}
+
 // ---------------------------------------------------------------- fused kernel -------
 struct FastSmem {
     uint32_t table[kTableSlots];   // (term - lo + 1) << 8 | count
@@ -622,13 +677,8 @@ __device__ void fast_one(const uint32_t q, FastSmem& S, const DevIndex& X, const
     const uint32_t L = P.limit;
     const size_t ob = (size_t)q * P.out_stride;
 
-    if (m == kQueryWildcard) {  // nGramSearch.hpp:356-369, answer precomputed at index time
-        const uint32_t n = min(L, X.n_keys);
-        for (uint32_t i = tid; i < n; i += kFastThreads) {
-            out_k[ob + i] = X.wild_key[i];
-            out_s[ob + i] = X.wild_score[i];
-        }
-        if (tid == 0) out_n[q] = n;
+    if (m == kQueryWildcard) {  // nGramSearch.hpp:356-369
+        wild_answer(X, P, q, tid, kFastThreads, out_n, out_k, out_s);
         return;
     }
     if (m == 0) {
@@ -860,15 +910,13 @@ __global__ __launch_bounds__(kFastThreads) void k_fast(DevIndex X, SearchParams 
 }
 
 // ---------------------------------------------------------------- wave kernel --------
-// Tier 1: W WAVES PER QUERY (W = 1, 2 or 4) sharing one LDS table of W x 8 KB. A query's gram
-// lists are cut into term-id parts of <= W x kWaveChunks 16-byte chunks (bucket skip table; a
-// bucket above the cap is split by lower_bound). Every wave plans the same parts (redundantly,
-// no synchronisation); wave w loads chunks [w, w+1) x kWaveChunks of each part into registers,
-// the lists' chunks packed across the wave, while the previous part is counted against the
-// shared LDS sketch / hash table with predication only. Block barriers wait for LDS only, so
-// the next part's loads stay in flight. Candidate resolution, survivors and the top-L run on
-// wave 0. A repeated query gram is kept as a separate occurrence (its list is read once per
-// occurrence), which is the reference's multiplicity (hpp:289-298).
+// Tier 1: ONE WAVE PER QUERY with a wave-private LDS table. A query's gram lists are cut into
+// term-id parts of <= kWaveChunks 16-byte chunks (bucket skip table; a bucket above the cap is
+// split by lower_bound); the wave loads a part into registers, the lists' chunks packed across
+// its lanes, while the previous part is counted against the LDS sketch / hash table with
+// predication only. A repeated query gram is kept as a separate occurrence (its list is read once
+// per occurrence), which is the reference's multiplicity (hpp:289-298). (Two and four waves per
+// query sharing one table were measured slower and are gone.)
 // LDS table geometry: tier 1a keeps 4 KB (occupancy), the full kernel 8 KB (its occupancy is
 // set by VGPRs; a bigger sketch means fewer false candidates on the heavy queries it runs)
 template <bool LEAN>
@@ -878,17 +926,17 @@ struct TableGeom {
     static constexpr int kCap = kSlots / 2;    // entries per exact-count pass (<= 50 % load)
 };
 
-template <int W, bool LEAN = false>
+template <bool LEAN = false>
 struct alignas(16) WaveSmem {
-    uint32_t table[TableGeom<LEAN>::kSlots * W];  // exact: (term - lo + 1) << 8 | count; sketch: 8 x u4 counters
+    uint32_t table[TableGeom<LEAN>::kSlots];  // exact: (term - lo + 1) << 8 | count; sketch: 8 x u4 counters
     uint64_t cand_own[LEAN ? 1 : kWaveCand];  // (~enc) << 32 | key
     // the candidate buffer; tier 1a (LEAN) fills it only after the part loop, over the dead table
     __device__ __forceinline__ uint64_t* cand() {
         if constexpr (LEAN) return reinterpret_cast<uint64_t*>(table);
         else return cand_own;
     }
-    uint2 segtab[W][64];             // staging, per wave: per list {first chunk - position, first | end entry << 16}
-    uint8_t mark[W][kWaveChunks];    // staging, per wave: list index + 1 at the (wave-local) position of its first chunk
+    uint2 segtab[64];                // staging: per list {first chunk - position, first | end entry << 16}
+    uint8_t mark[kWaveChunks];       // staging: list index + 1 at the position of its first chunk
     unsigned long long lstart[kDmaRounds];  // tier 1a staging: bit (pre - 1) per list start, 64 chunk positions a word
     uint32_t g4[LEAN ? 64 : 1];      // tier 1a: per list lane, the 16-byte chunk of its list's first posting
     uint32_t surv_t[kWaveSurv];      // survivor terms
@@ -897,9 +945,9 @@ struct alignas(16) WaveSmem {
     uint32_t q[kWaveMaxGrams + 8];   // normalised query, one code point per entry
     uint8_t peq[LEAN ? 4 : 256];     // tier 1b: Myers match masks of the query (short search)
     uint32_t surv_total;             // stats
-    uint32_t ncand;                  // sketch candidates of the part, all waves
-    uint32_t x_surv_n, x_cand_n;     // wave 0's emit state, handed round in exact-path turns
-    uint32_t xcnt;                   // exact-pass range sizing: max entries in range over the waves
+    uint32_t ncand;                  // (unused by tier 1b)
+    uint32_t x_surv_n, x_cand_n;     // tier 1a: arena blocks chained (spill_arena)
+    uint32_t xcnt;                   // ... and the one before the last
     uint64_t x_tau;
 };
 
@@ -919,18 +967,6 @@ __device__ __forceinline__ uint32_t rank_below(unsigned long long b) {
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
-}
-
-// Ordering point for LDS shared by the block's W waves: this wave's LDS operations complete,
-// then a raw s_barrier. Global loads in flight are NOT drained (no vmcnt wait), unlike
-// __syncthreads().
-template <int W>
-__device__ __forceinline__ void grp_sync() {
-    if constexpr (W == 1) {
-        wave_sync();
-    } else {
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    }
 }
 
 template <class T>
@@ -1232,8 +1268,8 @@ __device__ void wave_emit(SM& S, const DevIndex& X, const SearchParams& P, uint3
     wave_sync();
 }
 
-template <int W, bool LEAN>
-__device__ __forceinline__ void surv_append(WaveSmem<W, LEAN>& S, bool pass, uint32_t t, uint32_t code, uint32_t& surv_n) {
+template <bool LEAN>
+__device__ __forceinline__ void surv_append(WaveSmem<LEAN>& S, bool pass, uint32_t t, uint32_t code, uint32_t& surv_n) {
     const unsigned long long b = __ballot(pass);
     if (pass) {
         const uint32_t i = surv_n + rank_below(b);
@@ -1243,11 +1279,40 @@ __device__ __forceinline__ void surv_append(WaveSmem<W, LEAN>& S, bool pass, uin
     surv_n += __popcll(b);
 }
 
-template <int W, bool LEAN>
+// zero the wave's LDS table (16-byte stores, lane-strided)
+template <bool LEAN>
+__device__ __forceinline__ void clear_table(WaveSmem<LEAN>& S, uint32_t lane) {
+    uint4* T4 = reinterpret_cast<uint4*>(S.table);
+#pragma unroll
+    for (uint32_t i = 0; i < (uint32_t)TableGeom<LEAN>::kSlots / 256; ++i) T4[lane + 64 * i] = make_uint4(0, 0, 0, 0);
+}
+
+// Exact counts of a sketch part's nc <= 64 candidate entries (S.cbuf; lane l < nc takes entry l):
+// a term's count is the number of candidates holding it (every entry of a term lands in the same
+// cell), owned by the first of them. Terms whose count reaches cmin become survivors.
+template <bool LEAN>
+__device__ __forceinline__ void cand_counts(WaveSmem<LEAN>& S, uint32_t nc, uint32_t cmin, uint32_t n_short,
+                                            uint32_t n_terms, uint32_t& surv_n) {
+    const uint32_t lane = lane_id();
+    uint32_t lc = lane;  // opaque: the slot address is made here, not kept across the part loop (spilled)
+    asm volatile("" : "+v"(lc));
+    const uint32_t t = lc < nc ? S.cbuf[lc] : kStray;
+    uint32_t cnt = 0;
+    bool first = true;
+    for (uint32_t j = 0; j < nc; ++j) {
+        const uint32_t tj = __builtin_amdgcn_readlane(t, j);
+        const bool eq = t == tj;
+        cnt += eq;
+        first &= !(eq && j < lane);
+    }
+    surv_append(S, lane < nc && first && cnt >= cmin, min(n_short + t, n_terms - 1u), cnt, surv_n);
+}
+
+template <bool LEAN>
 __device__ __forceinline__ uint32_t wave_insert_slot(uint32_t* T, uint32_t rel, unsigned* err) {
-    constexpr uint32_t kSlots = TableGeom<LEAN>::kSlots * W;
+    constexpr uint32_t kSlots = TableGeom<LEAN>::kSlots;
     uint32_t probes = 0;
-    uint32_t h = (rel * 0x9E3779B1u) >> (32 - TableGeom<LEAN>::kBits - (W == 4 ? 2 : W == 2 ? 1 : 0));
+    uint32_t h = (rel * 0x9E3779B1u) >> (32 - TableGeom<LEAN>::kBits);
     const uint32_t want = rel << 8;
     for (;;) {
         uint32_t cur = T[h];
@@ -1272,66 +1337,61 @@ __device__ __forceinline__ uint32_t wave_insert_slot(uint32_t* T, uint32_t rel, 
 // are spread over a range much wider than the table, and consecutive ids get distinct cells.
 // Tier 1a takes the low bits alone (the xor fold measured 10 % slower there): its parts are contiguous term-id ranges
 // whose few hundred entries are spread over an id span far wider than the table.
-template <int W, bool LEAN>
+template <bool LEAN>
 __device__ __forceinline__ uint32_t sketch_cell(uint32_t t) {  // u4 counter index: 8 per table word
-    constexpr uint32_t kBits = TableGeom<LEAN>::kBits + 3 + (W == 4 ? 2 : W == 2 ? 1 : 0);
+    constexpr uint32_t kBits = TableGeom<LEAN>::kBits + 3;
     if constexpr (LEAN) return t & ((1u << kBits) - 1u);
     return (t ^ (t >> kBits)) & ((1u << kBits) - 1u);
 }
 // the table word holding t's cell; tier 1a's low-bit cells address it as the byte offset
 // (t >> 1) & 0xffc, two instructions (the word index form takes three)
-template <int W, bool LEAN>
+template <bool LEAN>
 __device__ __forceinline__ uint32_t* sketch_word(uint32_t* table, uint32_t t) {
-    constexpr uint32_t kBits = TableGeom<LEAN>::kBits + 3 + (W == 4 ? 2 : W == 2 ? 1 : 0);
+    constexpr uint32_t kBits = TableGeom<LEAN>::kBits + 3;
     if constexpr (LEAN)
         return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(table) + ((t >> 1) & (((1u << kBits) - 1u) >> 1 & ~3u)));
-    return table + (sketch_cell<W, LEAN>(t) >> 3);
+    return table + (sketch_cell<LEAN>(t) >> 3);
 }
 // (sketch_cell(t) & 7) * 4 in the low 5 bits, higher bits arbitrary: v_lshlrev and v_bfe_u32 read
 // only the low 5 bits of a shift / offset, so the mask is never materialised (the tier-1a kernel
 // is VALU-issue bound)
-template <int W, bool LEAN>
+template <bool LEAN>
 __device__ __forceinline__ uint32_t sketch_sh4(uint32_t t) {
-    constexpr uint32_t kBits = TableGeom<LEAN>::kBits + 3 + (W == 4 ? 2 : W == 2 ? 1 : 0);
+    constexpr uint32_t kBits = TableGeom<LEAN>::kBits + 3;
     if constexpr (LEAN) return t << 2;
     return (t ^ (t >> kBits)) << 2;
 }
 
-// Loads this wave's share of one part into registers. Lane g < ng contributes entries
-// [cur, cur + len) of its list (list base gbase, a0 = gbase % 4); the part's 16-byte chunks are
-// numbered across all lists (DPP prefix sum) and wave w takes chunks [w, w+1) x kWaveChunks,
-// lane l holding chunks l, 64 + l, ... of that range in v[0], v[1], ...: about one load
+// Loads one part into registers. Lane g < ng contributes entries [cur, cur + len) of its list
+// (list base gbase, a0 = gbase % 4); the part's 16-byte chunks are numbered across all lists (DPP
+// prefix sum), lane l holding chunks l, 64 + l, ... in v[0], v[1], ...: about one load
 // instruction per 256 postings whatever the number of lists (MI355X issues scattered loads at
 // a fixed rate per instruction). A chunk finds its list through a marker per list
 // start plus a max-scan; vmask bit 4r+e says whether entry e of v[r] belongs to the part (chunk
-// edges hold up to 3 entries of neighbouring lists). Returns this wave's chunk count; *tch_all
-// receives the part's.
-template <int W, bool LEAN>
-__device__ __forceinline__ uint32_t stage_part(WaveSmem<W, LEAN>& S, const uint4* __restrict__ post4, uint64_t gbase,
+// edges hold up to 3 entries of neighbouring lists). Returns the part's chunk count.
+template <bool LEAN>
+__device__ __forceinline__ uint32_t stage_part(WaveSmem<LEAN>& S, const uint4* __restrict__ post4, uint64_t gbase,
                                                uint32_t a0, uint32_t cur, uint32_t len,
-                                               uint4 (&v)[kDmaRounds], uint32_t& vmask, uint32_t dbg = 0) {
-    const uint32_t lane = lane_id(), wid = W == 1 ? 0u : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+                                               uint4 (&v)[kDmaRounds], uint32_t& vmask) {
+    const uint32_t lane = lane_id();
     const uint32_t head = (a0 + cur) & 3u;
     const uint32_t nch = len ? (head + len + 3) >> 2 : 0u;
     const uint32_t incl = wave_incl_scan(nch);
     const uint32_t pre = incl - nch;
     const uint32_t tch = __builtin_amdgcn_readlane(incl, 63);
-    const uint32_t c0 = wid * kWaveChunks;  // this wave's first chunk of the part
-    const uint32_t mt = __builtin_amdgcn_readfirstlane(tch > c0 ? min(tch - c0, (uint32_t)kWaveChunks) : 0u);
-    uint8_t* mk = S.mark[wid];
+    const uint32_t mt = __builtin_amdgcn_readfirstlane(min(tch, (uint32_t)kWaveChunks));
+    uint8_t* mk = S.mark;
 #pragma unroll
     for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r)
         if (64 * r < mt) mk[64 * r + lane] = 0;
     wave_sync();
     if (nch) {
-        if (pre >= c0 && pre < c0 + kWaveChunks) mk[pre - c0] = (uint8_t)(lane + 1);
+        if (pre < kWaveChunks) mk[pre] = (uint8_t)(lane + 1);
         const uint32_t first = (uint32_t)((gbase + cur) >> 2);
-        S.segtab[wid][lane] = make_uint2(first - pre, (4 * pre + head) | ((4 * pre + head + len) << 16));
+        S.segtab[lane] = make_uint2(first - pre, (4 * pre + head) | ((4 * pre + head + len) << 16));
     }
     wave_sync();
-    // the list holding this wave's first chunk may start in an earlier wave's range
-    const unsigned long long before = __ballot(nch != 0 && pre < c0);
-    uint32_t carry = before ? 64u - (uint32_t)__clzll(before) : 0u;
+    uint32_t carry = 0;
     // all rounds' max-scans are independent; the carries chain only through their lane-63
     // values, so the LDS reads and loads of the rounds can be in flight together
     uint32_t scn[kDmaRounds];
@@ -1350,16 +1410,12 @@ __device__ __forceinline__ uint32_t stage_part(WaveSmem<W, LEAN>& S, const uint4
 #pragma unroll
     for (uint32_t r = 0; r < (uint32_t)kDmaRounds; ++r) {
         if (64 * r < mt) {
-            const uint32_t lc = 64 * r + lane, c = c0 + lc;
-            const bool ok = lc < mt;
-            const uint2 seg = S.segtab[wid][(scn[r] - 1u) & 63u];
+            const uint32_t c = 64 * r + lane;
+            const bool ok = c < mt;
+            const uint2 seg = S.segtab[(scn[r] - 1u) & 63u];
             // inactive lanes must not load: a shared fallback address would be read by every wave
             // of the GPU and serialise on one L2 channel
-            if (ok && !(dbg & 8u)) v[r] = post4[seg.x + c];  // dbg 8: staging without the loads
-            else if (ok) {  // random-looking term ids (no repeats) in place of the loaded ones
-                const uint32_t hsh = (c + 0x9E3779B9u * (uint32_t)(gbase + cur)) * 0x85EBCA6Bu;
-                v[r] = make_uint4(hsh >> 8, (hsh * 0xC2B2AE35u) >> 8, (hsh * 0x27D4EB2Fu) >> 8, (hsh * 0x165667B1u) >> 8);
-            }
+            if (ok) v[r] = post4[seg.x + c];
             // entries [lo_e, hi_e) of this chunk are in the list segment [y, z)
             const int y = (int)(seg.y & 0xFFFFu), z = (int)(seg.y >> 16);
             const uint32_t lo_e = (uint32_t)min(max(y - (int)(4 * c), 0), 4);
@@ -1371,19 +1427,17 @@ __device__ __forceinline__ uint32_t stage_part(WaveSmem<W, LEAN>& S, const uint4
     return mt;
 }
 
-// Exact count of the part's entries with term ids in [ta, tb) (all waves; at most kWaveCap x W
-// of them): shared LDS hash table term -> count. Each such entry's register is replaced by
+// Exact count of the part's entries with term ids in [ta, tb) (at most kWaveCap of them): LDS
+// hash table term -> count. Each such entry's register is replaced by
 // its slot, tagged with the pass number (bit 31 | pass << 16 | slot; term ids stay below 2^31),
 // so later passes over other term ranges skip it; the extraction exchanges the slot with 0,
-// so the first holder of a term owns its count (no table scan; the table ends empty). One wave
-// (W = 1: the multi-wave variants were slower and are gone).
-template <int W, bool LEAN>
-__device__ __forceinline__ void part_exact(WaveSmem<W, LEAN>& S, uint4 (&v)[kDmaRounds], uint32_t vmask, uint32_t mt,
+// so the first holder of a term owns its count (no table scan; the table ends empty).
+template <bool LEAN>
+__device__ __forceinline__ void part_exact(WaveSmem<LEAN>& S, uint4 (&v)[kDmaRounds], uint32_t vmask, uint32_t mt,
                                            uint32_t ta, uint32_t tb, uint32_t pass, const DevIndex& X,
                                            const SearchParams& P, uint32_t m, uint32_t L, uint32_t cmin,
                                            float sc_long, float sc_short, uint32_t& surv_n, uint32_t& cand_n,
                                            uint64_t& tau, unsigned* err) {
-    static_assert(W == 1, "one wave per query");
     mt = __builtin_amdgcn_readfirstlane(mt);
     const uint32_t tag = 0x80000000u | (pass << 16);
 #pragma unroll
@@ -1393,7 +1447,7 @@ __device__ __forceinline__ void part_exact(WaveSmem<W, LEAN>& S, uint4 (&v)[kDma
             for (uint32_t e = 0; e < 4; ++e) {
                 uint32_t& x = e == 0 ? v[r].x : e == 1 ? v[r].y : e == 2 ? v[r].z : v[r].w;
                 if (((vmask >> (4 * r + e)) & 1u) && x - ta < tb - ta)
-                    x = tag | wave_insert_slot<W, LEAN>(S.table, x - ta + 1u, err);
+                    x = tag | wave_insert_slot<LEAN>(S.table, x - ta + 1u, err);
             }
         }
     }
@@ -1404,10 +1458,7 @@ __device__ __forceinline__ void part_exact(WaveSmem<W, LEAN>& S, uint4 (&v)[kDma
             uint64_t ta2 = tau;
             // one element slot per step (a single wave_emit call site keeps the registers out of scratch)
             for (uint32_t k = 0; k < 4 * (uint32_t)kDmaRounds && 64 * (k >> 2) < mt; ++k) {
-                if (sn + 64 > (uint32_t)kWaveSurv) {
-                    if (P.dbg & 64u) sn = 0;  // dbg 64 (ablation): survivors dropped, no calcScore
-                    else wave_emit(S, X, P, m, L, sc_long, sc_short, sn, cn, ta2);
-                }
+                if (sn + 64 > (uint32_t)kWaveSurv) wave_emit(S, X, P, m, L, sc_long, sc_short, sn, cn, ta2);
                 uint32_t x = kStray;
                 if (k < 16) {  // 16-way selects (k is uniform)
 #pragma unroll
@@ -1441,11 +1492,10 @@ __device__ __forceinline__ void part_exact(WaveSmem<W, LEAN>& S, uint4 (&v)[kDma
 // the wave gets their exact counts by comparing the <= 64 candidates with each other. Returns the number of candidate entries; above 64 the caller counts the part exactly
 // (the table is clean again). (u16 counters with no-return adds were measured: the 4x fewer
 // cells per KB cost more in false candidates than the returns cost in waits.)
-template <int W, bool LEAN, int NR = kDmaRounds>
-__device__ __forceinline__ uint32_t part_sketch(WaveSmem<W, LEAN>& S, const uint4 (&v)[NR], uint32_t vmask,
+template <bool LEAN, int NR = kDmaRounds>
+__device__ __forceinline__ uint32_t part_sketch(WaveSmem<LEAN>& S, const uint4 (&v)[NR], uint32_t vmask,
                                                 uint32_t mt, uint32_t cmin, uint32_t n_short, uint32_t n_terms,
-                                                uint32_t& surv_n, uint32_t dbg) {
-    static_assert(W == 1, "one wave per query");
+                                                uint32_t& surv_n) {
     const uint32_t lane = lane_id();
     mt = __builtin_amdgcn_readfirstlane(mt);
     const uint32_t cm1 = __builtin_amdgcn_readfirstlane(cmin - 1u);
@@ -1464,16 +1514,15 @@ __device__ __forceinline__ uint32_t part_sketch(WaveSmem<W, LEAN>& S, const uint
             uint32_t old[4];
 #pragma unroll
             for (uint32_t e = 0; e < 4; ++e)
-                old[e] = atomicAdd(sketch_word<W, LEAN>(S.table, t[e]), 1u << (sketch_sh4<W, LEAN>(t[e]) & 31u));
+                old[e] = atomicAdd(sketch_word<LEAN>(S.table, t[e]), 1u << (sketch_sh4<LEAN>(t[e]) & 31u));
 #pragma unroll
-            for (uint32_t e = 0; e < 4; ++e) seen = max(seen, __builtin_amdgcn_ubfe(old[e], sketch_sh4<W, LEAN>(t[e]), 4u));
+            for (uint32_t e = 0; e < 4; ++e) seen = max(seen, __builtin_amdgcn_ubfe(old[e], sketch_sh4<LEAN>(t[e]), 4u));
         }
     }
     const bool ovf = seen == kSketchMax, hot = seen >= cm1;
     wave_sync();
-    if ((dbg & 2u) || !__ballot(hot || ovf)) {  // no cell reached cmin (or dbg 2, ablation: add pass only)
-        uint4* T4 = reinterpret_cast<uint4*>(S.table);
-        for (uint32_t i = lane; i < (uint32_t)TableGeom<LEAN>::kSlots / 4; i += 64) T4[i] = make_uint4(0, 0, 0, 0);
+    if (!__ballot(hot || ovf)) {  // no cell reached cmin: no candidates
+        clear_table(S, lane);
         wave_sync();
         return 0;
     }
@@ -1488,12 +1537,12 @@ __device__ __forceinline__ uint32_t part_sketch(WaveSmem<W, LEAN>& S, const uint
             const uint32_t t[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
             uint32_t w[4];
 #pragma unroll
-            for (uint32_t e = 0; e < 4; ++e) w[e] = *sketch_word<W, LEAN>(S.table, t[e]);
+            for (uint32_t e = 0; e < 4; ++e) w[e] = *sketch_word<LEAN>(S.table, t[e]);
 #pragma unroll
             for (uint32_t e = 0; e < 4; ++e) {
                 // the entry's mask bit is tested only in the (rare) branch taken when some cell of the
                 // slot reached cmin
-                bool f = __builtin_amdgcn_ubfe(w[e], sketch_sh4<W, LEAN>(t[e]), 4u) >= cmin;
+                bool f = __builtin_amdgcn_ubfe(w[e], sketch_sh4<LEAN>(t[e]), 4u) >= cmin;
                 if (__ballot(f)) {
                     f = f && ((vmask >> (4 * r + e)) & 1u);
                     const unsigned long long b = __ballot(f);
@@ -1506,26 +1555,8 @@ __device__ __forceinline__ uint32_t part_sketch(WaveSmem<W, LEAN>& S, const uint
     }
     wave_sync();
     const uint32_t nc = __builtin_amdgcn_readfirstlane(nw + ov);
-    {
-        uint4* T4 = reinterpret_cast<uint4*>(S.table);
-        for (uint32_t i = lane; i < (uint32_t)TableGeom<LEAN>::kSlots / 4; i += 64) T4[i] = make_uint4(0, 0, 0, 0);
-    }
-    if (nc && nc <= 64 && !(dbg & 4u)) {
-        // lane l < nc holds candidate l; its term's exact count is the number of candidates with
-        // that term (every entry of a term lands in the same cell), owned by the first of them
-        uint32_t lc = lane;  // opaque: the slot address is made here, not kept across the part loop (spilled)
-        asm volatile("" : "+v"(lc));
-        const uint32_t t = lc < nc ? S.cbuf[lc] : kStray;
-        uint32_t cnt = 0;
-        bool first = true;
-        for (uint32_t j = 0; j < nc; ++j) {
-            const uint32_t tj = __builtin_amdgcn_readlane(t, j);
-            const bool eq = t == tj;
-            cnt += eq;
-            first &= !(eq && j < lane);
-        }
-        surv_append(S, lane < nc && first && cnt >= cmin, min(n_short + t, n_terms - 1u), cnt, surv_n);
-    }
+    clear_table(S, lane);
+    if (nc && nc <= 64) cand_counts(S, nc, cmin, n_short, n_terms, surv_n);
     wave_sync();
     return nc;
 }
@@ -1539,7 +1570,7 @@ __device__ __forceinline__ uint32_t part_sketch(WaveSmem<W, LEAN>& S, const uint
 // caller hands the query to tier 1b. Parts are cut to a quarter of a sketch part so that pairs
 // colliding in the 8,192 cells stay few.
 template <int NR = kDmaRounds>
-__device__ __forceinline__ uint32_t part_ones(WaveSmem<1, true>& S, const uint4 (&v)[NR], uint32_t vmask, uint32_t mt,
+__device__ __forceinline__ uint32_t part_ones(WaveSmem<true>& S, const uint4 (&v)[NR], uint32_t vmask, uint32_t mt,
                                               uint32_t n_short, uint32_t n_terms, uint32_t& surv_n,
                                               uint32_t* __restrict__ et, uint8_t* __restrict__ ec, uint32_t& spilled,
                                               uint32_t ecap) {
@@ -1553,9 +1584,9 @@ __device__ __forceinline__ uint32_t part_ones(WaveSmem<1, true>& S, const uint4 
             uint32_t old[4];  // (the four adds issued together, as in part_sketch)
 #pragma unroll
             for (uint32_t e = 0; e < 4; ++e)
-                old[e] = atomicAdd(sketch_word<1, true>(S.table, t[e]), 1u << (sketch_sh4<1, true>(t[e]) & 31u));
+                old[e] = atomicAdd(sketch_word<true>(S.table, t[e]), 1u << (sketch_sh4<true>(t[e]) & 31u));
 #pragma unroll
-            for (uint32_t e = 0; e < 4; ++e) seen = max(seen, __builtin_amdgcn_ubfe(old[e], sketch_sh4<1, true>(t[e]), 4u));
+            for (uint32_t e = 0; e < 4; ++e) seen = max(seen, __builtin_amdgcn_ubfe(old[e], sketch_sh4<true>(t[e]), 4u));
         }
     }
     const bool ovf = __ballot(seen == kSketchMax) != 0;
@@ -1568,10 +1599,10 @@ __device__ __forceinline__ uint32_t part_ones(WaveSmem<1, true>& S, const uint4 
                 const uint32_t t[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
                 uint32_t w[4];
 #pragma unroll
-                for (uint32_t e = 0; e < 4; ++e) w[e] = *sketch_word<1, true>(S.table, t[e]);
+                for (uint32_t e = 0; e < 4; ++e) w[e] = *sketch_word<true>(S.table, t[e]);
 #pragma unroll
                 for (uint32_t e = 0; e < 4; ++e) {
-                    const uint32_t c = ((vmask >> (4 * r + e)) & 1u) ? __builtin_amdgcn_ubfe(w[e], sketch_sh4<1, true>(t[e]), 4u) : 0u;
+                    const uint32_t c = ((vmask >> (4 * r + e)) & 1u) ? __builtin_amdgcn_ubfe(w[e], sketch_sh4<true>(t[e]), 4u) : 0u;
                     const bool one = c == 1, two = c >= 2;
                     const unsigned long long b1 = __ballot(one);
                     if (b1) {
@@ -1593,36 +1624,19 @@ __device__ __forceinline__ uint32_t part_ones(WaveSmem<1, true>& S, const uint4 
         }
     }
     wave_sync();
-    {
-        uint4* T4 = reinterpret_cast<uint4*>(S.table);
-        for (uint32_t i = lane; i < (uint32_t)TableGeom<true>::kSlots / 4; i += 64) T4[i] = make_uint4(0, 0, 0, 0);
-    }
+    clear_table(S, lane);
     if (ovf || nw > 64 || spilled + surv_n > ecap) {
         wave_sync();
         return 65;
     }
-    if (nw) {  // exact counts of the candidates (as part_sketch), every one of them a survivor
-        uint32_t lc = lane;  // opaque, as in part_sketch
-        asm volatile("" : "+v"(lc));
-        const uint32_t t = lc < nw ? S.cbuf[lc] : kStray;
-        uint32_t cnt = 0;
-        bool first = true;
-        for (uint32_t j = 0; j < nw; ++j) {
-            const uint32_t tj = __builtin_amdgcn_readlane(t, j);
-            const bool eq = t == tj;
-            cnt += eq;
-            first &= !(eq && j < lane);
-        }
-        surv_append(S, lane < nw && first, min(n_short + t, n_terms - 1u), cnt, surv_n);
-    }
+    if (nw) cand_counts(S, nw, 1u, n_short, n_terms, surv_n);  // (every candidate a survivor)
     wave_sync();
     return nw;
 }
 
-// One query on W waves: tier 1b (the full wave kernel, k_wave) and the server kernel. Tier 1a's
+// One query on one wave: tier 1b (the full wave kernel, k_wave) and the server kernel. Tier 1a's
 // lean kernel has part loops of its own (lean_query, lean_query_g).
-template <int W, bool LEAN = false>
-__device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t q, const DevIndex& X, const SearchParams& P,
+__device__ __forceinline__ void wave_query(WaveSmem<>& S, const uint32_t q, const DevIndex& X, const SearchParams& P,
                                            const uint8_t* __restrict__ qnorm, const uint64_t* __restrict__ qoff,
                                            const uint32_t* __restrict__ qm, uint32_t* __restrict__ out_n,
                                            uint32_t* __restrict__ out_k, float* __restrict__ out_s,
@@ -1633,8 +1647,7 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
     const uint32_t lane = lane_id(), tid = threadIdx.x;
     // sliced tier 1b: this wave takes the term ids of skip-table buckets [K * slice / nsl,
     // K * (slice + 1) / nsl) and leaves its top-L records for k_merge (SearchParams.prec)
-    static_assert(!LEAN, "tier 1a runs lean_query / lean_query_g");
-    const bool sliced = W == 1 && nsl > 1;
+    const bool sliced = nsl > 1;
     if (sliced) {  // queries answered without the long search: slice 0 answers, k_merge skips them
         const uint32_t m0 = qm[q];
         const bool direct = m0 == kQueryWildcard || m0 == 0 || m0 <= X.full_scan_len ||
@@ -1646,18 +1659,12 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
     }
     (void)fb;
     (void)fbc;
-    const uint32_t wid = W == 1 ? 0u : __builtin_amdgcn_readfirstlane(tid >> 6);
     // m_in_lds: the caller (k_serve) put the normalised query in S.q already
     const uint32_t m = m_in_lds != kQueryInGlobal ? m_in_lds : qm[q];
     const uint32_t L = P.limit;
     const size_t ob = (size_t)q * P.out_stride;
-    if (m == kQueryWildcard) {  // nGramSearch.hpp:356-369, answer precomputed at index time
-        const uint32_t n = min(L, X.n_keys);
-        for (uint32_t i = tid; i < n; i += 64 * W) {
-            out_k[ob + i] = X.wild_key[i];
-            out_s[ob + i] = X.wild_score[i];
-        }
-        if (tid == 0) out_n[q] = n;
+    if (m == kQueryWildcard) {  // nGramSearch.hpp:356-369
+        wild_answer(X, P, q, tid, 64, out_n, out_k, out_s);
         return;
     }
     if (m == 0) {  // nothing left after normalisation, nGramSearch.hpp:374-375
@@ -1670,24 +1677,18 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
     }
     const uint32_t n = m - X.gsz + 1;  // grams of the query (hpp:29-36; 3-grams: m - 2)
     const uint32_t n_long = X.n_terms - X.n_short;
-#ifdef NGS_PHASE_STAMPS
-    unsigned long long wt_ = __builtin_amdgcn_s_memtime();
-    unsigned long long wacc_[16] = {};
-#endif
+    WPHASE_BEGIN
     if (m_in_lds == kQueryInGlobal) {
         const uint8_t* qg = qnorm + qoff[q];
-        for (uint32_t i = tid; i < m; i += 64 * W) S.q[i] = char_at(qg, i, X.csize);
+        for (uint32_t i = tid; i < m; i += 64) S.q[i] = char_at(qg, i, X.csize);
     }
     if (tid == 0) {
         S.surv_total = 0;
         S.ncand = 0;
         S.xcnt = 0;
     }
-    {
-        uint4* T4 = reinterpret_cast<uint4*>(S.table);
-        for (uint32_t i = tid; i < (uint32_t)TableGeom<LEAN>::kSlots * W / 4; i += 64 * W) T4[i] = make_uint4(0, 0, 0, 0);
-    }
-    grp_sync<W>();
+    clear_table(S, lane);
+    wave_sync();
     uint32_t cand_n = 0, surv_n = 0;
     uint64_t tau = kNoCand;
     unsigned* err = &stats->errors;
@@ -1699,7 +1700,7 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
     const uint32_t cmin = pm ? (uint32_t)(__ffsll((long long)pm) - 1) : 1000u;
 
     // ---- searchShort over shortLib (nGramSearch.hpp:262-270), 4 <= m < 9, wave 0 ----
-    if (wid == 0 && slice == 0 && m < X.short_query_len && X.n_short) {
+    if (slice == 0 && m < X.short_query_len && X.n_short) {
         uint32_t qc[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) qc[i] = (uint32_t)i < m ? S.q[i] : 0;
@@ -1759,33 +1760,9 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
     // lane i: occurrence i of a query gram; lanes 0..ng-1 then own the occurrences whose gram
     // has postings (a gram repeated k times owns k lanes: count with multiplicity). Every wave
     // computes the same plan.
-    uint64_t gbase = 0;
-    uint32_t glen = 0, grow = 0;
-    bool have = false;
-    if (lane < n) {
-        const uint32_t code = gram_at(X, [&](uint32_t i) { return S.q[i]; }, lane);
-        if (code != UINT32_MAX) {
-            gbase = X.gram_off[code];
-            glen = (uint32_t)(X.gram_off[code + 1] - gbase);
-            grow = X.gram_row[code];
-            have = glen != 0;
-        }
-    }
-    const unsigned long long hb = __ballot(have);
-    const uint32_t ng = __popcll(hb);
-    {
-        uint32_t src = 0;
-        unsigned long long rest = hb;
-        for (uint32_t k = 0; k <= lane && rest; ++k) {  // lane k takes the k-th set bit
-            src = __ffsll((long long)rest) - 1;
-            rest &= rest - 1;
-        }
-        const uint64_t b2 = __shfl(gbase, (int)src);
-        const uint32_t l2 = __shfl(glen, (int)src), r2 = __shfl(grow, (int)src);
-        gbase = lane < ng ? b2 : 0;
-        glen = lane < ng ? l2 : 0;
-        grow = lane < ng ? r2 : 0;
-    }
+    uint64_t gbase;
+    uint32_t glen, grow;
+    const uint32_t ng = gram_lists(X, [&](uint32_t i) { return S.q[i]; }, n, lane, gbase, glen, grow);
     const uint64_t p_total = wave_sum((uint64_t)glen);
     uint64_t p_stat = p_total;  // postings this wave reads (its slice's)
     // sketch counting for 2 <= cmin <= 15; at cmin 2 two colliding entries already make a false
@@ -1793,12 +1770,12 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
     const bool sketch = cmin >= kSketchMinCmin && cmin <= kSketchMax;
     const uint32_t shrink = 0;  // (tier 1b counts cmin-2 parts in full: half-size parts measured no faster)
     // part cap: a sketch part holds twice the entries of an exact pass (u8 vs u32 cells)
-    const uint32_t kChunks = ((sketch ? (uint32_t)kWaveChunks : (uint32_t)kExactChunks) * W) >> shrink;
+    const uint32_t kChunks = (sketch ? (uint32_t)kWaveChunks : (uint32_t)kExactChunks) >> shrink;
     WSTAMP(1);
     if (p_total && cmin <= n) {
         const uint32_t K = X.n_buckets, span = X.bucket_span;
         const uint32_t wmax = (uint32_t)max64(1, min64(K, kMaxPartSpan / max(span, 1u)));
-        const uint32_t w = (uint32_t)max64(1, min64(wmax, (uint64_t)K * ((sketch ? kSketchTarget : kWaveTarget) >> shrink) * W / p_total));
+        const uint32_t w = (uint32_t)max64(1, min64(wmax, (uint64_t)K * ((sketch ? kSketchTarget : kWaveTarget) >> shrink) / p_total));
         const uint32_t* sk = X.skip + (size_t)grow * (K + 1);
         const uint4* post4 = reinterpret_cast<const uint4*>(X.post);
         const uint32_t a0 = (uint32_t)gbase & 3u;  // list start within its 16-byte chunk
@@ -1930,25 +1907,21 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
             have_p = __builtin_amdgcn_readfirstlane(have_p ? 1u : 0u) != 0;  // uniform: scalar loop exit
             // ---- part i+1: issue this wave's loads ----
             if (have_p) {
-                p_mt = stage_part(S, post4, gbase, a0, cur, len, pv, p_vm, P.dbg);
+                p_mt = stage_part(S, post4, gbase, a0, cur, len, pv, p_vm);
                 p_lo = lo;
                 p_hi = hi_t;
                 cur += len;
             }
             WSTAMP(4);
             // ---- count part i while part i+1 is in flight ----
-            if (have_c && !(P.dbg & 1u)) {  // dbg 1: load only, no counting
-                if (wid == 0 && surv_n + 64 > (uint32_t)kWaveSurv)
-                    wave_emit(S, X, P, m, L, sc_long, sc_short, surv_n, cand_n, tau);
+            if (have_c) {
+                if (surv_n + 64 > (uint32_t)kWaveSurv) wave_emit(S, X, P, m, L, sc_long, sc_short, surv_n, cand_n, tau);
                 // the count this part must reach: cmin, raised once the running top-L is full and
-                // a term of fewer hits could not enter it (tier 1b, one wave)
-                uint32_t ceff = cmin;
-                if constexpr (W == 1) {
-                    if (!(P.dbg & 128u)) ceff = raised_cmin(S, X, P, m, n, L, cmin, sc_long, sc_short, surv_n, cand_n, tau);
-                }
+                // a term of fewer hits could not enter it
+                const uint32_t ceff = raised_cmin(S, X, P, m, n, L, cmin, sc_long, sc_short, surv_n, cand_n, tau);
                 // (survivors must pass the threshold exactly: no sketch past its u4 range)
                 const bool sk = ceff >= kSketchMinCmin && ceff <= kSketchMax;
-                const uint32_t nc = sk ? part_sketch(S, cv, c_vm, c_mt, ceff, X.n_short, X.n_terms, surv_n, P.dbg) : 65u;
+                const uint32_t nc = sk ? part_sketch(S, cv, c_vm, c_mt, ceff, X.n_short, X.n_terms, surv_n) : 65u;
                 const bool done = nc <= 64;
                 WCOUNT(11, 1);
                 WCOUNT(12, done ? 0 : 1);
@@ -1956,8 +1929,8 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
                 WCOUNT(14, c_mt);
                 WSTAMP(5);
                 if (!done) {
-                    // exact count in term-id ranges of <= kWaveCap entries per wave (one range unless a
-                    // sketch part overflowed)
+                    // exact count in term-id ranges of <= kWaveCap entries (one range unless a sketch
+                    // part overflowed)
                     const uint32_t mtu = __builtin_amdgcn_readfirstlane(c_mt);
                     uint32_t ta = c_lo, pass = 0;
                     while (ta < c_hi) {
@@ -1974,14 +1947,7 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
                                 }
                             }
                             cnt = wave_sum_u32(cnt);
-                            if constexpr (W > 1) {  // the largest share over the waves decides
-                                if (lane == 0) atomicMax(&S.xcnt, cnt);
-                                grp_sync<W>();
-                                cnt = __builtin_amdgcn_readfirstlane(S.xcnt);
-                                grp_sync<W>();
-                                if (wid == 0 && lane == 0) S.xcnt = 0;
-                            }
-                            if (cnt <= (uint32_t)TableGeom<LEAN>::kCap || tb - ta <= 1) break;
+                            if (cnt <= (uint32_t)TableGeom<false>::kCap || tb - ta <= 1) break;
                             tb = ta + (tb - ta) / 2;
                         }
                         part_exact(S, cv, c_vm, c_mt, ta, tb, pass++, X, P, m, L, ceff, sc_long, sc_short, surv_n,
@@ -1995,7 +1961,6 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
         }
     }
     WSTAMP(7);
-    if (wid != 0) return;
     if (surv_n) wave_emit(S, X, P, m, L, sc_long, sc_short, surv_n, cand_n, tau);
     WSTAMP(8);
     wave_flush(S, cand_n, tau, L, X.keys_unique != 0);
@@ -2033,13 +1998,10 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
         atomicAdd(&sl->survivors, (unsigned long long)S.surv_total);
     }
     WSTAMP(10);
-#ifdef NGS_PHASE_STAMPS
-    if (lane == 0)
-        for (int i = 0; i < 16; ++i) atomicAdd(&g_phase[16 + i], wacc_[i]);
-#endif
+    WPHASE_END(16)
 }
 
-// Tier 1a's staging of one part into registers (W = 1). Lane g < ng brings entries [cur, cur + len)
+// Tier 1a's staging of one part into registers. Lane g < ng brings entries [cur, cur + len)
 // of its list: nch 16-byte chunks from position pre = incl - nch of the part's packed chunk
 // numbering on (incl: the planner's inclusive prefix sum, mt chunks in all). Lane l loads chunks
 // l, 64 + l, ... . A chunk finds its list by counting the list starts below it: every non-empty
@@ -2048,7 +2010,7 @@ __device__ __forceinline__ void wave_query(WaveSmem<W, LEAN>& S, const uint32_t 
 // non-empty lists' {first chunk - pre, entry bounds} sit in segtab by ordinal. (stage_part, the
 // full kernel's staging, spends a marker array and a max-scan per round on the same lookup.)
 template <bool G4>
-__device__ __forceinline__ void lean_stage(WaveSmem<1, true>& S, gptr<uint4> post4, uint64_t gbase,
+__device__ __forceinline__ void lean_stage(WaveSmem<true>& S, gptr<uint4> post4, uint64_t gbase,
                                            uint32_t a0, uint32_t cur, uint32_t len, uint32_t nch, uint32_t incl,
                                            uint32_t mt, uint4 (&v)[kDmaRounds], uint32_t& vmask) {
     const uint32_t lane = lane_id();
@@ -2079,7 +2041,7 @@ __device__ __forceinline__ void lean_stage(WaveSmem<1, true>& S, gptr<uint4> pos
     if (nch) {
         if (pre) atomicOr(&S.lstart[(pre - 1) >> 6], 1ull << ((pre - 1) & 63u));
         const uint32_t first = g4 + ((a0 + cur) >> 2);  // the list's chunk base (u32: chunk ids < 2^32)
-        S.segtab[0][ord] = make_uint2(first - pre, (4 * pre + head) | ((4 * pre + head + len) << 16));
+        S.segtab[ord] = make_uint2(first - pre, (4 * pre + head) | ((4 * pre + head + len) << 16));
     }
     wave_sync();
     uint32_t below = 0;  // list starts in the earlier words
@@ -2096,7 +2058,7 @@ __device__ __forceinline__ void lean_stage(WaveSmem<1, true>& S, gptr<uint4> pos
             below += (uint32_t)__popc(wlo) + (uint32_t)__popc(whi);
             const uint32_t c = 64 * r + lo;
             const bool ok = c < mt;
-            const uint2 seg = S.segtab[0][idx & 63u];
+            const uint2 seg = S.segtab[idx & 63u];
             if (ok) v[r] = post4[seg.x + c];  // inactive lanes load nothing
             // entries [lo_e, hi_e) of this chunk are in the list segment [y, z)
             const int y = (int)(seg.y & 0xFFFFu), z = (int)(seg.y >> 16);
@@ -2108,12 +2070,69 @@ __device__ __forceinline__ void lean_stage(WaveSmem<1, true>& S, gptr<uint4> pos
     }
 }
 
+// Tier 1a's routing of query q (both lean paths; slice slc of a sliced heavy query): the
+// wildcard, empty queries and those past tier 1's gram and limit bounds are answered or listed
+// for tier 2 by slice 0, and queries of the other launch (heavy_class: same test, same cmin) are
+// left to it. Returns kLeanDone for those, kLeanShort for a short-search query (tier 1b), and
+// kLeanCount otherwise, with S.q holding the query, the table clear, and lanes 0..ng-1 its lists.
+constexpr uint32_t kLeanDone = 0, kLeanShort = 1, kLeanCount = 2;
+struct LeanPlan {
+    uint32_t m, n, cmin, ng, glen, grow;
+    bool rank;
+    uint64_t gbase, p_total;
+};
+__device__ __forceinline__ uint32_t lean_route(WaveSmem<true>& S, const uint32_t q, const DevIndex& X,
+                                               const SearchParams& P, const uint8_t* __restrict__ qnorm,
+                                               const uint64_t* __restrict__ qoff, const uint32_t* __restrict__ qm,
+                                               uint32_t* __restrict__ out_n, uint32_t* __restrict__ out_k,
+                                               float* __restrict__ out_s, uint32_t* __restrict__ list2,
+                                               uint32_t* __restrict__ count2, uint32_t slc, LeanPlan& lp) {
+    const uint32_t lane = lane_id();
+    const uint32_t m = qm[q];
+    if (m == kQueryWildcard) {  // nGramSearch.hpp:356-369
+        if (!slc) wild_answer(X, P, q, lane, 64, out_n, out_k, out_s);
+        return kLeanDone;
+    }
+    if (m == 0) {  // nothing left after normalisation, nGramSearch.hpp:374-375
+        if (lane == 0 && !slc) out_n[q] = 0;
+        return kLeanDone;
+    }
+    if (m <= X.full_scan_len || m - X.gsz + 1 > kWaveMaxGrams || P.limit > kWaveMaxLimit) {
+        if (lane == 0 && !slc) list2[atomicAdd(count2, 1u)] = q;  // tier 2 / library-wide path
+        return kLeanDone;
+    }
+    const uint32_t n = m - X.gsz + 1;  // grams of the query (hpp:29-36)
+    // lane c holds the fp32 score of c hits, (float)c / n (hpp:300); the smallest passing count
+    const float sc_long = lane <= n ? (float)lane / (float)n : 0.0f;
+    const unsigned long long pm = __ballot(lane <= n && lane > 0 && !(sc_long < P.thr));
+    // threshold 0 with rank lists: the multi-hit terms only, k_emit adds the one-hit records
+    // (emit_rank_prefix)
+    const bool rank = X.rank_post && (pm & 2ull);
+    const uint32_t cmin = pm ? (rank ? 2u : (uint32_t)(__ffsll((long long)pm) - 1)) : 1000u;
+    const bool short_search = m < X.short_query_len && X.n_short;
+    if (!P.lean_all && (cmin <= kHeavyCmin || short_search)) return kLeanDone;
+    if (short_search) return kLeanShort;
+    const uint8_t* qg = qnorm + qoff[q];
+    for (uint32_t i = lane; i < m; i += 64) S.q[i] = char_at(qg, i, X.csize);
+    if (lane == 0) S.x_surv_n = 0;  // no arena blocks chained (spill_arena)
+    clear_table(S, lane);
+    wave_sync();
+    // ---- searchLong (nGramSearch.hpp:278-301) ----
+    lp.ng = gram_lists(X, [&](uint32_t i) { return S.q[i]; }, n, lane, lp.gbase, lp.glen, lp.grow);
+    lp.p_total = wave_sum((uint64_t)lp.glen);
+    lp.m = m;
+    lp.n = n;
+    lp.cmin = cmin;
+    lp.rank = rank;
+    return kLeanCount;
+}
+
 // Tier 1a (LEAN, DEFER): one wave per query, sketch counting only, survivors spilled to HBM for
 // k_emit. The full kernel's part loop (bucket groups, term-id sub-parts, loads one part ahead)
 // with its own staging (lean_stage) and the sketch counter part_sketch; a query that needs exact
 // counting, a short search or more than kEmitCap survivor slots is handed to tier 1b untouched.
 template <bool ONES>
-__device__ __forceinline__ void lean_query(WaveSmem<1, true>& S, const uint32_t q, const DevIndex& X,
+__device__ __forceinline__ void lean_query(WaveSmem<true>& S, const uint32_t q, const DevIndex& X,
                                            const SearchParams& P, const uint8_t* __restrict__ qnorm,
                                            const uint64_t* __restrict__ qoff, const uint32_t* __restrict__ qm,
                                            uint32_t* __restrict__ out_n, uint32_t* __restrict__ out_k,
@@ -2145,84 +2164,17 @@ __device__ __forceinline__ void lean_query(WaveSmem<1, true>& S, const uint32_t 
         }
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     };
-    const uint32_t m = qm[q];
-    const uint32_t L = P.limit;
-    // (the whole-query cases below are slice 0's)
-    if (m == kQueryWildcard) {  // nGramSearch.hpp:356-369, answer precomputed at index time
-        if (slc) return;
-        const uint32_t nk = min(L, X.n_keys);
-        const size_t ob = (size_t)q * P.out_stride;
-        for (uint32_t i = lane; i < nk; i += 64) {
-            out_k[ob + i] = X.wild_key[i];
-            out_s[ob + i] = X.wild_score[i];
-        }
-        if (lane == 0) out_n[q] = nk;
+    WPHASE_BEGIN
+    LeanPlan lp;
+    const uint32_t route = lean_route(S, q, X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, slc, lp);
+    if (route != kLeanCount) {
+        if (route == kLeanShort && !slc) bail();  // short search: tier 1b
         return;
     }
-    if (m == 0) {  // nothing left after normalisation, nGramSearch.hpp:374-375
-        if (lane == 0 && !slc) out_n[q] = 0;
-        return;
-    }
-    if (m <= X.full_scan_len || m - X.gsz + 1 > kWaveMaxGrams || L > kWaveMaxLimit) {
-        if (lane == 0 && !slc) list2[atomicAdd(count2, 1u)] = q;  // tier 2 / library-wide path
-        return;
-    }
-    const uint32_t n = m - X.gsz + 1;  // grams of the query (hpp:29-36)
+    const uint32_t L = P.limit, n = lp.n, cmin = lp.cmin, ng = lp.ng, glen = lp.glen, grow = lp.grow;
     const uint32_t n_long = X.n_terms - X.n_short;
-#ifdef NGS_PHASE_STAMPS
-    unsigned long long wt_ = __builtin_amdgcn_s_memtime();
-    unsigned long long wacc_[16] = {};
-#endif
-    // lane c holds the fp32 score of c hits, (float)c / n (hpp:300); the smallest passing count
-    const float sc_long = lane <= n ? (float)lane / (float)n : 0.0f;
-    const unsigned long long pm = __ballot(lane <= n && lane > 0 && !(sc_long < P.thr));
-    // threshold 0 with rank lists: the multi-hit terms only, k_emit adds the one-hit records
-    // (emit_rank_prefix)
-    const bool rank = X.rank_post && (pm & 2ull);
-    const uint32_t cmin = pm ? (rank ? 2u : (uint32_t)(__ffsll((long long)pm) - 1)) : 1000u;
-    // heavy_class() lists these for launches of their own (same test, same cmin)
-    if (!P.lean_all && (cmin <= kHeavyCmin || (m < X.short_query_len && X.n_short))) return;
-    if (m < X.short_query_len && X.n_short) {  // short search: tier 1b
-        if (!slc) bail();
-        return;
-    }
-    const uint8_t* qg = qnorm + qoff[q];
-    for (uint32_t i = lane; i < m; i += 64) S.q[i] = char_at(qg, i, X.csize);
-    {
-        uint4* T4 = reinterpret_cast<uint4*>(S.table);
-        for (uint32_t i = lane; i < (uint32_t)kWaveSlots / 4; i += 64) T4[i] = make_uint4(0, 0, 0, 0);
-    }
-    wave_sync();
-    // ---- searchLong (nGramSearch.hpp:278-301): lanes 0..ng-1 own the gram occurrences with
-    // postings (a gram repeated k times owns k lanes: counts with multiplicity) ----
-    uint64_t gbase = 0;
-    uint32_t glen = 0, grow = 0;
-    bool have = false;
-    if (lane < n) {
-        const uint32_t code = gram_at(X, [&](uint32_t i) { return S.q[i]; }, lane);
-        if (code != UINT32_MAX) {
-            gbase = X.gram_off[code];
-            glen = (uint32_t)(X.gram_off[code + 1] - gbase);
-            grow = X.gram_row[code];
-            have = glen != 0;
-        }
-    }
-    const unsigned long long hb = __ballot(have);
-    const uint32_t ng = __popcll(hb);
-    {
-        uint32_t src = 0;
-        unsigned long long rest = hb;
-        for (uint32_t k = 0; k <= lane && rest; ++k) {  // lane k takes the k-th set bit
-            src = __ffsll((long long)rest) - 1;
-            rest &= rest - 1;
-        }
-        const uint64_t b2 = __shfl(gbase, (int)src);
-        const uint32_t l2 = __shfl(glen, (int)src), r2 = __shfl(grow, (int)src);
-        gbase = lane < ng ? b2 : 0;
-        glen = lane < ng ? l2 : 0;
-        grow = lane < ng ? r2 : 0;
-    }
-    const uint64_t p_total = wave_sum((uint64_t)glen);
+    const bool rank = lp.rank;
+    const uint64_t gbase = lp.gbase, p_total = lp.p_total;
     WSTAMP(0);
     const bool sketch = cmin >= kSketchMinCmin && cmin <= kSketchMax;
     const bool ones = ONES && cmin == 1;  // part_ones (the heavy list's launch only)
@@ -2420,10 +2372,10 @@ __device__ __forceinline__ void lean_query(WaveSmem<1, true>& S, const uint32_t 
                     asm volatile("" : "+s"(qs));
                     nc = ones ? part_ones(S, cv, c_vm, c_mt, X.n_short, X.n_terms, surv_n, P.est + (size_t)qs * P.ecap,
                                           P.esc + (size_t)qs * P.ecap, spilled, P.ecap)
-                              : part_sketch(S, cv, c_vm, c_mt, cmin, X.n_short, X.n_terms, surv_n, P.dbg);
+                              : part_sketch(S, cv, c_vm, c_mt, cmin, X.n_short, X.n_terms, surv_n);
                 }
                 else
-                    nc = part_sketch(S, cv, c_vm, c_mt, cmin, X.n_short, X.n_terms, surv_n, P.dbg);
+                    nc = part_sketch(S, cv, c_vm, c_mt, cmin, X.n_short, X.n_terms, surv_n);
                 WCOUNT(11, 1);
                 WCOUNT(13, (c_mt + 63) / 64);
                 WCOUNT(14, nc);
@@ -2436,10 +2388,7 @@ __device__ __forceinline__ void lean_query(WaveSmem<1, true>& S, const uint32_t 
     }
     if (!spill()) { slot_full(); bail(); return; }
     WSTAMP(6);
-#ifdef NGS_PHASE_STAMPS
-    if (lane == 0)
-        for (int i = 0; i < 16; ++i) atomicAdd(&g_phase[16 + i], wacc_[i]);
-#endif
+    WPHASE_END(16)
     if (nslq > 1) finish_slice();
     else if (lane == 0) P.esn[q] = spilled | (P.lean_all ? kEmitHeavy : 0u);
     if (lane == 0 && !(P.dbg & 32u)) {
@@ -2463,7 +2412,7 @@ __device__ __forceinline__ void lean_query(WaveSmem<1, true>& S, const uint32_t 
 // undercount): entry e of chunk k is in the segment iff 4k + e - head < len.
 
 // sketch count of a part staged by lane groups (3 <= cmin <= 15): part_sketch's one-wave loose path
-__device__ __forceinline__ uint32_t lean_sketch_g(WaveSmem<1, true>& S, const uint4 (&v)[kDmaRounds], uint32_t R,
+__device__ __forceinline__ uint32_t lean_sketch_g(WaveSmem<true>& S, const uint4 (&v)[kDmaRounds], uint32_t R,
                                                   uint32_t k0, uint32_t G, uint32_t nch, uint32_t head, uint32_t len,
                                                   uint32_t cmin, uint32_t n_short, uint32_t n_terms, uint32_t& surv_n) {
     const uint32_t lane = lane_id();
@@ -2477,17 +2426,15 @@ __device__ __forceinline__ uint32_t lean_sketch_g(WaveSmem<1, true>& S, const ui
             uint32_t old[4];
 #pragma unroll
             for (uint32_t e = 0; e < 4; ++e)
-                old[e] = atomicAdd(sketch_word<1, true>(S.table, t[e]), 1u << (sketch_sh4<1, true>(t[e]) & 31u));
+                old[e] = atomicAdd(sketch_word<true>(S.table, t[e]), 1u << (sketch_sh4<true>(t[e]) & 31u));
 #pragma unroll
-            for (uint32_t e = 0; e < 4; ++e) seen = max(seen, __builtin_amdgcn_ubfe(old[e], sketch_sh4<1, true>(t[e]), 4u));
+            for (uint32_t e = 0; e < 4; ++e) seen = max(seen, __builtin_amdgcn_ubfe(old[e], sketch_sh4<true>(t[e]), 4u));
         }
     }
     const bool ovf = seen == kSketchMax, hot = seen >= cm1;
     wave_sync();
-    uint4* T4 = reinterpret_cast<uint4*>(S.table);
     if (!__ballot(hot || ovf)) {  // no cell reached cmin: no candidates
-#pragma unroll
-        for (uint32_t i = 0; i < (uint32_t)kWaveSlots / 256; ++i) T4[lane + 64 * i] = make_uint4(0, 0, 0, 0);
+        clear_table(S, lane);
         wave_sync();
         return 0;
     }
@@ -2499,10 +2446,10 @@ __device__ __forceinline__ uint32_t lean_sketch_g(WaveSmem<1, true>& S, const ui
             const uint32_t t[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
             uint32_t w[4];
 #pragma unroll
-            for (uint32_t e = 0; e < 4; ++e) w[e] = *sketch_word<1, true>(S.table, t[e]);
+            for (uint32_t e = 0; e < 4; ++e) w[e] = *sketch_word<true>(S.table, t[e]);
 #pragma unroll
             for (uint32_t e = 0; e < 4; ++e) {
-                bool f = __builtin_amdgcn_ubfe(w[e], sketch_sh4<1, true>(t[e]), 4u) >= cmin;
+                bool f = __builtin_amdgcn_ubfe(w[e], sketch_sh4<true>(t[e]), 4u) >= cmin;
                 if (__ballot(f)) {  // rare: the entry's segment bounds (and chunks not loaded) only here
                     uint32_t kk = k0;  // opaque: the round's entry offset is made here, not kept across the part loop
                     asm volatile("" : "+v"(kk));
@@ -2517,24 +2464,8 @@ __device__ __forceinline__ uint32_t lean_sketch_g(WaveSmem<1, true>& S, const ui
     }
     const uint32_t nc = nw + ov;
     wave_sync();
-#pragma unroll
-    for (uint32_t i = 0; i < (uint32_t)kWaveSlots / 256; ++i) T4[lane + 64 * i] = make_uint4(0, 0, 0, 0);
-    if (nc && nc <= 64) {
-        // lane l < nc holds candidate l; its term's exact count is the number of candidates with
-        // that term (every entry of a term lands in the same cell), owned by the first of them
-        uint32_t lc = lane;  // opaque: the slot address is made here, not kept across the part loop
-        asm volatile("" : "+v"(lc));
-        const uint32_t t = lc < nc ? S.cbuf[lc] : kStray;
-        uint32_t cnt = 0;
-        bool first = true;
-        for (uint32_t j = 0; j < nc; ++j) {
-            const uint32_t tj = __builtin_amdgcn_readlane(t, j);
-            const bool eq = t == tj;
-            cnt += eq;
-            first &= !(eq && j < lane);
-        }
-        surv_append(S, lane < nc && first && cnt >= cmin, min(n_short + t, n_terms - 1u), cnt, surv_n);
-    }
+    clear_table(S, lane);
+    if (nc && nc <= 64) cand_counts(S, nc, cmin, n_short, n_terms, surv_n);
     wave_sync();
     return nc;
 }
@@ -2545,8 +2476,7 @@ struct PartGroups {
     uint32_t nch, head, len, R;
 };
 
-template <bool ONES>
-__device__ __forceinline__ void lean_query_g(WaveSmem<1, true>& S, const uint32_t q, const DevIndex& X,
+__device__ __forceinline__ void lean_query_g(WaveSmem<true>& S, const uint32_t q, const DevIndex& X,
                                              const SearchParams& P, const uint8_t* __restrict__ qnorm,
                                              const uint64_t* __restrict__ qoff, const uint32_t* __restrict__ qm,
                                              uint32_t* __restrict__ out_n, uint32_t* __restrict__ out_k,
@@ -2558,84 +2488,19 @@ __device__ __forceinline__ void lean_query_g(WaveSmem<1, true>& S, const uint32_
         if (lane == 0) fb[atomicAdd(fbc, 1u)] = q;
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     };
-    const uint32_t m = qm[q];
-    const uint32_t L = P.limit;
-    if (m == kQueryWildcard) {  // nGramSearch.hpp:356-369, answer precomputed at index time
-        const uint32_t nk = min(L, X.n_keys);
-        const size_t ob = (size_t)q * P.out_stride;
-        for (uint32_t i = lane; i < nk; i += 64) {
-            out_k[ob + i] = X.wild_key[i];
-            out_s[ob + i] = X.wild_score[i];
-        }
-        if (lane == 0) out_n[q] = nk;
+    WPHASE_BEGIN
+    LeanPlan lp;
+    const uint32_t route = lean_route(S, q, X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, 0u, lp);
+    if (route != kLeanCount) {
+        if (route == kLeanShort) bail();  // short search: tier 1b
         return;
     }
-    if (m == 0) {  // nothing left after normalisation, nGramSearch.hpp:374-375
-        if (lane == 0) out_n[q] = 0;
-        return;
-    }
-    if (m <= X.full_scan_len || m - X.gsz + 1 > kWaveMaxGrams || L > kWaveMaxLimit) {
-        if (lane == 0) list2[atomicAdd(count2, 1u)] = q;  // tier 2 / library-wide path
-        return;
-    }
-    const uint32_t n = m - X.gsz + 1;  // grams of the query (hpp:29-36)
+    const uint32_t L = P.limit, n = lp.n, cmin = lp.cmin, ng = lp.ng, glen = lp.glen, grow = lp.grow;
     const uint32_t n_long = X.n_terms - X.n_short;
-#ifdef NGS_PHASE_STAMPS
-    unsigned long long wt_ = __builtin_amdgcn_s_memtime();
-    unsigned long long wacc_[16] = {};
-#endif
-    // lane c holds the fp32 score of c hits, (float)c / n (hpp:300); the smallest passing count
-    const float sc_long = lane <= n ? (float)lane / (float)n : 0.0f;
-    const unsigned long long pm = __ballot(lane <= n && lane > 0 && !(sc_long < P.thr));
-    // threshold 0 with rank lists: the multi-hit terms only, k_emit adds the one-hit records
-    // (emit_rank_prefix)
-    const bool rank = X.rank_post && (pm & 2ull);
-    const uint32_t cmin = pm ? (rank ? 2u : (uint32_t)(__ffsll((long long)pm) - 1)) : 1000u;
-    // heavy_class() lists these for launches of their own (same test, same cmin)
-    if (!P.lean_all && (cmin <= kHeavyCmin || (m < X.short_query_len && X.n_short))) return;
-    if (m < X.short_query_len && X.n_short) { bail(); return; }  // short search: tier 1b
-    const uint8_t* qg = qnorm + qoff[q];
-    for (uint32_t i = lane; i < m; i += 64) S.q[i] = char_at(qg, i, X.csize);
-    if (lane == 0) S.x_surv_n = 0;  // no arena blocks chained (spill_arena)
-    {
-        uint4* T4 = reinterpret_cast<uint4*>(S.table);
-#pragma unroll
-        for (uint32_t i = 0; i < (uint32_t)kWaveSlots / 256; ++i) T4[lane + 64 * i] = make_uint4(0, 0, 0, 0);
-    }
-    wave_sync();
-    // ---- searchLong (nGramSearch.hpp:278-301): the gram occurrences with postings, compacted to
-    // lanes 0..ng-1 (a gram repeated k times owns k lanes: counts with multiplicity) ----
-    uint64_t gbase = 0;
-    uint32_t glen = 0, grow = 0;
-    bool have = false;
-    if (lane < n) {
-        const uint32_t code = gram_at(X, [&](uint32_t i) { return S.q[i]; }, lane);
-        if (code != UINT32_MAX) {
-            gbase = X.gram_off[code];
-            glen = (uint32_t)(X.gram_off[code + 1] - gbase);
-            grow = X.gram_row[code];
-            have = glen != 0;
-        }
-    }
-    const unsigned long long hb = __ballot(have);
-    const uint32_t ng = __popcll(hb);
-    {
-        uint32_t src = 0;
-        unsigned long long rest = hb;
-        for (uint32_t k = 0; k <= lane && rest; ++k) {  // lane k takes the k-th set bit
-            src = __ffsll((long long)rest) - 1;
-            rest &= rest - 1;
-        }
-        const uint64_t b2 = __shfl(gbase, (int)src);
-        const uint32_t l2 = __shfl(glen, (int)src), r2 = __shfl(grow, (int)src);
-        gbase = lane < ng ? b2 : 0;
-        glen = lane < ng ? l2 : 0;
-        grow = lane < ng ? r2 : 0;
-    }
-    const uint64_t p_total = wave_sum((uint64_t)glen);
+    const bool rank = lp.rank;
+    const uint64_t gbase = lp.gbase, p_total = lp.p_total;
     WSTAMP(0);
     const bool sketch = cmin >= kSketchMinCmin && cmin <= kSketchMax;
-    static_assert(!ONES, "part_ones runs in lean_query (the heavy list's launch)");
     if (p_total && cmin <= n && !sketch) { bail(); return; }  // exact counting: tier 1b
     uint32_t surv_n = 0, spilled = 0;
     // rank lists: the query's lists for k_emit (emit_rank_prefix) in its last kRankInfo slots
@@ -2907,10 +2772,7 @@ __device__ __forceinline__ void lean_query_g(WaveSmem<1, true>& S, const uint32_
         return;
     }
     WSTAMP(6);
-#ifdef NGS_PHASE_STAMPS
-    if (lane == 0)
-        for (int i = 0; i < 16; ++i) atomicAdd(&g_phase[32 + i], wacc_[i]);
-#endif
+    WPHASE_END(32)
     if (lane == 0) P.esn[q] = spilled | (P.lean_all ? kEmitHeavy : 0u);
     if (lane == 0 && !(P.dbg & 32u)) {
         DevStats* sl = stats + (q & (kStatSlots - 1));
@@ -2927,8 +2789,7 @@ __device__ __forceinline__ void lean_query_g(WaveSmem<1, true>& S, const uint32_
 
 // Tier 1b / experiments: the full wave kernel, over every query (qlist == nullptr) or over the
 // queries tier 1a handed over (qlist[0 .. *qcount), grid-stride).
-template <int W>
-__global__ __launch_bounds__(64 * W, kWaveWavesPerSimd) void k_wave(DevIndex X, SearchParams P,
+__global__ __launch_bounds__(64, kWaveWavesPerSimd) void k_wave(DevIndex X, SearchParams P,
                                                                    const uint8_t* __restrict__ qnorm,
                                                                    const uint64_t* __restrict__ qoff,
                                                                    const uint32_t* __restrict__ qm,
@@ -2940,16 +2801,16 @@ __global__ __launch_bounds__(64 * W, kWaveWavesPerSimd) void k_wave(DevIndex X, 
                                                                    DevStats* __restrict__ stats,
                                                                    const uint32_t* __restrict__ qlist,
                                                                    const uint32_t* __restrict__ qcount) {
-    __shared__ WaveSmem<W> S;
-    const uint32_t nsl = W == 1 && P.nslices > 1 ? P.nslices : 1u;  // sliced: k_merge follows
+    __shared__ WaveSmem<> S;
+    const uint32_t nsl = P.nslices > 1 ? P.nslices : 1u;  // sliced: k_merge follows
     if (!qlist) {  // every query of the batch: a workgroup per (query, slice)
         const uint32_t q = blockIdx.x / nsl;
-        wave_query<W, false>(S, q, X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats, nullptr,
+        wave_query(S, q, X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats, nullptr,
                              nullptr, blockIdx.x - q * nsl, nsl);
         return;
     }
     const uint32_t cnt = *qcount;
-    if (W == 1 && P.qhead) {
+    if (P.qhead) {
         // a persistent grid of about one workgroup per slot of the GPU pulls (query, slice) items:
         // a near-empty list no longer dispatches B x slices workgroups beside tier 1a, and a long
         // one balances like the hardware dispatcher did. Workgroups beyond the item count leave
@@ -2960,7 +2821,7 @@ __global__ __launch_bounds__(64 * W, kWaveWavesPerSimd) void k_wave(DevIndex X, 
         for (uint32_t t = blockIdx.x;;) {
             if (t >= items) break;
             const uint32_t i = t / nsl;
-            wave_query<W, false>(S, qlist[i], X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats,
+            wave_query(S, qlist[i], X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats,
                                  nullptr, nullptr, t - i * nsl, nsl);
             __syncthreads();
             // the first gridDim.x items went one to a workgroup; the rest are pulled in turn
@@ -2972,7 +2833,7 @@ __global__ __launch_bounds__(64 * W, kWaveWavesPerSimd) void k_wave(DevIndex X, 
     }
     for (uint32_t t = blockIdx.x; t < cnt * nsl; t += gridDim.x) {
         const uint32_t i = t / nsl;
-        wave_query<W, false>(S, qlist[i], X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats,
+        wave_query(S, qlist[i], X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats,
                              nullptr, nullptr, t - i * nsl, nsl);
         __syncthreads();
     }
@@ -2995,7 +2856,7 @@ __device__ __forceinline__ uint32_t sys_load32(const uint32_t* p) {
 
 __global__ __launch_bounds__(64) void k_serve(DevIndex X, SearchParams P0, ServeBlock* blk, DevStats* scratch,
                                               uint32_t* list2, uint32_t idle_ms, uint32_t life_ms) {
-    __shared__ WaveSmem<1> S;
+    __shared__ WaveSmem<> S;
     const uint32_t lane = lane_id();
     uint32_t* count2 = reinterpret_cast<uint32_t*>(scratch + kStatSlots);
     if (lane == 0) __hip_atomic_store(&blk->alive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -3045,7 +2906,7 @@ __global__ __launch_bounds__(64) void k_serve(DevIndex X, SearchParams P0, Serve
         }
         if (lane == 0) __hip_atomic_store(count2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         wave_sync();
-        wave_query<1, false>(S, 0u, X, P, blk->q, blk->off, &blk->m, &blk->n, blk->keys, blk->scores, list2, count2,
+        wave_query(S, 0u, X, P, blk->q, blk->off, &blk->m, &blk->n, blk->keys, blk->scores, list2, count2,
                              scratch, nullptr, nullptr, 0u, 1u, m);
         const uint32_t routed = __hip_atomic_load(count2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (lane == 0) {
@@ -3061,15 +2922,14 @@ __global__ __launch_bounds__(64) void k_serve(DevIndex X, SearchParams P0, Serve
     if (lane == 0) __hip_atomic_store(&blk->alive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// Tier 1a: the lean wave kernel over every query (qlist == nullptr), or over the heavy list.
-// DEFER (both launches): survivors spill to HBM for k_emit.
-// ONES: the heavy list's launch, which also takes cmin-1 queries (part_ones); the main launch
-// is compiled without that path. LISTED: the launch walks a query list (the heavy list), else
-// one workgroup per query (the main launch): either way the part loop is compiled once (with
-// both in one kernel the main launch carried 76 B of scratch spills and 434 lane reloads; the
-// same speed, profiles/r03_s5_ab_lean_one_copy.txt)
-template <bool DEFER, bool ONES = false, bool LISTED = true, bool PACKED = false, bool LOOPED = false>
-__global__ __launch_bounds__(64, PACKED ? kHeavyLeanWavesPerSimd : kLeanWavesPerSimd) void k_wave_lean(DevIndex X, SearchParams P,
+// Tier 1a: the lean wave kernel, survivors spilled to HBM for k_emit. The main launch
+// (HEAVY false) takes one query per workgroup; HEAVY: the heavy list's launch, (query, term-id
+// slice) items of the list (LOOPED: the overflow launch, grid-stride), and with ONES also its
+// cmin-1 queries (part_ones). Each launch compiles its own part loop (with both loops in one
+// kernel the main launch carried 76 B of scratch spills and 434 lane reloads; the same speed,
+// profiles/r03_s5_ab_lean_one_copy.txt)
+template <bool HEAVY, bool ONES = false, bool LOOPED = false>
+__global__ __launch_bounds__(64, HEAVY ? kHeavyLeanWavesPerSimd : kLeanWavesPerSimd) void k_wave_lean(DevIndex X, SearchParams P,
                                                                     const uint8_t* __restrict__ qnorm,
                                                                     const uint64_t* __restrict__ qoff,
                                                                     const uint32_t* __restrict__ qm,
@@ -3082,23 +2942,14 @@ __global__ __launch_bounds__(64, PACKED ? kHeavyLeanWavesPerSimd : kLeanWavesPer
                                                                     uint32_t* __restrict__ fb, uint32_t* __restrict__ fbc,
                                                                     const uint32_t* __restrict__ qlist,
                                                                     const uint32_t* __restrict__ qcount) {
-    __shared__ WaveSmem<1, true> S;
+    __shared__ WaveSmem<true> S;
     // lane-group staging (lean_query_g) for the main launch; the heavy list's launch keeps the packed
     // staging (lean_query): its threshold-0 queries' part_ones parts are ~3 chunks per list, where a
-    // per-list cap splits most parts (lane groups there measured slower, C2 32.0-32.8 against
-    // 37.1-37.3 Mq/s)
-    auto one = [&](uint32_t q) {
-        if constexpr (PACKED || ONES)
-            lean_query<ONES>(S, q, X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats, fb, fbc);
-        else
-            lean_query_g<ONES>(S, q, X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats, fb, fbc);
-    };
-    if constexpr (!LISTED) {
-        one(blockIdx.x);
-        return;
-    }
-    const uint32_t cnt = *qcount;  // the heavy list, grid-stride
-    if constexpr (PACKED) {
+    // per-list cap splits most parts
+    if constexpr (!HEAVY) {
+        lean_query_g(S, blockIdx.x, X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats, fb, fbc);
+    } else {
+        const uint32_t cnt = *qcount;
         // (query, term-id slice) items, one per workgroup (heavy_grid sizes the launch for every
         // item; the rest exit), a query's slices on neighbouring workgroups: enough slices that a
         // short list fills the GPU and no query's wave outlasts the rest by much. No item loop: in one
@@ -3123,11 +2974,6 @@ __global__ __launch_bounds__(64, PACKED ? kHeavyLeanWavesPerSimd : kLeanWavesPer
             lean_query<ONES>(S, qlist[k], X, P, qnorm, qoff, qm, out_n, out_k, out_s, list2, count2, stats, fb, fbc,
                              i - k * nsl, nsl);
         }
-        return;
-    }
-    for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
-        one(qlist[i]);
-        wave_sync();
     }
 }
 
@@ -4061,7 +3907,7 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
             // one and recorded after it, so that two calls in flight do not run their main launches at once
             auto main_lean = [&]() {
                 if (main_ev && main_wait) (void)hipStreamWaitEvent(s, main_ev, 0);
-                hipLaunchKernelGGL((k_wave_lean<true, false, false>), dim3(P.n_queries), dim3(64), 0, s, X,
+                hipLaunchKernelGGL((k_wave_lean<false>), dim3(P.n_queries), dim3(64), 0, s, X,
                                    P, qnorm, off, qm,
                                    out_n, out_k, out_s, list2, count2, stats, fb, fbc, (const uint32_t*)nullptr,
                                    (const uint32_t*)nullptr);
@@ -4087,22 +3933,22 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
                     const bool ones = !X.rank_post && !(1.0f / (float)n_min < P.thr);
                     PH.hbase = 0;
                     if (ones)
-                        hipLaunchKernelGGL((k_wave_lean<true, true, true, true>), dim3(ghl), dim3(64), 0, side, X, PH,
+                        hipLaunchKernelGGL((k_wave_lean<true, true>), dim3(ghl), dim3(64), 0, side, X, PH,
                                            qnorm, off, qm, out_n, out_k, out_s, list2, count2, stats, fb2, fbc2, heavy,
                                            hcount);
                     else
-                        hipLaunchKernelGGL((k_wave_lean<true, false, true, true>), dim3(ghl), dim3(64), 0, side, X, PH, qnorm,
+                        hipLaunchKernelGGL((k_wave_lean<true, false>), dim3(ghl), dim3(64), 0, side, X, PH, qnorm,
                                            off, qm, out_n, out_k, out_s, list2, count2, stats, fb2, fbc2, heavy, hcount);
                     dbg_check(side, "k_wave_lean (heavy list)");
                     if (ghl < ghb) {  // items past the first grid, if this call has more than the last
                         PH.hbase = ghl;
                         const uint32_t gov = std::min<uint32_t>(ghb - ghl, kHeavyOverflowGrid);
                         if (ones)
-                            hipLaunchKernelGGL((k_wave_lean<true, true, true, true, true>), dim3(gov), dim3(64), 0,
+                            hipLaunchKernelGGL((k_wave_lean<true, true, true>), dim3(gov), dim3(64), 0,
                                                side, X, PH, qnorm, off, qm, out_n, out_k, out_s, list2, count2, stats,
                                                fb2, fbc2, heavy, hcount);
                         else
-                            hipLaunchKernelGGL((k_wave_lean<true, false, true, true, true>), dim3(gov), dim3(64), 0, side,
+                            hipLaunchKernelGGL((k_wave_lean<true, false, true>), dim3(gov), dim3(64), 0, side,
                                                X, PH, qnorm, off, qm, out_n, out_k, out_s, list2, count2, stats, fb2,
                                                fbc2, heavy, hcount);
                         dbg_check(side, "k_wave_lean (heavy list overflow)");
@@ -4112,9 +3958,9 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
                                        side, X, PH, qnorm, off, qm, out_n, out_k, out_s, stats, heavy, hcount);
                     dbg_check(side, "k_emit (heavy list)");
                 }
-                hipLaunchKernelGGL(k_wave<1>, dim3(g1s), dim3(64), 0, side, X, PHO, qnorm, off, qm, out_n, out_k,
+                hipLaunchKernelGGL(k_wave, dim3(g1s), dim3(64), 0, side, X, PHO, qnorm, off, qm, out_n, out_k,
                                    out_s, list2, count2, stats, (const uint32_t*)fb2, (const uint32_t*)fbc2);
-                dbg_check(side, "k_wave<1> (heavy hand-overs)");
+                dbg_check(side, "k_wave (heavy hand-overs)");
                 if (P.nslices > 1) {
                     hipLaunchKernelGGL(k_merge, dim3(g1b), dim3(64), 0, side, X, P, (const uint32_t*)fb2,
                                        (const uint32_t*)fbc2, out_n, out_k, out_s, stats);
@@ -4130,9 +3976,9 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
                 SearchParams PF = P;
                 PF.nslices = 1;
                 PF.qhead = gcount + 10;
-                hipLaunchKernelGGL(k_wave<1>, dim3(gfull), dim3(64), 0, side2, X, PF, qnorm, off, qm, out_n, out_k,
+                hipLaunchKernelGGL(k_wave, dim3(gfull), dim3(64), 0, side2, X, PF, qnorm, off, qm, out_n, out_k,
                                    out_s, list2, count2, stats, full, fcount);
-                dbg_check(side2, "k_wave<1> (full list)");
+                dbg_check(side2, "k_wave (full list)");
             }
             if (side2 != s && (e = hipEventRecord(join2, side2)) != hipSuccess) return e;
             // all_heavy (every lean query on the heavy list, e.g. threshold 0): the main launch finishes
@@ -4146,9 +3992,9 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
             }
             // tier 1b over the queries tier 1a handed over
             if (!all_heavy) {
-                hipLaunchKernelGGL(k_wave<1>, dim3(g1s), dim3(64), 0, s, X, PM, qnorm, off, qm, out_n, out_k, out_s,
+                hipLaunchKernelGGL(k_wave, dim3(g1s), dim3(64), 0, s, X, PM, qnorm, off, qm, out_n, out_k, out_s,
                                    list2, count2, stats, (const uint32_t*)fb, (const uint32_t*)fbc);
-                dbg_check(s, "k_wave<1> (hand-overs)");
+                dbg_check(s, "k_wave (hand-overs)");
             }
             if (P.nslices > 1 && !all_heavy) {
                 hipLaunchKernelGGL(k_merge, dim3(g1b), dim3(64), 0, s, X, P, (const uint32_t*)fb, (const uint32_t*)fbc,
@@ -4162,10 +4008,10 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
             break;
         }
         case 1:
-            hipLaunchKernelGGL(k_wave<1>, dim3(P.n_queries * std::max<uint32_t>(P.nslices, 1u)), dim3(64), 0, s, X, P,
+            hipLaunchKernelGGL(k_wave, dim3(P.n_queries * std::max<uint32_t>(P.nslices, 1u)), dim3(64), 0, s, X, P,
                                qnorm, off, qm, out_n, out_k, out_s, list2, count2, stats, (const uint32_t*)nullptr,
                                (const uint32_t*)nullptr);
-            dbg_check(s, "k_wave<1>");
+            dbg_check(s, "k_wave");
             if (P.nslices > 1) {
                 hipLaunchKernelGGL(k_merge, dim3(P.n_queries), dim3(64), 0, s, X, P, (const uint32_t*)nullptr,
                                    (const uint32_t*)nullptr, out_n, out_k, out_s, stats);

@@ -94,7 +94,12 @@ def test_concurrent_calls_and_dispose():
                         with lock:
                             counts["after_dispose_empty"] += 1
                     else:
-                        record(f"worker {wid} {name} op {op:.2f} thr {t} limit {l}: {res[0][:3]} vs {want[0][:3]}")
+                        bad = [i for i, (r, w) in enumerate(zip(res, want)) if not _same(r, w)]
+                        i = bad[0] if bad else 0
+                        qi = batch[i] if op >= 0.6 else q
+                        record(f"worker {wid} {name} op {op:.2f} thr {t} limit {l} batch {len(res)} "
+                               f"({len(bad)} wrong, first #{i} q={qi!r}): got {len(res[i])} {res[i][:4]} "
+                               f"want {len(want[i])} {want[i][:4]}")
                 with lock:
                     counts["calls"] += 1
                     if op >= 0.6:

@@ -6,7 +6,7 @@ import csv
 import statistics
 import sys
 
-MAIN = "k_wave_lean<true, false, false, false, false>"
+MAIN = "k_wave_lean<false,"
 rows = list(csv.DictReader(open(sys.argv[1])))
 qs = collections.defaultdict(set)
 for r in rows:

@@ -21,7 +21,7 @@ from collections import defaultdict
 
 # the main tier-1a launch (one workgroup per query); the heavy list's launch has the same grid since
 # round 5 (one workgroup per item), so it is told apart by its template arguments
-MAIN = "k_wave_lean<true, false, false,"  # (ONES and LISTED off: the main launch only)
+MAIN = "k_wave_lean<false,"  # (HEAVY off: the main launch only)
 
 N_CU = 256
 N_SE = 32  # 8 XCDs x 4 shader engines

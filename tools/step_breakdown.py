@@ -6,7 +6,7 @@ import csv
 import re
 import sys
 
-MAIN = "k_wave_lean<true, false, false, false, false>"
+MAIN = "k_wave_lean<false,"
 
 
 def short(n):
