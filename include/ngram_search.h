@@ -268,8 +268,9 @@ NGS_API const char* ngsVersion(void);
 /* Diagnostics: the host batch path's phases (scoreBatch / searchBatch / batch score paths of more
  * than 16 queries), nanoseconds summed over the calls since the last reset: [0] query packing,
  * [1] copies in + kernels queued, [2] kernels waited for, [3] device pack + offsets back,
- * [4] records back + marshalling, [5] whole calls, [6] number of calls. Writes min(n, 7) values,
- * resets them all if `reset`, returns 7. */
+ * [4] records back + marshalling, [5] whole calls, [6] number of calls; [7] the number of
+ * one-stream batch calls (all queries heavy, at most 16,384) replayed from a captured graph,
+ * any entry point. Writes min(n, 8) values, resets them all if `reset`, returns 8. */
 NGS_API int ngsHostPhases(uint64_t* out, int n, int reset);
 
 /* Diagnostics: per-phase time of the LDS kernels (s_memtime shader-clock ticks, summed over

@@ -73,6 +73,7 @@ enum HostPhase : int {
     kHpRecords,       // the records back, marshalled into the new[]'d arrays as they land
     kHpCall,          // the whole call (scoreBatch / searchBatch)
     kHpCalls,         // (count) calls
+    kHpReplays,       // (count) one-stream calls replayed from a captured graph (queue_search)
     kHpN
 };
 std::atomic<uint64_t> g_host_phase[kHpN];
@@ -360,6 +361,14 @@ struct Context {
     Pinned h_off, h_raw, h_res;  // queries in; results out
     uint8_t* d_sio = nullptr;     // the latency path's block (kSioBytes): one copy in, one copy out
     uint8_t* h_sio = nullptr;     // ... its pinned host image
+    // one-stream calls (queue_search): calls captured as graphs, replayed when a call's launch
+    // arguments (the signature) repeat one of them; gseen: recent signatures, a call is captured on
+    // its second occurrence. Up to kGraphs of each (a pipelined caller rotates its output buffers
+    // over the contexts in flight: C2's bench loop, 4 buffers over 3 contexts)
+    static constexpr size_t kGraphs = 8;
+    std::vector<std::pair<std::vector<uint8_t>, hipGraphExec_t>> graphs;
+    std::vector<std::vector<uint8_t>> gseen;
+    bool gfail = false;  // a capture failed: this context queues its calls one by one
 
     ~Context() {
         hipSetDevice(device);
@@ -369,6 +378,7 @@ struct Context {
                         (void*)d_group, (void*)d_stats, (void*)d_sio, (void*)d_out, (void*)d_pos, (void*)d_pk, (void*)d_ps, d_ptemp, (void*)gen.cnt,
                         (void*)gen.kenc, (void*)gen.list, (void*)gen.sorted, (void*)gen.lcount, gen.temp})
             if (p) hipFree(p);
+        for (auto& g : graphs) hipGraphExecDestroy(g.second);
         if (h_stats) hipHostFree(h_stats);
         if (h_sio) hipHostFree(h_sio);
         for (hipEvent_t e : ev)
@@ -1103,7 +1113,7 @@ int queue_search(Library& L, Replica& R, Context& c, const uint8_t* d_raw, const
     // together with the results)
     DevStats* sd = small ? reinterpret_cast<DevStats*>(c.d_sio) : c.d_stats;
     uint32_t* gc = reinterpret_cast<uint32_t*>(sd + kStatSlots);
-    P = SearchParams{};
+    std::memset(&P, 0, sizeof(P));  // (padding too: the bytes are a replay signature, Context::gsig)
     P.thr = thr;
     P.limit = limit;
     P.out_stride = stride;
@@ -1197,28 +1207,68 @@ int queue_search(Library& L, Replica& R, Context& c, const uint8_t* d_raw, const
     if (zero_in_prep) {
         P.zero_stats = reinterpret_cast<uint32_t*>(c.d_stats);
         P.zero_words = (uint32_t)(kStatSlots * sizeof(DevStats) / sizeof(uint32_t));
-    } else if (!small && !HIP_CHECK(hipMemsetAsync(c.d_stats, 0, sizeof(DevStats) * (kStatSlots + 1 + 2 * kListSlots), s))) {
-        return -4;
     }
-    if (timing) HIP_CHECK(hipEventRecord(c.ev[0], s));
     DevIndex X;
     if (!R.index_for(P.valid, X)) return -4;
-    if (!HIP_CHECK(launch_prep(d_raw, d_off, B, P, c.d_norm, c.d_qm, X.csize, X, c.d_heavy, gc + 3, c.d_full,
-                               gc + 5, c.d_lslots, c.d_lctr, s, side, c.prep_ev, c.lists_ev)))
-        return -4;
-    c.stats_clean = !small && P.waves == 0;  // k_lists queued: it leaves the list counters zero
-    if (timing) HIP_CHECK(hipEventRecord(c.ev[1], s));  // the end of k_prep is the start of the tier-1 phase
-    // the main tier-1a launches of this replica's calls one after another: with two calls in flight
-    // the second call's main launch otherwise starts in the first one's and the two share the GPU
-    // (C3, one box, three passes each: 31.3-31.6 against 30.1-30.6 Mq/s,
-    // profiles/r05_s15_ab_serial_main.txt; C5 the same)
-    {
+    // A one-stream call (side == s: batches up to kOneStreamBatch queries that are all heavy, C2) is
+    // ~0.1 ms of GPU work for ~12 queued operations, 50 us of host time per call. When a call's
+    // launch arguments repeat the context's previous call (a server's or a bench's batches into the
+    // same buffers), the sequence is captured as a graph on the second occurrence and replayed
+    // from then on (one submission: ~4 us of host time for 10 launches against ~30,
+    // tools/ubench/graph_launch.hip). Such calls leave the replica's main-launch order alone
+    // (main_ev): their main launch only routes, every lean query being on the heavy list.
+    static const bool no_graphs = std::getenv("NGS_SYNC_DEBUG") != nullptr;
+    bool capture = false;
+    std::vector<uint8_t> sig;
+    // (not on the null stream, which cannot be captured)
+    if (!small && side == s && s && !timing && !no_graphs && !c.gfail) {
+        auto put = [&](const void* p, size_t n) {
+            sig.insert(sig.end(), static_cast<const uint8_t*>(p), static_cast<const uint8_t*>(p) + n);
+        };
+        const void* ptrs[] = {d_raw, d_off, d_n, d_k, d_s, s, c.d_norm, c.d_qm, c.d_list2, c.d_fb, c.d_fb2,
+                              c.d_heavy, c.d_full, c.d_glist, c.d_lslots, c.d_lctr, c.d_stats, c.h_stats};
+        put(ptrs, sizeof(ptrs));
+        put(&X, sizeof(X));
+        put(&P, sizeof(P));
+        const uint32_t flags[] = {B, all_heavy ? 1u : 0u, zero_in_prep ? 1u : 0u};
+        put(flags, sizeof(flags));
+        for (auto& g : c.graphs) {
+            if (g.first != sig) continue;
+            if (!HIP_CHECK(hipGraphLaunch(g.second, s))) return -4;
+            c.stats_clean = true;
+            g_host_phase[kHpReplays].fetch_add(1, std::memory_order_relaxed);
+            return 0;
+        }
+        capture = std::find(c.gseen.begin(), c.gseen.end(), sig) != c.gseen.end();
+        if (!capture) {
+            if (c.gseen.size() >= Context::kGraphs) c.gseen.erase(c.gseen.begin());
+            c.gseen.push_back(sig);
+        }
+    }
+    if (capture && !HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal))) {
+        (void)hipGetLastError();
+        capture = false;
+        c.gfail = true;
+    }
+    auto queue_ops = [&]() -> bool {
+        if (!zero_in_prep && !small &&
+            !HIP_CHECK(hipMemsetAsync(c.d_stats, 0, sizeof(DevStats) * (kStatSlots + 1 + 2 * kListSlots), s)))
+            return false;
+        if (timing) HIP_CHECK(hipEventRecord(c.ev[0], s));
+        if (!HIP_CHECK(launch_prep(d_raw, d_off, B, P, c.d_norm, c.d_qm, X.csize, X, c.d_heavy, gc + 3, c.d_full,
+                                   gc + 5, c.d_lslots, c.d_lctr, s, side, c.prep_ev, c.lists_ev)))
+            return false;
+        if (timing) HIP_CHECK(hipEventRecord(c.ev[1], s));  // the end of k_prep is the start of the tier-1 phase
+        // the main tier-1a launches of this replica's calls one after another: with two calls in flight
+        // the second call's main launch otherwise starts in the first one's and the two share the GPU
+        // (C3, one box, three passes each: 31.3-31.6 against 30.1-30.6 Mq/s,
+        // profiles/r05_s15_ab_serial_main.txt; C5 the same)
         std::unique_lock<std::mutex> g(R.main_mu, std::defer_lock);
         hipEvent_t mev = nullptr;
         bool mwait = false;
-        if (!small) {
+        if (!small && !capture) {
             g.lock();
-            if (!R.main_ev && !HIP_CHECK(hipEventCreateWithFlags(&R.main_ev, hipEventDisableTiming))) return -4;
+            if (!R.main_ev && !HIP_CHECK(hipEventCreateWithFlags(&R.main_ev, hipEventDisableTiming))) return false;
             mev = R.main_ev;
             mwait = R.main_rec;
             R.main_rec = true;
@@ -1226,11 +1276,35 @@ int queue_search(Library& L, Replica& R, Context& c, const uint8_t* d_raw, const
         if (!HIP_CHECK(launch_fast(X, P, c.d_norm, d_off, c.d_qm, d_n, d_k, d_s, c.d_list2, gc + 1, c.d_fb, gc + 2,
                                    c.d_fb2, gc + 4, c.d_heavy, gc + 3, c.d_full, gc + 5, c.d_glist, gc, sd, s, side,
                                    side2, c.join, c.join2, c.lists_ev, all_heavy, mev, mwait)))
-            return -4;
+            return false;
+        if (timing) HIP_CHECK(hipEventRecord(c.ev[3], s));
+        // the statistics and the path counts in one read-back (the general path adds no statistics)
+        return small || HIP_CHECK(hipMemcpyAsync(c.h_stats, c.d_stats, kSioStats, hipMemcpyDeviceToHost, s));
+    };
+    const bool queued = queue_ops();
+    if (capture) {
+        hipGraph_t graph = nullptr;
+        hipGraphExec_t exec = nullptr;
+        const bool ended = HIP_CHECK(hipStreamEndCapture(s, &graph));
+        const bool made = ended && queued && graph && HIP_CHECK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+        if (graph) hipGraphDestroy(graph);
+        (void)hipGetLastError();
+        if (made) {
+            c.gseen.erase(std::find(c.gseen.begin(), c.gseen.end(), sig));
+            if (c.graphs.size() >= Context::kGraphs) {
+                hipGraphExecDestroy(c.graphs.front().second);
+                c.graphs.erase(c.graphs.begin());
+            }
+            c.graphs.emplace_back(std::move(sig), exec);
+            if (!HIP_CHECK(hipGraphLaunch(exec, s))) return -4;
+        } else {  // nothing of the call ran: queue it one by one, and so from now on
+            c.gfail = true;
+            if (!queue_ops()) return -4;
+        }
+    } else if (!queued) {
+        return -4;
     }
-    if (timing) HIP_CHECK(hipEventRecord(c.ev[3], s));
-    // the statistics and the path counts in one read-back (the general path adds no statistics)
-    if (!small && !HIP_CHECK(hipMemcpyAsync(c.h_stats, c.d_stats, kSioStats, hipMemcpyDeviceToHost, s))) return -4;
+    c.stats_clean = !small && P.waves == 0;  // k_lists queued: it leaves the list counters zero
     return 0;
 }
 
