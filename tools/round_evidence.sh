@@ -18,7 +18,7 @@ fi
 timeout -k 10 400 python3 bench.py > $O/c3_bench.json 2> $O/c3_bench.err || { echo "c3 bench failed"; tail -5 $O/c3_bench.err; exit 1; }
 timeout -k 10 300 python3 bench.py --config c2 > $O/c2_bench.json 2> $O/c2_bench.err || { echo "c2 bench failed"; exit 1; }
 timeout -k 10 400 python3 bench.py --config c5 --no-cpu-baseline --no-dropin --steps 20 > $O/c5_bench.json 2> $O/c5_bench.err || { echo "c5 bench failed"; exit 1; }
-timeout -k 10 500 python3 bench.py --config c4 --no-cpu-baseline --no-dropin --steps 3 --warmup 4 > $O/c4_bench.json 2> $O/c4_bench.err || { echo "c4 bench failed"; exit 1; }
+timeout -k 10 500 python3 bench.py --config c4 --no-cpu-baseline --no-dropin --steps 12 --warmup 4 > $O/c4_bench.json 2> $O/c4_bench.err || { echo "c4 bench failed"; exit 1; }
 for c in c3 c2 c5 c4; do
   python3 -c "import json; d=json.load(open('$O/${c}_bench.json')); print('$c', d['value'], d['unit'], d['ms_per_step'], 'ms/step frac', d['roofline']['frac'])"
 done
