@@ -1746,8 +1746,19 @@ void set_valid(Library& L, const char* chars, int n) {
         const uint8_t c = (uint8_t)chars[i];
         v[c >> 5] |= 1u << (c & 31);
     }
-    std::lock_guard<std::mutex> g(L.valid_mu);
-    std::memcpy(L.valid, v, sizeof(v));
+    {
+        std::lock_guard<std::mutex> g(L.valid_mu);
+        std::memcpy(L.valid, v, sizeof(v));
+    }
+    // the set's key flags (Replica::index_for) built here, so that the first search under it, an
+    // ngsSearchDeviceAsync included, does not build and synchronise them (the caller's device kept)
+    int dev = -1;
+    (void)hipGetDevice(&dev);
+    for (auto& R : L.reps) {
+        DevIndex X;
+        (void)R->index_for(v, X);
+    }
+    if (dev >= 0) (void)hipSetDevice(dev);
 }
 
 // result strings point into the index's own key storage (valid until dispose, hpp:443-447)
