@@ -3,7 +3,7 @@
 Routing (ngs_kernels.hip: heavy_class, wave_query's hand-over, fast_one's guard):
 * tier 1a (k_wave_lean + k_emit): <= 63 grams, limit <= 128, cmin >= 3, no short search;
 * heavy list (k_wave_lean on a side stream): cmin 2 (8-character queries at thr 0.3);
-* full list / hand-overs (k_wave<1>, tier 1b): cmin 1 (thr 0) or a short search (|q| < 9);
+* full list / hand-overs (k_wave, tier 1b): cmin 1 (thr 0) or a short search (|q| < 9);
 * tier 2 (k_fast, one block per query): 64..255 grams (66..257 bytes) or limit 129..1024;
 * general (k_gen_*): |q| <= 3 (full-library scan), > 255 grams, or limit > 1024.
 
