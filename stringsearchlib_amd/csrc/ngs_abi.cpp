@@ -39,7 +39,7 @@ constexpr size_t kGeneralBudget = size_t(2) << 30;   // bytes of dense general-p
 constexpr uint32_t kSmallBatch = 16;                 // host batches up to this many queries take the latency path
 constexpr size_t kSmallBlock = size_t(1) << 20;      // ... if their output block is at most this many bytes
 constexpr size_t kPartBudget = size_t(1) << 30;      // bytes of sliced tier-1b partial results per call
-constexpr uint32_t kSmallSlices = 32;                // ... or term-id slices per query (sliced k_wave<1>)
+constexpr uint32_t kSmallSlices = 32;                // ... or term-id slices per query (sliced k_wave)
 constexpr size_t kSmallQ = size_t(64) << 10;         // ... and if their offsets + bytes fit this many bytes
 // the latency path's one block, device and pinned host: statistics | results | queries
 constexpr size_t kSioStats = sizeof(DevStats) * (kStatSlots + 1);
@@ -1220,8 +1220,10 @@ int queue_search(Library& L, Replica& R, Context& c, const uint8_t* d_raw, const
     static const bool no_graphs = std::getenv("NGS_SYNC_DEBUG") != nullptr;
     bool capture = false;
     std::vector<uint8_t> sig;
-    // (not on the null stream, which cannot be captured)
-    if (!small && side == s && s && !timing && !no_graphs && !c.gfail) {
+    // Only on the context's own stream: a capture takes in whatever any thread queues on the stream
+    // meanwhile, so a caller's stream (ngsSearchDevice), which other threads may share, is never
+    // captured (nor the null stream, which cannot be).
+    if (!small && side == s && s == c.stream && !timing && !no_graphs && !c.gfail) {
         auto put = [&](const void* p, size_t n) {
             sig.insert(sig.end(), static_cast<const uint8_t*>(p), static_cast<const uint8_t*>(p) + n);
         };

@@ -249,7 +249,7 @@ struct SearchParams {
     // tier kernels after it accumulate) in place of a memset launch; null otherwise
     uint32_t* zero_stats;
     uint32_t zero_words;
-    // tier 1b over a list (k_wave<1>): a persistent grid takes its (query, slice) items from this
+    // tier 1b over a list (k_wave): a persistent grid takes its (query, slice) items from this
     // counter (zeroed with the path counts) instead of one workgroup per item; null: grid-stride
     uint32_t* qhead;
 };
