@@ -495,11 +495,12 @@ struct Replica {
     }
 };
 
-// ngsServe: the low-latency score() path. A persistent one-wave kernel (k_serve) on a stream of
-// its own polls a request block in coherent pinned host memory; score() writes the normalised
-// query there, publishes a request number and spins until the kernel publishes it back with the
-// results: no launch, no copy, no stream wait per call. The kernel exits on stop, after
-// kServeIdleMs without a request or after kServeLifeMs, and is relaunched on demand.
+// ngsServe: the low-latency score() path. A persistent kernel (k_serve) on a stream of its own,
+// one wave per request slot, polls request blocks in coherent pinned host memory; score() takes a
+// free slot, writes the normalised query there, publishes a request number and spins until the
+// kernel publishes it back with the results: no launch, no copy, no stream wait per call, and up
+// to kServeSlots callers served side by side. The kernel exits on stop, after kServeIdleMs without
+// a request or after kServeLifeMs, and is relaunched on demand.
 constexpr uint32_t kServeIdleMs = 200;
 constexpr uint32_t kServeLifeMs = 10000;
 // score()/search() start the server by themselves (no ngsServe call) from this many single-query
@@ -509,24 +510,31 @@ constexpr uint32_t kAutoServeAfter = 4;
 struct Server {
     int device = 0;
     hipStream_t stream = nullptr;
-    ServeBlock* h = nullptr;  // coherent pinned host memory
-    ServeBlock* d = nullptr;  // its device view
+    ServeBlock* h = nullptr;  // kServeSlots request blocks, coherent pinned host memory
+    ServeBlock* d = nullptr;  // their device view
     DevStats* scratch = nullptr;
     uint32_t* list2 = nullptr;
-    uint64_t seq = 0;
-    bool launched = false;
+    unsigned long long* t_any = nullptr;  // the latest request time of any slot (device memory)
+    uint64_t seq[kServeSlots] = {};
+    std::mutex slot_mu[kServeSlots];  // one request per slot at a time
+    std::mutex launch_mu;             // one (re)launch at a time
+    std::atomic<bool> launched{false};
     uint32_t launch_valid[8] = {};  // the validChar set of its DevIndex.kt_flag
 
     bool init(int dev) {
         device = dev;
+        const size_t nst = (size_t)kServeSlots * (kStatSlots + 1);
         if (!HIP_CHECK(hipSetDevice(dev)) || !HIP_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking)) ||
-            !HIP_CHECK(hipHostMalloc((void**)&h, sizeof(ServeBlock), hipHostMallocCoherent | hipHostMallocMapped)) ||
+            !HIP_CHECK(hipHostMalloc((void**)&h, sizeof(ServeBlock) * kServeSlots,
+                                     hipHostMallocCoherent | hipHostMallocMapped)) ||
             !HIP_CHECK(hipHostGetDevicePointer((void**)&d, h, 0)) ||
-            !HIP_CHECK(hipMalloc((void**)&scratch, sizeof(DevStats) * (kStatSlots + 1))) ||
-            !HIP_CHECK(hipMalloc((void**)&list2, sizeof(uint32_t) * 4)))
+            !HIP_CHECK(hipMalloc((void**)&scratch, sizeof(DevStats) * nst)) ||
+            !HIP_CHECK(hipMalloc((void**)&list2, sizeof(uint32_t) * 4 * kServeSlots)) ||
+            !HIP_CHECK(hipMalloc((void**)&t_any, sizeof(unsigned long long))))
             return false;
-        std::memset((void*)h, 0, sizeof(ServeBlock));
-        return HIP_CHECK(hipMemset(scratch, 0, sizeof(DevStats) * (kStatSlots + 1)));
+        std::memset((void*)h, 0, sizeof(ServeBlock) * kServeSlots);
+        return HIP_CHECK(hipMemset(scratch, 0, sizeof(DevStats) * nst)) &&
+               HIP_CHECK(hipMemset(t_any, 0, sizeof(unsigned long long)));
     }
     // the kernel has left (idle, lifetime, stop) or was never launched
     bool stopped() { return !launched || hipStreamQuery(stream) == hipSuccess; }
@@ -544,13 +552,14 @@ struct Server {
         if (h) hipHostFree(h);
         if (scratch) hipFree(scratch);
         if (list2) hipFree(list2);
+        if (t_any) hipFree(t_any);
     }
 };
 
 struct Library {
     std::unique_ptr<Server> server;  // ngsServe (null: off)
     std::atomic<bool> serving{false};  // server != null, for the unlocked test in one_query
-    std::mutex server_mu;            // creating / dropping it, and one request at a time
+    std::shared_mutex server_mu;     // creating / dropping / stopping it (exclusive); requests (shared)
     std::atomic<int> serve_pref{0};  // 0: automatic (kAutoServeAfter), 1: ngsServe(h, 1), -1: ngsServe(h, 0)
     std::atomic<uint32_t> single_calls{0};  // score()/search() calls so far (automatic start)
     // batch calls in flight: the server kernel is stopped while any runs and not relaunched until
@@ -1820,31 +1829,49 @@ bool host_normalise(const uint32_t* valid, const char* q, uint8_t* out, uint32_t
 // the server routes to tier 2 or the general path, or a server that cannot be reached).
 bool serve_query(Library& L, const char* query, float thr, uint32_t limit, std::vector<uint32_t>& keys,
                  std::vector<float>& sc) {
-    // one request in flight (ngsServe(0) waits for it). A caller that finds the server busy with
-    // another thread's request waits its turn (~12 us): taking the regular path instead would stop
-    // the server for every contended call, and relaunch it on the next
-    std::unique_lock<std::mutex> g(L.server_mu);
+    // the server's lifetime (shared: requests of other threads run beside this one)
+    std::shared_lock<std::shared_mutex> g(L.server_mu);
     if (L.batches.load(std::memory_order_acquire) > 0) return false;
     Server* sv = L.server.get();
     const uint32_t Lm = effective_limit(L, limit);
     Replica& R = *L.reps.front();
     if (!sv || Lm == 0 || Lm > kWaveMaxLimit || R.dev.n_buckets / 8 > 1) return false;
-    ServeBlock* b = sv->h;
+    // a free request slot, tried from one of this thread's own; all busy: try them again (a request
+    // holds its slot ~15 us, and a thread put to sleep on a mutex took ~50 us to wake: 8 threads on
+    // 4 slots ran at 84k calls/s blocking, against 240k for 4 threads)
+    static std::atomic<uint32_t> next_hint{0};
+    thread_local const uint32_t hint = next_hint.fetch_add(1, std::memory_order_relaxed);
+    uint32_t slot = 0;
+    std::unique_lock<std::mutex> sl;
+    for (uint32_t i = 0; !sl.owns_lock(); ++i) {
+        const uint32_t k = (hint + i) % kServeSlots;
+        sl = std::unique_lock<std::mutex>(sv->slot_mu[k], std::try_to_lock);
+        if (sl.owns_lock()) slot = k;
+        else if (i % kServeSlots == kServeSlots - 1) {
+            if (i > 64 * kServeSlots) std::this_thread::yield();
+            else __builtin_ia32_pause();
+        }
+    }
+    ServeBlock* b = sv->h + slot;
     uint32_t m = 0;
     {
         std::lock_guard<std::mutex> gv(L.valid_mu);
         if (!host_normalise(L.valid, query, b->q, kServeMaxQuery, m)) return false;
         std::memcpy(b->valid, L.valid, sizeof(b->valid));
     }
-    // a running server reads the key flags of the validChar set it was launched with
-    if (R.dev.kt_off && !sv->stopped() && std::memcmp(sv->launch_valid, b->valid, sizeof(b->valid)) != 0) sv->stop();
     b->thr = thr;
     b->limit = Lm;
     b->m = m;
     b->off[0] = 0;
     b->off[1] = m == kQueryWildcard ? 0 : m;
-    const uint64_t seq = ++sv->seq;
-    auto launch = [&]() -> bool {
+    const uint64_t seq = ++sv->seq[slot];
+    // (re)launch when the kernel has left; a running server reads the key flags of the validChar set
+    // it was launched with, so a new set restarts it (the other slots' requests are answered by
+    // the new kernel: theirs stay posted)
+    auto launch = [&](bool force) -> bool {
+        std::lock_guard<std::mutex> gl(sv->launch_mu);
+        if (force && R.dev.kt_off && !sv->stopped()) sv->stop();
+        if (!sv->stopped()) return true;
         if (!HIP_CHECK(hipSetDevice(sv->device))) return false;
         SearchParams P{};
         P.n_queries = 1;
@@ -1852,19 +1879,27 @@ bool serve_query(Library& L, const char* query, float thr, uint32_t limit, std::
         DevIndex X;
         if (!R.index_for(b->valid, X)) return false;
         std::memcpy(sv->launch_valid, b->valid, sizeof(sv->launch_valid));
-        sv->launched = HIP_CHECK(launch_serve(X, P, sv->d, sv->scratch, sv->list2, kServeIdleMs, kServeLifeMs,
-                                              sv->stream));
+        sv->launched = HIP_CHECK(launch_serve(X, P, sv->d, sv->scratch, sv->list2, sv->t_any, kServeIdleMs,
+                                              kServeLifeMs, sv->stream));
         return sv->launched;
     };
-    if (sv->stopped() && !launch()) return false;
+    {
+        bool stale;
+        {
+            std::lock_guard<std::mutex> gl(sv->launch_mu);
+            stale = R.dev.kt_off && std::memcmp(sv->launch_valid, b->valid, sizeof(b->valid)) != 0;
+        }
+        if ((stale || sv->stopped()) && !launch(stale)) return false;
+    }
     __atomic_store_n(&b->req_seq, seq, __ATOMIC_RELEASE);  // the fields above first (x86 stores stay in order)
     const auto t0 = std::chrono::steady_clock::now();
     for (uint64_t spin = 1; __atomic_load_n(&b->done_seq, __ATOMIC_ACQUIRE) != seq; ++spin) {
         if ((spin & 1023) == 0) {
             // the kernel left (its idle time ran out as the request came in): relaunch, it
             // answers the posted request
-            if (sv->stopped() && !launch()) return false;
+            if (sv->stopped() && !launch(false)) return false;
             if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+                std::lock_guard<std::mutex> gl(sv->launch_mu);
                 sv->stop();  // unreachable: leave it to the regular path
                 return false;
             }
@@ -1884,7 +1919,7 @@ void maybe_auto_serve(Library& L) {
     if (L.serve_pref.load(std::memory_order_relaxed) != 0 || L.reps.empty() || L.host.csize != 1) return;
     if (L.reps.front()->dev.n_buckets / 8 > 1) return;  // a large library keeps the sliced latency path
     if (L.single_calls.fetch_add(1, std::memory_order_relaxed) + 1 < kAutoServeAfter) return;
-    std::unique_lock<std::mutex> g(L.server_mu, std::try_to_lock);
+    std::unique_lock<std::shared_mutex> g(L.server_mu, std::try_to_lock);
     if (!g.owns_lock() || L.server || L.serve_pref.load() != 0) return;
     auto sv = std::make_unique<Server>();
     if (!sv->init(L.reps.front()->device)) {
@@ -1909,7 +1944,7 @@ struct BatchGuard {
         if (!L) return;
         L->batches.fetch_add(1, std::memory_order_acq_rel);
         if (L->serving.load(std::memory_order_acquire)) {
-            std::lock_guard<std::mutex> g(L->server_mu);
+            std::lock_guard<std::shared_mutex> g(L->server_mu);
             if (L->server && !L->server->stopped()) L->server->stop();
         }
     }
@@ -2460,7 +2495,7 @@ NGS_API int ngsServe(uint32_t handle, int enable) {
     if (!L) return -1;
     if (!L->host.indexed || L->reps.empty()) return -2;
     if (L->host.csize != 1) return -3;
-    std::lock_guard<std::mutex> g(L->server_mu);
+    std::lock_guard<std::shared_mutex> g(L->server_mu);
     if (!enable) {
         L->serve_pref.store(-1);  // off, and no automatic start either
         L->serving.store(false, std::memory_order_release);
@@ -2506,7 +2541,7 @@ NGS_API int ngsServeState(uint32_t handle) {
     std::shared_lock<std::shared_mutex> lk(g_lock);
     Library* L = find_lib(handle);
     if (!L) return -1;
-    std::lock_guard<std::mutex> g(L->server_mu);
+    std::shared_lock<std::shared_mutex> g(L->server_mu);
     if (!L->server) return 0;
     return L->server->stopped() ? 1 : 2;
 }

@@ -287,6 +287,8 @@ constexpr uint32_t kNoPart = 0xFFFFFFFFu;  // pcnt[q * nslices]: the query was a
 // request block in coherent pinned host memory, answers the query with the tier-1 wave search
 // and writes the results back into the same block; no launch, copy or wait per call.
 constexpr uint32_t kServeMaxQuery = 256;   // normalised query characters the block holds
+constexpr uint32_t kServeSlots = 8;        // server waves, one request block each (4 and 2 measured
+                                           // lower past 4 / 2 concurrent callers: DESIGN.md §6)
 struct alignas(64) ServeBlock {
     // host -> device
     uint64_t req_seq;          // the host stores the request's number last (release)

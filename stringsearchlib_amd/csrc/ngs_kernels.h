@@ -31,12 +31,13 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
                        hipStream_t side, hipStream_t side2, hipEvent_t join, hipEvent_t join2,
                        hipEvent_t lists_ev, bool all_heavy = false, hipEvent_t main_ev = nullptr, bool main_wait = false);
 
-// The low-latency server (ngsServe): one persistent one-wave workgroup on `s` serving requests
-// from `blk` (coherent pinned host memory, device view) until blk->stop, or until no request
-// came for idle_ms, or after life_ms in all. scratch: kStatSlots + 1 DevStats of device memory
-// (statistics and the tier-2 routing count it ignores).
+// The low-latency server (ngsServe): kServeSlots persistent one-wave workgroups on `s`, wave i
+// serving requests from blk[i] (coherent pinned host memory, device view) until blk[0].stop, or
+// until no request came to any slot for idle_ms (t_any: device memory, the latest request time),
+// or after life_ms in all. scratch: kServeSlots x (kStatSlots + 1) DevStats of device memory
+// (statistics and the tier-2 routing count it ignores), list2: kServeSlots x 4 words.
 hipError_t launch_serve(const DevIndex& X, const SearchParams& P, ServeBlock* blk, DevStats* scratch,
-                        uint32_t* list2, uint32_t idle_ms, uint32_t life_ms, hipStream_t s);
+                        uint32_t* list2, unsigned long long* t_any, uint32_t idle_ms, uint32_t life_ms, hipStream_t s);
 
 // Result compaction for the host entry points: pos[0..B] = exclusive prefix sum of n[0..B) (n
 // holds B + 1 entries, n[B] = 0), then query q's n[q] records (k, s at q * stride) are copied to

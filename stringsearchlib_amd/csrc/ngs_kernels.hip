@@ -2844,12 +2844,15 @@ __global__ __launch_bounds__(64, kWaveWavesPerSimd) void k_wave(DevIndex X, Sear
 
 
 
-// ngsServe: the persistent low-latency server. One wave polls the request block (coherent pinned
-// host memory) with system-scope loads, answers each request with wave_query (the tier-1 wave
-// search, unsliced) writing the results straight into the block, then publishes the request's
-// number behind a system-scope release. It exits on blk->stop, after idle_ms without a request
-// or after life_ms in all (the host relaunches it on the next call), so it can never outlive its
-// process by more than that. s_memrealtime (100 MHz) is read through the scalar unit: a read.
+// ngsServe: the persistent low-latency server, one wave per request slot (kServeSlots, so that
+// concurrent score() callers are answered side by side). A wave polls its slot's request block
+// (coherent pinned host memory) with system-scope loads, answers each request with wave_query
+// (the tier-1 wave search, unsliced) writing the results straight into the block, then publishes
+// the request's number behind a system-scope release. The waves exit together: on slot 0's stop
+// flag, after idle_ms without a request on any slot (`last`: the latest request time, raised by
+// every wave) or after life_ms in all (the host relaunches them on the next call), so the server
+// can never outlive its process by more than that. s_memrealtime (100 MHz) is read through the
+// scalar unit: a read.
 __device__ __forceinline__ uint64_t sys_load64(const uint64_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -2857,10 +2860,14 @@ __device__ __forceinline__ uint32_t sys_load32(const uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__global__ __launch_bounds__(64) void k_serve(DevIndex X, SearchParams P0, ServeBlock* blk, DevStats* scratch,
-                                              uint32_t* list2, uint32_t idle_ms, uint32_t life_ms) {
+__global__ __launch_bounds__(64) void k_serve(DevIndex X, SearchParams P0, ServeBlock* blk0, DevStats* scratch0,
+                                              uint32_t* list20, unsigned long long* t_any, uint32_t idle_ms,
+                                              uint32_t life_ms) {
     __shared__ WaveSmem<> S;
-    const uint32_t lane = lane_id();
+    const uint32_t lane = lane_id(), slot = blockIdx.x;
+    ServeBlock* blk = blk0 + slot;
+    DevStats* scratch = scratch0 + (size_t)slot * (kStatSlots + 1);
+    uint32_t* list2 = list20 + 4 * slot;
     uint32_t* count2 = reinterpret_cast<uint32_t*>(scratch + kStatSlots);
     if (lane == 0) __hip_atomic_store(&blk->alive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     uint64_t last = sys_load64(&blk->done_seq);
@@ -2868,7 +2875,11 @@ __global__ __launch_bounds__(64) void k_serve(DevIndex X, SearchParams P0, Serve
     uint64_t t_req = t0;
     for (;;) {
         const uint64_t now = __builtin_amdgcn_s_memrealtime();
-        if (sys_load32(&blk->stop) || now - t_req > (uint64_t)idle_ms * 100000u ||
+        if (now - t_req > (uint64_t)idle_ms * 100000u) {  // this slot idle: any other slot's request?
+            const uint64_t ta = __hip_atomic_load(t_any, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            t_req = ta > t_req ? ta : t_req;
+        }
+        if (sys_load32(&blk0->stop) || now - t_req > (uint64_t)idle_ms * 100000u ||
             now - t0 > (uint64_t)life_ms * 100000u)
             break;
         const uint64_t r = sys_load64(&blk->req_seq);
@@ -2920,6 +2931,7 @@ __global__ __launch_bounds__(64) void k_serve(DevIndex X, SearchParams P0, Serve
         }
         last = seq;
         t_req = __builtin_amdgcn_s_memrealtime();
+        if (lane == 0) atomicMax(t_any, (unsigned long long)t_req);  // (vector atomic: keeps the others up)
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0) __hip_atomic_store(&blk->alive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -4035,8 +4047,8 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
 }
 
 hipError_t launch_serve(const DevIndex& X, const SearchParams& P, ServeBlock* blk, DevStats* scratch,
-                        uint32_t* list2, uint32_t idle_ms, uint32_t life_ms, hipStream_t s) {
-    hipLaunchKernelGGL(k_serve, dim3(1), dim3(64), 0, s, X, P, blk, scratch, list2, idle_ms, life_ms);
+                        uint32_t* list2, unsigned long long* t_any, uint32_t idle_ms, uint32_t life_ms, hipStream_t s) {
+    hipLaunchKernelGGL(k_serve, dim3(kServeSlots), dim3(64), 0, s, X, P, blk, scratch, list2, t_any, idle_ms, life_ms);
     return hipGetLastError();
 }
 
