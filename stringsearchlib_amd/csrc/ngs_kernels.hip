@@ -926,9 +926,7 @@ struct TableGeom {
     static constexpr int kCap = kSlots / 2;    // entries per exact-count pass (<= 50 % load)
 };
 
-// PK: tier 1a's packed staging (lean_query: the heavy list's launch); the main launch's lane-group
-// staging (lean_query_g) needs none of the staging arrays, and 1 KB less LDS per wave
-template <bool LEAN = false, bool PK = LEAN>
+template <bool LEAN = false>
 struct alignas(16) WaveSmem {
     uint32_t table[TableGeom<LEAN>::kSlots];  // exact: (term - lo + 1) << 8 | count; sketch: 8 x u4 counters
     uint64_t cand_own[LEAN ? 1 : kWaveCand];  // (~enc) << 32 | key
@@ -937,10 +935,10 @@ struct alignas(16) WaveSmem {
         if constexpr (LEAN) return reinterpret_cast<uint64_t*>(table);
         else return cand_own;
     }
-    uint2 segtab[PK || !LEAN ? 64 : 1];             // staging: per list {first chunk - position, first | end entry << 16}
-    uint8_t mark[PK || !LEAN ? kWaveChunks : 4];    // staging: list index + 1 at the position of its first chunk
-    unsigned long long lstart[PK ? kDmaRounds : 1];  // tier 1a staging: bit (pre - 1) per list start, 64 chunk positions a word
-    uint32_t g4[PK ? 64 : 1];        // tier 1a: per list lane, the 16-byte chunk of its list's first posting
+    uint2 segtab[64];                // staging: per list {first chunk - position, first | end entry << 16}
+    uint8_t mark[kWaveChunks];       // staging: list index + 1 at the position of its first chunk
+    unsigned long long lstart[kDmaRounds];  // tier 1a staging: bit (pre - 1) per list start, 64 chunk positions a word
+    uint32_t g4[LEAN ? 64 : 1];      // tier 1a: per list lane, the 16-byte chunk of its list's first posting
     uint32_t surv_t[kWaveSurv];      // survivor terms
     uint32_t cbuf[64];               // sketch candidates (terms)
     uint8_t surv_c[kWaveSurv];       // hit count, | 0x80 for a Levenshtein (short search) match count
@@ -1270,8 +1268,8 @@ __device__ void wave_emit(SM& S, const DevIndex& X, const SearchParams& P, uint3
     wave_sync();
 }
 
-template <bool LEAN, bool PK>
-__device__ __forceinline__ void surv_append(WaveSmem<LEAN, PK>& S, bool pass, uint32_t t, uint32_t code, uint32_t& surv_n) {
+template <bool LEAN>
+__device__ __forceinline__ void surv_append(WaveSmem<LEAN>& S, bool pass, uint32_t t, uint32_t code, uint32_t& surv_n) {
     const unsigned long long b = __ballot(pass);
     if (pass) {
         const uint32_t i = surv_n + rank_below(b);
@@ -1282,8 +1280,8 @@ __device__ __forceinline__ void surv_append(WaveSmem<LEAN, PK>& S, bool pass, ui
 }
 
 // zero the wave's LDS table (16-byte stores, lane-strided)
-template <bool LEAN, bool PK>
-__device__ __forceinline__ void clear_table(WaveSmem<LEAN, PK>& S, uint32_t lane) {
+template <bool LEAN>
+__device__ __forceinline__ void clear_table(WaveSmem<LEAN>& S, uint32_t lane) {
     uint4* T4 = reinterpret_cast<uint4*>(S.table);
 #pragma unroll
     for (uint32_t i = 0; i < (uint32_t)TableGeom<LEAN>::kSlots / 256; ++i) T4[lane + 64 * i] = make_uint4(0, 0, 0, 0);
@@ -1292,8 +1290,8 @@ __device__ __forceinline__ void clear_table(WaveSmem<LEAN, PK>& S, uint32_t lane
 // Exact counts of a sketch part's nc <= 64 candidate entries (S.cbuf; lane l < nc takes entry l):
 // a term's count is the number of candidates holding it (every entry of a term lands in the same
 // cell), owned by the first of them. Terms whose count reaches cmin become survivors.
-template <bool LEAN, bool PK>
-__device__ __forceinline__ void cand_counts(WaveSmem<LEAN, PK>& S, uint32_t nc, uint32_t cmin, uint32_t n_short,
+template <bool LEAN>
+__device__ __forceinline__ void cand_counts(WaveSmem<LEAN>& S, uint32_t nc, uint32_t cmin, uint32_t n_short,
                                             uint32_t n_terms, uint32_t& surv_n) {
     const uint32_t lane = lane_id();
     uint32_t lc = lane;  // opaque: the slot address is made here, not kept across the part loop (spilled)
@@ -1494,8 +1492,8 @@ __device__ __forceinline__ void part_exact(WaveSmem<LEAN>& S, uint4 (&v)[kDmaRou
 // the wave gets their exact counts by comparing the <= 64 candidates with each other. Returns the number of candidate entries; above 64 the caller counts the part exactly
 // (the table is clean again). (u16 counters with no-return adds were measured: the 4x fewer
 // cells per KB cost more in false candidates than the returns cost in waits.)
-template <bool LEAN, bool PK, int NR = kDmaRounds>
-__device__ __forceinline__ uint32_t part_sketch(WaveSmem<LEAN, PK>& S, const uint4 (&v)[NR], uint32_t vmask,
+template <bool LEAN, int NR = kDmaRounds>
+__device__ __forceinline__ uint32_t part_sketch(WaveSmem<LEAN>& S, const uint4 (&v)[NR], uint32_t vmask,
                                                 uint32_t mt, uint32_t cmin, uint32_t n_short, uint32_t n_terms,
                                                 uint32_t& surv_n) {
     const uint32_t lane = lane_id();
@@ -1572,7 +1570,7 @@ __device__ __forceinline__ uint32_t part_sketch(WaveSmem<LEAN, PK>& S, const uin
 // caller hands the query to tier 1b. Parts are cut to a quarter of a sketch part so that pairs
 // colliding in the 8,192 cells stay few.
 template <int NR = kDmaRounds>
-__device__ __forceinline__ uint32_t part_ones(WaveSmem<true, true>& S, const uint4 (&v)[NR], uint32_t vmask, uint32_t mt,
+__device__ __forceinline__ uint32_t part_ones(WaveSmem<true>& S, const uint4 (&v)[NR], uint32_t vmask, uint32_t mt,
                                               uint32_t n_short, uint32_t n_terms, uint32_t& surv_n,
                                               uint32_t* __restrict__ et, uint8_t* __restrict__ ec, uint32_t& spilled,
                                               uint32_t ecap) {
@@ -2012,7 +2010,7 @@ __device__ __forceinline__ void wave_query(WaveSmem<>& S, const uint32_t q, cons
 // non-empty lists' {first chunk - pre, entry bounds} sit in segtab by ordinal. (stage_part, the
 // full kernel's staging, spends a marker array and a max-scan per round on the same lookup.)
 template <bool G4>
-__device__ __forceinline__ void lean_stage(WaveSmem<true, true>& S, gptr<uint4> post4, uint64_t gbase,
+__device__ __forceinline__ void lean_stage(WaveSmem<true>& S, gptr<uint4> post4, uint64_t gbase,
                                            uint32_t a0, uint32_t cur, uint32_t len, uint32_t nch, uint32_t incl,
                                            uint32_t mt, uint4 (&v)[kDmaRounds], uint32_t& vmask) {
     const uint32_t lane = lane_id();
@@ -2083,8 +2081,7 @@ struct LeanPlan {
     bool rank;
     uint64_t gbase, p_total;
 };
-template <bool PK>
-__device__ __forceinline__ uint32_t lean_route(WaveSmem<true, PK>& S, const uint32_t q, const DevIndex& X,
+__device__ __forceinline__ uint32_t lean_route(WaveSmem<true>& S, const uint32_t q, const DevIndex& X,
                                                const SearchParams& P, const uint8_t* __restrict__ qnorm,
                                                const uint64_t* __restrict__ qoff, const uint32_t* __restrict__ qm,
                                                uint32_t* __restrict__ out_n, uint32_t* __restrict__ out_k,
@@ -2135,7 +2132,7 @@ __device__ __forceinline__ uint32_t lean_route(WaveSmem<true, PK>& S, const uint
 // with its own staging (lean_stage) and the sketch counter part_sketch; a query that needs exact
 // counting, a short search or more than kEmitCap survivor slots is handed to tier 1b untouched.
 template <bool ONES>
-__device__ __forceinline__ void lean_query(WaveSmem<true, true>& S, const uint32_t q, const DevIndex& X,
+__device__ __forceinline__ void lean_query(WaveSmem<true>& S, const uint32_t q, const DevIndex& X,
                                            const SearchParams& P, const uint8_t* __restrict__ qnorm,
                                            const uint64_t* __restrict__ qoff, const uint32_t* __restrict__ qm,
                                            uint32_t* __restrict__ out_n, uint32_t* __restrict__ out_k,
@@ -2415,7 +2412,7 @@ __device__ __forceinline__ void lean_query(WaveSmem<true, true>& S, const uint32
 // undercount): entry e of chunk k is in the segment iff 4k + e - head < len.
 
 // sketch count of a part staged by lane groups (3 <= cmin <= 15): part_sketch's one-wave loose path
-__device__ __forceinline__ uint32_t lean_sketch_g(WaveSmem<true, false>& S, const uint4 (&v)[kDmaRounds], uint32_t R,
+__device__ __forceinline__ uint32_t lean_sketch_g(WaveSmem<true>& S, const uint4 (&v)[kDmaRounds], uint32_t R,
                                                   uint32_t k0, uint32_t G, uint32_t nch, uint32_t head, uint32_t len,
                                                   uint32_t cmin, uint32_t n_short, uint32_t n_terms, uint32_t& surv_n) {
     const uint32_t lane = lane_id();
@@ -2479,7 +2476,7 @@ struct PartGroups {
     uint32_t nch, head, len, R;
 };
 
-__device__ __forceinline__ void lean_query_g(WaveSmem<true, false>& S, const uint32_t q, const DevIndex& X,
+__device__ __forceinline__ void lean_query_g(WaveSmem<true>& S, const uint32_t q, const DevIndex& X,
                                              const SearchParams& P, const uint8_t* __restrict__ qnorm,
                                              const uint64_t* __restrict__ qoff, const uint32_t* __restrict__ qm,
                                              uint32_t* __restrict__ out_n, uint32_t* __restrict__ out_k,
@@ -2957,7 +2954,7 @@ __global__ __launch_bounds__(64, HEAVY ? kHeavyLeanWavesPerSimd : kLeanWavesPerS
                                                                     uint32_t* __restrict__ fb, uint32_t* __restrict__ fbc,
                                                                     const uint32_t* __restrict__ qlist,
                                                                     const uint32_t* __restrict__ qcount) {
-    __shared__ WaveSmem<true, HEAVY> S;
+    __shared__ WaveSmem<true> S;
     // lane-group staging (lean_query_g) for the main launch; the heavy list's launch keeps the packed
     // staging (lean_query): its threshold-0 queries' part_ones parts are ~3 chunks per list, where a
     // per-list cap splits most parts
