@@ -1227,6 +1227,13 @@ int queue_search(Library& L, Replica& R, Context& c, const uint8_t* d_raw, const
     // tools/ubench/graph_launch.hip). Such calls leave the replica's main-launch order alone
     // (main_ev): their main launch only routes, every lean query being on the heavy list.
     static const bool no_graphs = std::getenv("NGS_SYNC_DEBUG") != nullptr;
+    // A capture runs alone: no other thread queues a call meanwhile (the threaded test saw another
+    // thread's launches fail with "dependency created on uncaptured work in another stream" while
+    // a capture was open). Calls hold the lock shared while they queue; a capture takes it
+    // exclusively if it can, and is otherwise left for a later occurrence of its call.
+    static std::shared_mutex capture_mu;
+    std::shared_lock<std::shared_mutex> queue_lock(capture_mu, std::defer_lock);
+    std::unique_lock<std::shared_mutex> capture_lock(capture_mu, std::defer_lock);
     bool capture = false;
     std::vector<uint8_t> sig;
     // Only on the context's own stream: a capture takes in whatever any thread queues on the stream
@@ -1245,6 +1252,7 @@ int queue_search(Library& L, Replica& R, Context& c, const uint8_t* d_raw, const
         put(flags, sizeof(flags));
         for (auto& g : c.graphs) {
             if (g.first != sig) continue;
+            queue_lock.lock();
             if (!HIP_CHECK(hipGraphLaunch(g.second, s))) return -4;
             c.stats_clean = true;
             g_host_phase[kHpReplays].fetch_add(1, std::memory_order_relaxed);
@@ -1256,6 +1264,8 @@ int queue_search(Library& L, Replica& R, Context& c, const uint8_t* d_raw, const
             c.gseen.push_back(sig);
         }
     }
+    if (capture && !capture_lock.try_lock()) capture = false;  // (the signature stays seen: next time)
+    if (!capture) queue_lock.lock();
     if (capture && !HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal))) {
         (void)hipGetLastError();
         capture = false;
