@@ -73,7 +73,7 @@ enum HostPhase : int {
     kHpRecords,       // the records back, marshalled into the new[]'d arrays as they land
     kHpCall,          // the whole call (scoreBatch / searchBatch)
     kHpCalls,         // (count) calls
-    kHpReplays,       // (count) one-stream calls replayed from a captured graph (queue_search)
+    kHpReplays,       // (count) one-stream calls replayed from a graph (queue_search)
     kHpN
 };
 std::atomic<uint64_t> g_host_phase[kHpN];
@@ -361,14 +361,14 @@ struct Context {
     Pinned h_off, h_raw, h_res;  // queries in; results out
     uint8_t* d_sio = nullptr;     // the latency path's block (kSioBytes): one copy in, one copy out
     uint8_t* h_sio = nullptr;     // ... its pinned host image
-    // one-stream calls (queue_search): calls captured as graphs, replayed when a call's launch
-    // arguments (the signature) repeat one of them; gseen: recent signatures, a call is captured on
+    // one-stream calls (queue_search): calls built as graphs, replayed when a call's launch
+    // arguments (the signature) repeat one of them; gseen: recent signatures, a call is built on
     // its second occurrence. Up to kGraphs of each (a pipelined caller rotates its output buffers
     // over the contexts in flight: C2's bench loop, 4 buffers over 3 contexts)
     static constexpr size_t kGraphs = 8;
     std::vector<std::pair<std::vector<uint8_t>, hipGraphExec_t>> graphs;
     std::vector<std::vector<uint8_t>> gseen;
-    bool gfail = false;  // a capture failed: this context queues its calls one by one
+    bool gfail = false;  // a graph failed to build: this context queues its calls one by one
 
     ~Context() {
         hipSetDevice(device);
@@ -1221,25 +1221,16 @@ int queue_search(Library& L, Replica& R, Context& c, const uint8_t* d_raw, const
     if (!R.index_for(P.valid, X)) return -4;
     // A one-stream call (side == s: batches up to kOneStreamBatch queries that are all heavy, C2) is
     // ~0.1 ms of GPU work for ~12 queued operations, 50 us of host time per call. When a call's
-    // launch arguments repeat the context's previous call (a server's or a bench's batches into the
-    // same buffers), the sequence is captured as a graph on the second occurrence and replayed
+    // launch arguments repeat an earlier call of the context (a server's or a bench's batches into
+    // the same buffers), the sequence is built as a graph on the second occurrence and replayed
     // from then on (one submission: ~4 us of host time for 10 launches against ~30,
     // tools/ubench/graph_launch.hip). Such calls leave the replica's main-launch order alone
     // (main_ev): their main launch only routes, every lean query being on the heavy list.
     static const bool no_graphs = std::getenv("NGS_SYNC_DEBUG") != nullptr;
-    // A capture runs alone: no other thread queues a call meanwhile (the threaded test saw another
-    // thread's launches fail with "dependency created on uncaptured work in another stream" while
-    // a capture was open). Calls hold the lock shared while they queue; a capture takes it
-    // exclusively if it can, and is otherwise left for a later occurrence of its call.
-    static std::shared_mutex capture_mu;
-    std::shared_lock<std::shared_mutex> queue_lock(capture_mu, std::defer_lock);
-    std::unique_lock<std::shared_mutex> capture_lock(capture_mu, std::defer_lock);
     bool capture = false;
     std::vector<uint8_t> sig;
-    // Only on the context's own stream: a capture takes in whatever any thread queues on the stream
-    // meanwhile, so a caller's stream (ngsSearchDevice), which other threads may share, is never
-    // captured (nor the null stream, which cannot be).
-    if (!small && side == s && s == c.stream && !timing && !no_graphs && !c.gfail) {
+    // (not on the null stream)
+    if (!small && side == s && s && !timing && !no_graphs && !c.gfail) {
         auto put = [&](const void* p, size_t n) {
             sig.insert(sig.end(), static_cast<const uint8_t*>(p), static_cast<const uint8_t*>(p) + n);
         };
@@ -1252,7 +1243,6 @@ int queue_search(Library& L, Replica& R, Context& c, const uint8_t* d_raw, const
         put(flags, sizeof(flags));
         for (auto& g : c.graphs) {
             if (g.first != sig) continue;
-            queue_lock.lock();
             if (!HIP_CHECK(hipGraphLaunch(g.second, s))) return -4;
             c.stats_clean = true;
             g_host_phase[kHpReplays].fetch_add(1, std::memory_order_relaxed);
@@ -1264,20 +1254,25 @@ int queue_search(Library& L, Replica& R, Context& c, const uint8_t* d_raw, const
             c.gseen.push_back(sig);
         }
     }
-    if (capture && !capture_lock.try_lock()) capture = false;  // (the signature stays seen: next time)
-    if (!capture) queue_lock.lock();
-    if (capture && !HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal))) {
-        (void)hipGetLastError();
-        capture = false;
-        c.gfail = true;
-    }
-    auto queue_ops = [&]() -> bool {
-        if (!zero_in_prep && !small &&
-            !HIP_CHECK(hipMemsetAsync(c.d_stats, 0, sizeof(DevStats) * (kStatSlots + 1 + 2 * kListSlots), s)))
-            return false;
+    // the call's operations, queued on s, or with gb appended to a graph being built (one-stream calls)
+    auto queue_ops = [&](GraphBuild* gb) -> bool {
+        const size_t stat_bytes = sizeof(DevStats) * (kStatSlots + 1 + 2 * kListSlots);
+        if (!zero_in_prep && !small) {
+            if (gb) {
+                hipMemsetParams mp{};
+                mp.dst = c.d_stats;
+                mp.value = 0;
+                mp.elementSize = 4;
+                mp.width = stat_bytes / 4;
+                mp.height = 1;
+                if (!HIP_CHECK(hipGraphAddMemsetNode(&gb->last, gb->graph, nullptr, 0, &mp))) return false;
+            } else if (!HIP_CHECK(hipMemsetAsync(c.d_stats, 0, stat_bytes, s))) {
+                return false;
+            }
+        }
         if (timing) HIP_CHECK(hipEventRecord(c.ev[0], s));
         if (!HIP_CHECK(launch_prep(d_raw, d_off, B, P, c.d_norm, c.d_qm, X.csize, X, c.d_heavy, gc + 3, c.d_full,
-                                   gc + 5, c.d_lslots, c.d_lctr, s, side, c.prep_ev, c.lists_ev)))
+                                   gc + 5, c.d_lslots, c.d_lctr, s, side, c.prep_ev, c.lists_ev, gb)))
             return false;
         if (timing) HIP_CHECK(hipEventRecord(c.ev[1], s));  // the end of k_prep is the start of the tier-1 phase
         // the main tier-1a launches of this replica's calls one after another: with two calls in flight
@@ -1287,7 +1282,7 @@ int queue_search(Library& L, Replica& R, Context& c, const uint8_t* d_raw, const
         std::unique_lock<std::mutex> g(R.main_mu, std::defer_lock);
         hipEvent_t mev = nullptr;
         bool mwait = false;
-        if (!small && !capture) {
+        if (!small && !gb) {
             g.lock();
             if (!R.main_ev && !HIP_CHECK(hipEventCreateWithFlags(&R.main_ev, hipEventDisableTiming))) return false;
             mev = R.main_ev;
@@ -1296,19 +1291,29 @@ int queue_search(Library& L, Replica& R, Context& c, const uint8_t* d_raw, const
         }
         if (!HIP_CHECK(launch_fast(X, P, c.d_norm, d_off, c.d_qm, d_n, d_k, d_s, c.d_list2, gc + 1, c.d_fb, gc + 2,
                                    c.d_fb2, gc + 4, c.d_heavy, gc + 3, c.d_full, gc + 5, c.d_glist, gc, sd, s, side,
-                                   side2, c.join, c.join2, c.lists_ev, all_heavy, mev, mwait)))
+                                   side2, c.join, c.join2, c.lists_ev, all_heavy, mev, mwait, gb)))
             return false;
         if (timing) HIP_CHECK(hipEventRecord(c.ev[3], s));
         // the statistics and the path counts in one read-back (the general path adds no statistics)
-        return small || HIP_CHECK(hipMemcpyAsync(c.h_stats, c.d_stats, kSioStats, hipMemcpyDeviceToHost, s));
+        if (small) return true;
+        if (gb) {
+            hipGraphNode_t n = nullptr;
+            if (!HIP_CHECK(hipGraphAddMemcpyNode1D(&n, gb->graph, gb->last ? &gb->last : nullptr, gb->last ? 1 : 0,
+                                                   c.h_stats, c.d_stats, kSioStats, hipMemcpyDeviceToHost)))
+                return false;
+            gb->last = n;
+            return true;
+        }
+        return HIP_CHECK(hipMemcpyAsync(c.h_stats, c.d_stats, kSioStats, hipMemcpyDeviceToHost, s));
     };
-    const bool queued = queue_ops();
+    // A graph is built node by node (no stream capture, which in this runtime fails other threads'
+    // launches while it is open: the threaded test's scoreBatch calls did) and instantiated
     if (capture) {
-        hipGraph_t graph = nullptr;
+        GraphBuild gb;
         hipGraphExec_t exec = nullptr;
-        const bool ended = HIP_CHECK(hipStreamEndCapture(s, &graph));
-        const bool made = ended && queued && graph && HIP_CHECK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
-        if (graph) hipGraphDestroy(graph);
+        bool made = HIP_CHECK(hipGraphCreate(&gb.graph, 0)) && queue_ops(&gb) &&
+                    HIP_CHECK(hipGraphInstantiate(&exec, gb.graph, nullptr, nullptr, 0));
+        if (gb.graph) hipGraphDestroy(gb.graph);
         (void)hipGetLastError();
         if (made) {
             c.gseen.erase(std::find(c.gseen.begin(), c.gseen.end(), sig));
@@ -1319,10 +1324,11 @@ int queue_search(Library& L, Replica& R, Context& c, const uint8_t* d_raw, const
             c.graphs.emplace_back(std::move(sig), exec);
             if (!HIP_CHECK(hipGraphLaunch(exec, s))) return -4;
         } else {  // nothing of the call ran: queue it one by one, and so from now on
+            if (exec) hipGraphExecDestroy(exec);
             c.gfail = true;
-            if (!queue_ops()) return -4;
+            if (!queue_ops(nullptr)) return -4;
         }
-    } else if (!queued) {
+    } else if (!queue_ops(nullptr)) {
         return -4;
     }
     c.stats_clean = !small && P.waves == 0;  // k_lists queued: it leaves the list counters zero

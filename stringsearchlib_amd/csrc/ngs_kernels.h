@@ -13,10 +13,20 @@ namespace ngs {
 // 2 * kListSlots * ceil(B / kListSlots) entries, `ctr` 2 * kListSlots counters 16 words apart
 // (zeroed by the caller). The lists are merged on `side` after an event on s (prep_ev), so the
 // main tier-1a launch queued next on s does not wait for them; lists_ev marks them done.
+// A graph being built node by node (hipGraphAdd*Node, no stream capture): a launch function given
+// one appends its kernels after `last` instead of queueing them. One-stream calls only (side ==
+// side2 == s: no events). err keeps the first failure.
+struct GraphBuild {
+    hipGraph_t graph = nullptr;
+    hipGraphNode_t last = nullptr;
+    hipError_t err = hipSuccess;
+};
+
 hipError_t launch_prep(const uint8_t* raw, const uint64_t* off, uint32_t B, const SearchParams& P,
                        uint8_t* qnorm, uint32_t* qm, uint32_t cs, const DevIndex& X, uint32_t* heavy,
                        uint32_t* hcount, uint32_t* full, uint32_t* fcount, uint32_t* slots, uint32_t* ctr,
-                       hipStream_t s, hipStream_t side, hipEvent_t prep_ev, hipEvent_t lists_ev);
+                       hipStream_t s, hipStream_t side, hipEvent_t prep_ev, hipEvent_t lists_ev,
+                       GraphBuild* gb = nullptr);
 
 // Fused per-query kernel: short Levenshtein scan of shortLib (4 <= m < 9), 3-gram posting
 // count in an LDS hash table per term-id part, threshold, term->key weighting, per-key max
@@ -29,7 +39,8 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
                        const uint32_t* heavy, const uint32_t* hcount, const uint32_t* full,
                        const uint32_t* fcount, uint32_t* glist, uint32_t* gcount, DevStats* stats, hipStream_t s,
                        hipStream_t side, hipStream_t side2, hipEvent_t join, hipEvent_t join2,
-                       hipEvent_t lists_ev, bool all_heavy = false, hipEvent_t main_ev = nullptr, bool main_wait = false);
+                       hipEvent_t lists_ev, bool all_heavy = false, hipEvent_t main_ev = nullptr, bool main_wait = false,
+                       GraphBuild* gb = nullptr);
 
 // The low-latency server (ngsServe): kServeSlots persistent one-wave workgroups on `s`, wave i
 // serving requests from blk[i] (coherent pinned host memory, device view) until blk[0].stop, or

@@ -15,6 +15,7 @@
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
+#include <tuple>
 
 #include "ngs_kernels.h"
 
@@ -3849,14 +3850,43 @@ static void dbg_check(hipStream_t s, const char* what) {
     if (e != hipSuccess) std::fprintf(stderr, "ngram_search: NGS_SYNC_DEBUG: %s failed: %s\n", what, hipGetErrorString(e));
 }
 
+// A kernel launch queued on s, or with gb, a kernel node appended to gb's graph after its last
+// node (the arguments converted to the kernel's parameter types and copied into the node)
+template <typename... KArgs, typename... Args>
+static void klaunch(GraphBuild* gb, void (*k)(KArgs...), dim3 grid, dim3 block, size_t shm, hipStream_t s,
+                    Args... args) {
+    if (!gb) {
+        hipLaunchKernelGGL(k, grid, block, shm, s, args...);
+        return;
+    }
+    if (gb->err != hipSuccess) return;
+    std::tuple<KArgs...> vals(static_cast<KArgs>(args)...);
+    void* ptrs[sizeof...(KArgs) > 0 ? sizeof...(KArgs) : 1];
+    std::apply([&](auto&... v) {
+        size_t i = 0;
+        ((ptrs[i++] = static_cast<void*>(&v)), ...);
+    }, vals);
+    hipKernelNodeParams p{};
+    p.func = reinterpret_cast<void*>(k);
+    p.gridDim = grid;
+    p.blockDim = block;
+    p.sharedMemBytes = (unsigned)shm;
+    p.kernelParams = ptrs;
+    p.extra = nullptr;
+    hipGraphNode_t n = nullptr;
+    gb->err = hipGraphAddKernelNode(&n, gb->graph, gb->last ? &gb->last : nullptr, gb->last ? 1 : 0, &p);
+    if (gb->err == hipSuccess) gb->last = n;
+}
+
 hipError_t launch_prep(const uint8_t* raw, const uint64_t* off, uint32_t B, const SearchParams& P, uint8_t* qnorm,
                        uint32_t* qm, uint32_t cs, const DevIndex& X, uint32_t* heavy, uint32_t* hcount,
                        uint32_t* full, uint32_t* fcount, uint32_t* slots, uint32_t* ctr, hipStream_t s,
-                       hipStream_t side, hipEvent_t prep_ev, hipEvent_t lists_ev) {
+                       hipStream_t side, hipEvent_t prep_ev, hipEvent_t lists_ev, GraphBuild* gb) {
     if (!B) return hipSuccess;
+    if (gb && side != s) return hipErrorInvalidValue;  // (a built graph has no events)
     const uint32_t cap = (B + kListSlots - 1) / kListSlots;
     const bool lists = P.waves == 0;
-    hipLaunchKernelGGL(k_prep, dim3((B + 3) / 4), dim3(64), 0, s, raw, off, B, P, qnorm, qm, cs, X,
+    klaunch(gb, k_prep, dim3((B + 3) / 4), dim3(64), 0, s, raw, off, B, P, qnorm, qm, cs, X,
                        lists ? slots : nullptr, ctr, cap);
     dbg_check(s, "k_prep");
     if (lists) {  // on the side stream: the main tier-1a launch needs only k_prep's output
@@ -3866,11 +3896,11 @@ hipError_t launch_prep(const uint8_t* raw, const uint64_t* off, uint32_t B, cons
         if (side != s &&
             ((e = hipEventRecord(prep_ev, s)) != hipSuccess || (e = hipStreamWaitEvent(side, prep_ev, 0)) != hipSuccess))
             return e;
-        hipLaunchKernelGGL(k_lists, dim3(1), dim3(64), 0, side, slots, ctr, cap, heavy, hcount, full, fcount);
+        klaunch(gb, k_lists, dim3(1), dim3(64), 0, side, slots, ctr, cap, heavy, hcount, full, fcount);
         dbg_check(side, "k_lists");
         if (side != s && (e = hipEventRecord(lists_ev, side)) != hipSuccess) return e;
     }
-    return hipGetLastError();
+    return gb ? gb->err : hipGetLastError();
 }
 
 // Workgroups for every (query, slice) item heavy_slices can make from a list of up to n_queries
@@ -3892,8 +3922,9 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
                        const uint32_t* heavy, const uint32_t* hcount, const uint32_t* full,
                        const uint32_t* fcount, uint32_t* glist, uint32_t* gcount, DevStats* stats, hipStream_t s,
                        hipStream_t side, hipStream_t side2, hipEvent_t join, hipEvent_t join2,
-                       hipEvent_t lists_ev, bool all_heavy, hipEvent_t main_ev, bool main_wait) {
+                       hipEvent_t lists_ev, bool all_heavy, hipEvent_t main_ev, bool main_wait, GraphBuild* gb) {
     if (!P.n_queries) return hipSuccess;
+    if (gb && (side != s || side2 != s || main_ev)) return hipErrorInvalidValue;  // (no events in a built graph)
     hipError_t e = hipSuccess;
     switch (P.waves) {  // SearchParams.waves: 0 = tier 1a + 1b (batches), 1 = tier 1b alone (latency path)
         case 0: {
@@ -3919,7 +3950,7 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
             // one and recorded after it, so that two calls in flight do not run their main launches at once
             auto main_lean = [&]() {
                 if (main_ev && main_wait) (void)hipStreamWaitEvent(s, main_ev, 0);
-                hipLaunchKernelGGL((k_wave_lean<false>), dim3(P.n_queries), dim3(64), 0, s, X,
+                klaunch(gb, (k_wave_lean<false>), dim3(P.n_queries), dim3(64), 0, s, X,
                                    P, qnorm, off, qm,
                                    out_n, out_k, out_s, list2, count2, stats, fb, fbc, (const uint32_t*)nullptr,
                                    (const uint32_t*)nullptr);
@@ -3945,36 +3976,36 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
                     const bool ones = !X.rank_post && !(1.0f / (float)n_min < P.thr);
                     PH.hbase = 0;
                     if (ones)
-                        hipLaunchKernelGGL((k_wave_lean<true, true>), dim3(ghl), dim3(64), 0, side, X, PH,
+                        klaunch(gb, (k_wave_lean<true, true>), dim3(ghl), dim3(64), 0, side, X, PH,
                                            qnorm, off, qm, out_n, out_k, out_s, list2, count2, stats, fb2, fbc2, heavy,
                                            hcount);
                     else
-                        hipLaunchKernelGGL((k_wave_lean<true, false>), dim3(ghl), dim3(64), 0, side, X, PH, qnorm,
+                        klaunch(gb, (k_wave_lean<true, false>), dim3(ghl), dim3(64), 0, side, X, PH, qnorm,
                                            off, qm, out_n, out_k, out_s, list2, count2, stats, fb2, fbc2, heavy, hcount);
                     dbg_check(side, "k_wave_lean (heavy list)");
                     if (ghl < ghb) {  // items past the first grid, if this call has more than the last
                         PH.hbase = ghl;
                         const uint32_t gov = std::min<uint32_t>(ghb - ghl, kHeavyOverflowGrid);
                         if (ones)
-                            hipLaunchKernelGGL((k_wave_lean<true, true, true>), dim3(gov), dim3(64), 0,
+                            klaunch(gb, (k_wave_lean<true, true, true>), dim3(gov), dim3(64), 0,
                                                side, X, PH, qnorm, off, qm, out_n, out_k, out_s, list2, count2, stats,
                                                fb2, fbc2, heavy, hcount);
                         else
-                            hipLaunchKernelGGL((k_wave_lean<true, false, true>), dim3(gov), dim3(64), 0, side,
+                            klaunch(gb, (k_wave_lean<true, false, true>), dim3(gov), dim3(64), 0, side,
                                                X, PH, qnorm, off, qm, out_n, out_k, out_s, list2, count2, stats, fb2,
                                                fbc2, heavy, hcount);
                         dbg_check(side, "k_wave_lean (heavy list overflow)");
                         PH.hbase = 0;
                     }
-                    hipLaunchKernelGGL(k_emit<true>, dim3((gh + kEmitWaves - 1) / kEmitWaves), dim3(64 * kEmitWaves), 0,
+                    klaunch(gb, k_emit<true>, dim3((gh + kEmitWaves - 1) / kEmitWaves), dim3(64 * kEmitWaves), 0,
                                        side, X, PH, qnorm, off, qm, out_n, out_k, out_s, stats, heavy, hcount);
                     dbg_check(side, "k_emit (heavy list)");
                 }
-                hipLaunchKernelGGL(k_wave, dim3(g1s), dim3(64), 0, side, X, PHO, qnorm, off, qm, out_n, out_k,
+                klaunch(gb, k_wave, dim3(g1s), dim3(64), 0, side, X, PHO, qnorm, off, qm, out_n, out_k,
                                    out_s, list2, count2, stats, (const uint32_t*)fb2, (const uint32_t*)fbc2);
                 dbg_check(side, "k_wave (heavy hand-overs)");
                 if (P.nslices > 1) {
-                    hipLaunchKernelGGL(k_merge, dim3(g1b), dim3(64), 0, side, X, P, (const uint32_t*)fb2,
+                    klaunch(gb, k_merge, dim3(g1b), dim3(64), 0, side, X, P, (const uint32_t*)fb2,
                                        (const uint32_t*)fbc2, out_n, out_k, out_s, stats);
                     dbg_check(side, "k_merge (heavy hand-overs)");
                 }
@@ -3988,7 +4019,7 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
                 SearchParams PF = P;
                 PF.nslices = 1;
                 PF.qhead = gcount + 10;
-                hipLaunchKernelGGL(k_wave, dim3(gfull), dim3(64), 0, side2, X, PF, qnorm, off, qm, out_n, out_k,
+                klaunch(gb, k_wave, dim3(gfull), dim3(64), 0, side2, X, PF, qnorm, off, qm, out_n, out_k,
                                    out_s, list2, count2, stats, full, fcount);
                 dbg_check(side2, "k_wave (full list)");
             }
@@ -3997,19 +4028,19 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
             // no query and hands none over (it returns before either for a heavy or full one), so its
             // k_emit and hand-over launches would find nothing
             if (!all_heavy) {
-                hipLaunchKernelGGL(k_emit<false>, dim3((P.n_queries + kEmitWaves - 1) / kEmitWaves), dim3(64 * kEmitWaves), 0,
+                klaunch(gb, k_emit<false>, dim3((P.n_queries + kEmitWaves - 1) / kEmitWaves), dim3(64 * kEmitWaves), 0,
                                    s, X, P, qnorm, off, qm, out_n, out_k, out_s, stats, (const uint32_t*)nullptr,
                                    (const uint32_t*)nullptr);
                 dbg_check(s, "k_emit");
             }
             // tier 1b over the queries tier 1a handed over
             if (!all_heavy) {
-                hipLaunchKernelGGL(k_wave, dim3(g1s), dim3(64), 0, s, X, PM, qnorm, off, qm, out_n, out_k, out_s,
+                klaunch(gb, k_wave, dim3(g1s), dim3(64), 0, s, X, PM, qnorm, off, qm, out_n, out_k, out_s,
                                    list2, count2, stats, (const uint32_t*)fb, (const uint32_t*)fbc);
                 dbg_check(s, "k_wave (hand-overs)");
             }
             if (P.nslices > 1 && !all_heavy) {
-                hipLaunchKernelGGL(k_merge, dim3(g1b), dim3(64), 0, s, X, P, (const uint32_t*)fb, (const uint32_t*)fbc,
+                klaunch(gb, k_merge, dim3(g1b), dim3(64), 0, s, X, P, (const uint32_t*)fb, (const uint32_t*)fbc,
                                    out_n, out_k, out_s, stats);
                 dbg_check(s, "k_merge (hand-overs)");
             }
@@ -4020,12 +4051,12 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
             break;
         }
         case 1:
-            hipLaunchKernelGGL(k_wave, dim3(P.n_queries * std::max<uint32_t>(P.nslices, 1u)), dim3(64), 0, s, X, P,
+            klaunch(gb, k_wave, dim3(P.n_queries * std::max<uint32_t>(P.nslices, 1u)), dim3(64), 0, s, X, P,
                                qnorm, off, qm, out_n, out_k, out_s, list2, count2, stats, (const uint32_t*)nullptr,
                                (const uint32_t*)nullptr);
             dbg_check(s, "k_wave");
             if (P.nslices > 1) {
-                hipLaunchKernelGGL(k_merge, dim3(P.n_queries), dim3(64), 0, s, X, P, (const uint32_t*)nullptr,
+                klaunch(gb, k_merge, dim3(P.n_queries), dim3(64), 0, s, X, P, (const uint32_t*)nullptr,
                                    (const uint32_t*)nullptr, out_n, out_k, out_s, stats);
                 dbg_check(s, "k_merge");
             }
@@ -4037,9 +4068,10 @@ hipError_t launch_fast(const DevIndex& X, const SearchParams& P, const uint8_t* 
     // long ones (> 63 grams) and those bound for the general path: 128 blocks, grid-stride (1,024
     // blocks that mostly exit cost ~20 us at C2 and ~50 us at C3 per call)
     const uint32_t grid2 = std::min<uint32_t>(P.n_queries, P.limit > kWaveMaxLimit ? 1024u : 128u);
-    hipLaunchKernelGGL(k_fast, dim3(grid2), dim3(kFastThreads), 0, s, X, P, qnorm, off, qm, out_n, out_k, out_s,
+    klaunch(gb, k_fast, dim3(grid2), dim3(kFastThreads), 0, s, X, P, qnorm, off, qm, out_n, out_k, out_s,
                        (const uint32_t*)list2, (const uint32_t*)count2, glist, gcount, stats);
     dbg_check(s, "k_fast");
+    if (gb) return gb->err;
     return hipGetLastError();
 }
 
