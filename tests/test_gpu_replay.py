@@ -49,7 +49,7 @@ def test_replayed_calls_read_their_own_queries(weighted):
     d_key = torch.empty(B * stride, dtype=torch.int32, device=dev)
     d_sc = torch.empty(B * stride, dtype=torch.float32, device=dev)
     L = _native.lib()
-    side = torch.cuda.Stream(dev)  # (the null stream is never captured)
+    side = torch.cuda.Stream(dev)  # (calls on the null stream are queued one by one, never replayed)
     stream = side.cuda_stream
 
     ph = (C.c_uint64 * 8)()
