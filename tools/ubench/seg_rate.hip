@@ -3,6 +3,9 @@
 // BUF bytes, the segments' 16-byte chunks packed across the wave (lane l: chunk l, 64 + l, ...),
 // DEPTH parts in flight per wave (registers), then consumes the oldest.
 // Reports posting throughput (u32 entries/s) and the cycles per wave-instruction per CU.
+// `seg_rate c3`: only the C3 main launch's part shape (58 parts of ~434 postings per query over
+// ~10 lists: segments of ~43 entries; 6 waves per SIMD = 24 per CU) over 512 MB and 2 GB buffers,
+// one kernel per line so that rocprofv3 --pmc FETCH_SIZE gives each shape's fetch per posting.
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>
@@ -69,10 +72,26 @@ int run(const uint4* d, uint64_t n_chunks, uint32_t* sink, int waves_per_cu, con
     return 0;
 }
 
-int main() {
+int main(int argc, char** argv) {
     const uint64_t big = (512ull << 20) / 16, small = (2ull << 20) / 16;  // chunks, powers of two
     uint4* d;
     uint32_t* sink;
+    if (argc > 1 && argv[1][0] == 'c') {
+        const uint64_t huge = (2048ull << 20) / 16;
+        CHECK(hipMalloc(&d, huge * 16 + 4096));
+        CHECK(hipMalloc(&sink, 64));
+        CHECK(hipMemset(d, 1, huge * 16));
+        for (uint64_t n : {big, huge}) {
+            const char* tag = n == big ? "512MB" : "2GB";
+            run<10, 43, 1>(d, n, sink, 24, tag);
+            run<10, 43, 2>(d, n, sink, 24, tag);
+            run<12, 36, 1>(d, n, sink, 24, tag);
+            run<8, 54, 1>(d, n, sink, 24, tag);
+            run<10, 86, 1>(d, n, sink, 24, tag);
+            run<10, 128, 1>(d, n, sink, 24, tag);
+        }
+        return 0;
+    }
     CHECK(hipMalloc(&d, big * 16 + 4096));
     CHECK(hipMalloc(&sink, 64));
     CHECK(hipMemset(d, 1, big * 16));
