@@ -51,10 +51,10 @@ __global__ __launch_bounds__(64) void k_seg(const uint4* __restrict__ src, uint3
 }
 
 template <int NSEG, int SEGLEN, int DEPTH>
-int run(const uint4* d, uint64_t n_chunks, uint32_t* sink, int waves_per_cu, const char* tag) {
+int run(const uint4* d, uint64_t n_chunks, uint32_t* sink, int waves_per_cu, const char* tag, int reps = 64) {
     constexpr int CH = (SEGLEN + 3) / 4 + 1;
     constexpr int ROUNDS = (NSEG * CH + 63) / 64;
-    const int blocks = 256 * waves_per_cu, iters = 64 / DEPTH;
+    const int blocks = 256 * waves_per_cu, iters = reps / DEPTH;
     hipEvent_t a, b;
     hipEventCreate(&a); hipEventCreate(&b);
     k_seg<NSEG, SEGLEN, DEPTH, ROUNDS><<<blocks, 64>>>(d, (uint32_t)(n_chunks - 1), 2, sink);
@@ -83,12 +83,17 @@ int main(int argc, char** argv) {
         CHECK(hipMemset(d, 1, huge * 16));
         for (uint64_t n : {big, huge}) {
             const char* tag = n == big ? "512MB" : "2GB";
-            run<10, 43, 1>(d, n, sink, 24, tag);
-            run<10, 43, 2>(d, n, sink, 24, tag);
-            run<12, 36, 1>(d, n, sink, 24, tag);
-            run<8, 54, 1>(d, n, sink, 24, tag);
-            run<10, 86, 1>(d, n, sink, 24, tag);
-            run<10, 128, 1>(d, n, sink, 24, tag);
+            // the part shape of the main launch at its occupancy (24 waves per CU) ...
+            run<10, 43, 1>(d, n, sink, 24, tag, 256);
+            run<10, 43, 2>(d, n, sink, 24, tag, 256);
+            run<12, 36, 1>(d, n, sink, 24, tag, 256);
+            run<8, 54, 1>(d, n, sink, 24, tag, 256);
+            // ... and parts twice as long, which need twice the LDS sketch: 12 or 16 waves per CU
+            run<10, 86, 1>(d, n, sink, 24, tag, 256);
+            run<10, 86, 1>(d, n, sink, 16, tag, 256);
+            run<10, 86, 1>(d, n, sink, 12, tag, 256);
+            run<10, 86, 2>(d, n, sink, 12, tag, 256);
+            run<10, 128, 1>(d, n, sink, 24, tag, 256);
         }
         return 0;
     }
